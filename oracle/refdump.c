@@ -1,0 +1,260 @@
+/*
+ * refdump.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Golden-vector harness for the compiled reference (oracle/_ref/libswmm5_ref.so).
+ * It drives the reference's own public API (swmm_open/start/step/end/close,
+ * src/solver/swmm5.c:256-682) and, because the reference library exports its
+ * global object arrays (src/solver/globals.h:151-169), reads full-precision
+ * fp64 state after swmm_start and after every swmm_step.  Nothing in the
+ * reference is modified; the harness only reads.
+ *
+ * Output: a "SWDUMP1" record file: repeated records of
+ *     char name[48]; char dtype ('d' = f64, 'i' = i32); int64 count; data
+ * Per-step arrays are written as one record per field with count = S * N
+ * (row-major [step][object]).  Reader: tests/_dumpio.py.
+ *
+ * usage: refdump in.inp out.rpt out.out dump.bin [maxSteps] [every]
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#define  EXTERN extern
+#include "headers.h"
+#include "swmm5.h"
+
+static FILE* F;
+
+static void rec(const char* name, char dt, long long n, const void* data)
+{
+    char nm[48];
+    memset(nm, 0, sizeof nm);
+    strncpy(nm, name, 47);
+    fwrite(nm, 1, 48, F);
+    fwrite(&dt, 1, 1, F);
+    fwrite(&n, sizeof n, 1, F);
+    fwrite(data, dt == 'd' ? 8 : 4, (size_t)n, F);
+}
+
+typedef struct { char name[48]; char dt; int per; int nobj; double* d; int* i; long long used; long long cap; } Series;
+#define MAXSER 64
+static Series Ser[MAXSER];
+static int NSer = 0;
+
+static Series* ser(const char* name, char dt, int nobj)
+{
+    int k;
+    for (k = 0; k < NSer; k++) if (!strcmp(Ser[k].name, name)) return &Ser[k];
+    Series* s = &Ser[NSer++];
+    memset(s, 0, sizeof *s);
+    strncpy(s->name, name, 47);
+    s->dt = dt; s->nobj = nobj;
+    return s;
+}
+static void pushd(const char* name, int n, double (*get)(int))
+{
+    Series* s = ser(name, 'd', n);
+    if (s->used + n > s->cap) { s->cap = (s->used + n) * 2 + 64; s->d = realloc(s->d, s->cap * 8); }
+    for (int k = 0; k < n; k++) s->d[s->used + k] = get(k);
+    s->used += n;
+}
+static void pushi(const char* name, int n, int (*get)(int))
+{
+    Series* s = ser(name, 'i', n);
+    if (s->used + n > s->cap) { s->cap = (s->used + n) * 2 + 64; s->i = realloc(s->i, s->cap * 4); }
+    for (int k = 0; k < n; k++) s->i[s->used + k] = get(k);
+    s->used += n;
+}
+
+/* ---- accessors ---------------------------------------------------------- */
+#define ND(f) static double nd_##f(int j) { return Node[j].f; }
+#define NI(f) static int    ni_##f(int j) { return (int)Node[j].f; }
+#define LD(f) static double ld_##f(int j) { return Link[j].f; }
+#define LI(f) static int    li_##f(int j) { return (int)Link[j].f; }
+#define XD(f) static double xd_##f(int j) { return Link[j].xsect.f; }
+#define XI(f) static int    xi_##f(int j) { return (int)Link[j].xsect.f; }
+#define CD(f) static double cd_##f(int j) { return Link[j].type == CONDUIT ? Conduit[Link[j].subIndex].f : 0.0; }
+#define CI(f) static int    ci_##f(int j) { return Link[j].type == CONDUIT ? (int)Conduit[Link[j].subIndex].f : 0; }
+
+ND(invertElev) ND(initDepth) ND(fullDepth) ND(surDepth) ND(pondedArea) ND(crownElev)
+ND(fullVolume) ND(newDepth) ND(oldDepth) ND(newVolume) ND(oldVolume) ND(inflow)
+ND(outflow) ND(overflow) ND(newLatFlow) ND(oldLatFlow) ND(losses) ND(oldNetInflow)
+ND(oldFlowInflow)
+NI(type) NI(degree)
+static int ni_outfallType(int j) { return Node[j].type == OUTFALL ? Outfall[Node[j].subIndex].type : -1; }
+static int ni_outfallFlap(int j) { return Node[j].type == OUTFALL ? Outfall[Node[j].subIndex].hasFlapGate : 0; }
+static double nd_fixedStage(int j) { return Node[j].type == OUTFALL ? Outfall[Node[j].subIndex].fixedStage : 0.0; }
+
+LD(offset1) LD(offset2) LD(q0) LD(qLimit) LD(cLossInlet) LD(cLossOutlet) LD(cLossAvg)
+LD(seepRate) LD(newFlow) LD(oldFlow) LD(newDepth) LD(oldDepth) LD(newVolume) LD(oldVolume)
+LD(froude) LD(dqdh) LD(surfArea1) LD(surfArea2) LD(setting) LD(qFull)
+LI(type) LI(node1) LI(node2) LI(hasFlapGate) LI(direction) LI(flowClass) LI(bypassed)
+LI(normalFlow) LI(inletControl)
+XD(yFull) XD(wMax) XD(ywMax) XD(aFull) XD(rFull) XD(sFull) XD(sMax) XD(yBot) XD(aBot)
+XD(sBot) XD(rBot)
+XI(type) XI(culvertCode)
+CD(length) CD(roughness) CD(modLength) CD(roughFactor) CD(slope) CD(beta) CD(qMax)
+CD(a1) CD(a2) CD(q1) CD(q2) CD(evapLossRate) CD(seepLossRate)
+CI(barrels) CI(hasLosses) CI(fullState) CI(capacityLimited) CI(superCritical)
+
+static int NP = 0;
+static double nq_buf(int j) { return 0.0; }
+
+static void pushState(void)
+{
+    int nn = Nobjects[NODE], nl = Nobjects[LINK], p;
+    pushd("s.node.newDepth", nn, nd_newDepth);
+    pushd("s.node.newVolume", nn, nd_newVolume);
+    pushd("s.node.inflow", nn, nd_inflow);
+    pushd("s.node.outflow", nn, nd_outflow);
+    pushd("s.node.overflow", nn, nd_overflow);
+    pushd("s.node.newLatFlow", nn, nd_newLatFlow);
+    pushd("s.node.losses", nn, nd_losses);
+    pushd("s.node.oldNetInflow", nn, nd_oldNetInflow);
+    pushd("s.link.newFlow", nl, ld_newFlow);
+    pushd("s.link.newDepth", nl, ld_newDepth);
+    pushd("s.link.newVolume", nl, ld_newVolume);
+    pushd("s.link.froude", nl, ld_froude);
+    pushd("s.link.dqdh", nl, ld_dqdh);
+    pushd("s.link.surfArea1", nl, ld_surfArea1);
+    pushd("s.link.surfArea2", nl, ld_surfArea2);
+    pushd("s.link.a1", nl, cd_a1);
+    pushd("s.link.q1", nl, cd_q1);
+    pushi("s.link.flowClass", nl, li_flowClass);
+    pushi("s.link.fullState", nl, ci_fullState);
+    pushi("s.link.normalFlow", nl, li_normalFlow);
+    pushi("s.link.capacityLimited", nl, ci_capacityLimited);
+    pushi("s.link.bypassed", nl, li_bypassed);
+    for (p = 0; p < NP; p++)
+    {
+        char nm[48];
+        Series* s;
+        int j;
+        snprintf(nm, sizeof nm, "s.node.qual%d", p);
+        s = ser(nm, 'd', nn);
+        if (s->used + nn > s->cap) { s->cap = (s->used + nn) * 2 + 64; s->d = realloc(s->d, s->cap * 8); }
+        for (j = 0; j < nn; j++) s->d[s->used + j] = Node[j].newQual[p];
+        s->used += nn;
+        snprintf(nm, sizeof nm, "s.link.qual%d", p);
+        s = ser(nm, 'd', nl);
+        if (s->used + nl > s->cap) { s->cap = (s->used + nl) * 2 + 64; s->d = realloc(s->d, s->cap * 8); }
+        for (j = 0; j < nl; j++) s->d[s->used + j] = Link[j].newQual[p];
+        s->used += nl;
+    }
+    (void)nq_buf;
+}
+
+static void writeStatic(void)
+{
+    int nn = Nobjects[NODE], nl = Nobjects[LINK], j;
+    int* ib = malloc(sizeof(int) * (nn > nl ? nn : nl) + 64);
+    double* db = malloc(sizeof(double) * (nn > nl ? nn : nl) + 64);
+    int counts[4] = { nn, nl, Nobjects[POLLUT], 0 };
+    double opt[16];
+    int iopt[16];
+#define WN_D(f) for (j = 0; j < nn; j++) db[j] = nd_##f(j); rec("node." #f, 'd', nn, db);
+#define WN_I(f) for (j = 0; j < nn; j++) ib[j] = ni_##f(j); rec("node." #f, 'i', nn, ib);
+#define WL_D(p, f) for (j = 0; j < nl; j++) db[j] = p##_##f(j); rec("link." #f, 'd', nl, db);
+#define WL_I(p, f) for (j = 0; j < nl; j++) ib[j] = p##_##f(j); rec("link." #f, 'i', nl, ib);
+#define WX_I(f) for (j = 0; j < nl; j++) ib[j] = xi_##f(j); rec("link.x" #f, 'i', nl, ib);
+    rec("counts", 'i', 4, counts);
+    opt[0] = RouteStep; opt[1] = CourantFactor; opt[2] = MinRouteStep; opt[3] = MinSurfArea;
+    opt[4] = HeadTol; opt[5] = CrownCutoff; opt[6] = LengtheningStep; opt[7] = Evap.rate;
+    opt[8] = TotalDuration; opt[9] = ReportStep; opt[10] = StartDateTime; opt[11] = 0;
+    rec("opt.d", 'd', 12, opt);
+    iopt[0] = MaxTrials; iopt[1] = SurchargeMethod; iopt[2] = InertDamping; iopt[3] = NormalFlowLtd;
+    iopt[4] = AllowPonding; iopt[5] = RouteModel; iopt[6] = ForceMainEqn; iopt[7] = FlowUnits;
+    iopt[8] = UnitSystem; iopt[9] = IgnoreQuality; iopt[10] = 0; iopt[11] = 0;
+    rec("opt.i", 'i', 12, iopt);
+    if (Nobjects[POLLUT] > 0)
+    {
+        double pk[64], pc[64], pi0[64];
+        for (j = 0; j < Nobjects[POLLUT] && j < 64; j++)
+        { pk[j] = Pollut[j].kDecay; pc[j] = Pollut[j].dwfConcen; pi0[j] = Pollut[j].initConcen; }
+        rec("pollut.kDecay", 'd', Nobjects[POLLUT], pk);
+        rec("pollut.dwfConcen", 'd', Nobjects[POLLUT], pc);
+        rec("pollut.initConcen", 'd', Nobjects[POLLUT], pi0);
+    }
+    WN_I(type) WN_I(degree) WN_I(outfallType) WN_I(outfallFlap)
+    WN_D(invertElev) WN_D(initDepth) WN_D(fullDepth) WN_D(surDepth) WN_D(pondedArea)
+    WN_D(crownElev) WN_D(fullVolume) WN_D(fixedStage)
+    WN_D(newDepth) WN_D(oldDepth) WN_D(newVolume) WN_D(oldVolume) WN_D(inflow) WN_D(outflow)
+    WN_D(newLatFlow) WN_D(oldLatFlow) WN_D(oldNetInflow) WN_D(oldFlowInflow) WN_D(overflow)
+    WL_I(li, type) WL_I(li, node1) WL_I(li, node2) WL_I(li, hasFlapGate) WL_I(li, direction)
+    WL_I(li, flowClass) WX_I(type) WL_I(xi, culvertCode)
+    WL_I(ci, barrels) WL_I(ci, hasLosses) WL_I(ci, superCritical)
+    WL_D(ld, offset1) WL_D(ld, offset2) WL_D(ld, q0) WL_D(ld, qLimit) WL_D(ld, cLossInlet)
+    WL_D(ld, cLossOutlet) WL_D(ld, cLossAvg) WL_D(ld, seepRate) WL_D(ld, setting) WL_D(ld, qFull)
+    WL_D(xd, yFull) WL_D(xd, wMax) WL_D(xd, ywMax) WL_D(xd, aFull) WL_D(xd, rFull) WL_D(xd, sFull)
+    WL_D(xd, sMax) WL_D(xd, yBot) WL_D(xd, aBot) WL_D(xd, sBot) WL_D(xd, rBot)
+    WL_D(cd, length) WL_D(cd, roughness) WL_D(cd, modLength) WL_D(cd, roughFactor)
+    WL_D(cd, slope) WL_D(cd, beta) WL_D(cd, qMax)
+    WL_D(ld, newFlow) WL_D(ld, oldFlow) WL_D(ld, newDepth) WL_D(ld, oldDepth) WL_D(ld, newVolume)
+    WL_D(ld, oldVolume) WL_D(cd, a1) WL_D(cd, a2) WL_D(cd, q1) WL_D(cd, q2)
+    free(ib);
+    free(db);
+}
+
+int main(int argc, char** argv)
+{
+    double elapsed = 0.0;
+    int maxSteps = 0, every = 1, step = 0, k;
+    double* dts = NULL;
+    double* tms = NULL;
+    int nrec = 0, cap = 0;
+    float e1, e2, e3;
+    if (argc < 5)
+    {
+        fprintf(stderr, "usage: refdump in.inp out.rpt out.out dump.bin [maxSteps] [every]\n");
+        return 2;
+    }
+    if (argc > 5) maxSteps = atoi(argv[5]);
+    if (argc > 6) every = atoi(argv[6]);
+    if (every < 1) every = 1;
+    if (swmm_open(argv[1], argv[2], argv[3])) { fprintf(stderr, "swmm_open failed %d\n", ErrorCode); return 1; }
+    if (swmm_start(1)) { fprintf(stderr, "swmm_start failed %d\n", ErrorCode); return 1; }
+    NP = Nobjects[POLLUT];
+    F = fopen(argv[4], "wb");
+    if (!F) return 1;
+    fwrite("SWDUMP1\0", 1, 8, F);
+    writeStatic();
+    do
+    {
+        double told = NewRoutingTime;
+        swmm_step(&elapsed);
+        step++;
+        if (step % every == 0 || elapsed <= 0.0)
+        {
+            if (nrec + 1 > cap) { cap = 2 * cap + 64; dts = realloc(dts, cap * 8); tms = realloc(tms, cap * 8); }
+            dts[nrec] = (NewRoutingTime - told) / 1000.0;
+            tms[nrec] = NewRoutingTime;
+            nrec++;
+            pushState();
+        }
+        if (maxSteps > 0 && step >= maxSteps) break;
+    } while (elapsed > 0.0 && !ErrorCode);
+    rec("s.dt", 'd', nrec, dts);
+    rec("s.time", 'd', nrec, tms);
+    {
+        int ev[2] = { every, step };
+        rec("s.every", 'i', 2, ev);
+    }
+    for (k = 0; k < NSer; k++)
+    {
+        if (Ser[k].dt == 'd') rec(Ser[k].name, 'd', Ser[k].used, Ser[k].d);
+        else rec(Ser[k].name, 'i', Ser[k].used, Ser[k].i);
+    }
+    {
+        int nc[2] = { (int)NonConvergeCount, (int)TotalStepCount };
+        rec("run.counts", 'i', 2, nc);
+    }
+    swmm_end();
+    swmm_getMassBalErr(&e1, &e2, &e3);
+    {
+        double me[3] = { e1, e2, e3 };
+        rec("run.massbal", 'd', 3, me);
+    }
+    fclose(F);
+    swmm_report();
+    swmm_close();
+    return 0;
+}

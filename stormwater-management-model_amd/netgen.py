@@ -1,0 +1,267 @@
+"""Synthetic SWMM .inp writers for the dynamic-wave routing workloads.
+
+Two networks, both plain EPA-SWMM 5.2 input files (so the reference solver and
+this framework read the very same bytes):
+
+* ``write_grid``    -- the Manhattan grid of SURVEY.md section 8(d): nx x ny
+  junctions ``J{i}_{j}``, conduits to (i+1, j) and (i, j+1) numbered row-major
+  (+i link first, then +j link), one 8-ft outlet conduit to a FREE outfall
+  ``OUT``, constant DWF at every junction, optional pollutants.  Conduit
+  numbering fixes the link-index order that the reference's serial node sums
+  follow (src/solver/dynwave.c:398-411), so it is part of the contract.
+* ``write_example`` -- a small authored DYNWAVE network (about 20 conduits)
+  exercising mixed shapes, invert offsets (UP/DN_CRITICAL flow classes,
+  dwflow.c:297-413), an adverse-slope conduit (reversed under DW,
+  link.c:1082-1087), one FREE and one FIXED outfall (node.c:1413-1492),
+  DWF and an [INFLOWS] hydrograph.
+
+Grid sizes used by the benchmarks: 224^2 -> 99,905 conduits, 707^2 ->
+998,285, 1414^2 -> 3,995,965.
+"""
+from __future__ import annotations
+
+import io
+import os
+
+__all__ = ["write_grid", "write_example", "grid_counts"]
+
+
+def grid_counts(nx: int, ny: int) -> tuple[int, int]:
+    """(nodes, conduits) of an nx x ny grid including the outfall and outlet."""
+    return nx * ny + 1, 2 * nx * ny - nx - ny + 1
+
+
+def _options(f, *, route_step, variable_step, end_time, report_step, threads,
+             min_surfarea=None, extra=()):
+    f.write("[OPTIONS]\n")
+    f.write("FLOW_UNITS CFS\nINFILTRATION HORTON\nFLOW_ROUTING DYNWAVE\n")
+    f.write("START_DATE 01/01/2020\nSTART_TIME 00:00:00\n")
+    f.write("REPORT_START_DATE 01/01/2020\nREPORT_START_TIME 00:00:00\n")
+    f.write("END_DATE 01/01/2020\nEND_TIME %s\n" % end_time)
+    f.write("REPORT_STEP %s\n" % report_step)
+    f.write("WET_STEP 00:05:00\nDRY_STEP 01:00:00\n")
+    f.write("ROUTING_STEP %s\n" % route_step)
+    f.write("VARIABLE_STEP %s\n" % variable_step)
+    f.write("THREADS %d\n" % threads)
+    if min_surfarea is not None:
+        f.write("MIN_SURFAREA %s\n" % min_surfarea)
+    for line in extra:
+        f.write(line + "\n")
+    f.write("\n")
+
+
+def write_grid(path: str, nx: int, ny: int, *, diameter: float = 1.5,
+               q: float = 0.02, route_step: float = 1.0,
+               variable_step: float = 0.0, end_time: str = "06:00:00",
+               report_step: str = "00:15:00", pollutants: int = 0,
+               threads: int = 1, report_all: bool | None = None,
+               extra_options=()) -> tuple[int, int]:
+    """Write the SURVEY.md 8(d) Manhattan grid; returns (nodes, conduits)."""
+    if report_all is None:
+        report_all = nx * ny <= 2500
+    slope_drop = 0.002 * 400.0
+    buf = io.StringIO()
+    w = buf.write
+    w("[TITLE]\nSynthetic %dx%d Manhattan grid (DYNWAVE)\n\n" % (nx, ny))
+    _options(buf, route_step=route_step, variable_step=variable_step,
+             end_time=end_time, report_step=report_step, threads=threads,
+             extra=extra_options)
+    if pollutants:
+        conc = [5.0, 10.0, 15.0, 20.0, 25.0, 30.0]
+        decay = [0.0, 0.1, 0.2, 0.3, 0.4, 0.5]
+        w("[POLLUTANTS]\n")
+        for p in range(pollutants):
+            w("P%d MG/L 0 0 0 %g NO * 0 %g 0\n" % (p, decay[p], conc[p]))
+        w("\n")
+    w("[JUNCTIONS]\n")
+    for i in range(nx):
+        for j in range(ny):
+            w("J%d_%d %.4f 10 0 0 0\n" % (i, j, 100.0 - slope_drop * (i + j)))
+    out_elev = 100.0 - slope_drop * (nx - 1 + ny - 1) - slope_drop
+    w("\n[OUTFALLS]\nOUT %.4f FREE NO\n\n" % out_elev)
+    w("[CONDUITS]\n")
+    k = 0
+    for i in range(nx):
+        for j in range(ny):
+            if i + 1 < nx:
+                w("C%d J%d_%d J%d_%d 400 0.013 0 0 0 0\n" % (k, i, j, i + 1, j))
+                k += 1
+            if j + 1 < ny:
+                w("C%d J%d_%d J%d_%d 400 0.013 0 0 0 0\n" % (k, i, j, i, j + 1))
+                k += 1
+    w("C%d J%d_%d OUT 400 0.013 0 0 0 0\n\n" % (k, nx - 1, ny - 1))
+    nlinks = k + 1
+    w("[XSECTIONS]\n")
+    for c in range(nlinks - 1):
+        w("C%d CIRCULAR %g 0 0 0 1\n" % (c, diameter))
+    w("C%d CIRCULAR 8 0 0 0 1\n\n" % (nlinks - 1))
+    w("[DWF]\n")
+    for i in range(nx):
+        for j in range(ny):
+            w("J%d_%d FLOW %g\n" % (i, j, q))
+            for p in range(pollutants):
+                w("J%d_%d P%d %g\n" % (i, j, p, [5.0, 10.0, 15.0, 20.0, 25.0, 30.0][p]))
+    w("\n[REPORT]\nINPUT NO\nCONTROLS NO\n")
+    if report_all:
+        w("NODES ALL\nLINKS ALL\n")
+    w("\n")
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    with open(path, "w") as f:
+        f.write(buf.getvalue())
+    return nx * ny + 1, nlinks
+
+
+_EXAMPLE = """[TITLE]
+Authored DYNWAVE example: mixed shapes, offsets, adverse slope, 2 outfalls
+
+[OPTIONS]
+FLOW_UNITS CFS
+INFILTRATION HORTON
+FLOW_ROUTING DYNWAVE
+START_DATE 01/01/2020
+START_TIME 00:00:00
+REPORT_START_DATE 01/01/2020
+REPORT_START_TIME 00:00:00
+END_DATE 01/01/2020
+END_TIME {end_time}
+REPORT_STEP 00:05:00
+WET_STEP 00:05:00
+DRY_STEP 01:00:00
+ROUTING_STEP {route_step}
+VARIABLE_STEP {variable_step}
+INERTIAL_DAMPING PARTIAL
+NORMAL_FLOW_LIMITED BOTH
+THREADS 1
+{pollut_opt}
+[POLLUTANTS]
+{pollut}
+[JUNCTIONS]
+;;Name Elev MaxDepth InitDepth SurDepth Aponded
+N1  120.0  8  0.0  0  0
+N2  118.5  8  0.5  0  0
+N3  117.0  9  0    0  0
+N4  115.4  9  0    0  0
+N5  119.0  7  0    0  0
+N6  117.6  7  0    0  0
+N7  114.0  10 0    0  0
+N8  112.5  10 0    0  0
+N9  111.0  10 0    0  0
+N10 113.2  6  0    0  0
+N11 110.1  10 0    0  0
+N12 108.7  10 0    0  0
+N13 109.9  6  0    0  0
+N14 107.2  10 0    2  0
+N15 105.5  12 0    0  0
+
+[OUTFALLS]
+O1  103.0  FREE   NO
+O2  104.0  FIXED  105.2  NO
+
+[CONDUITS]
+;;Name From To Length N InOffset OutOffset InitFlow MaxFlow
+C1  N1  N2  400  0.013  0    0    0  0
+C2  N2  N3  400  0.013  0    0.5  0  0
+C3  N3  N4  450  0.013  0    0    0  0
+C4  N5  N6  350  0.015  0    0    0  0
+C5  N6  N4  420  0.015  1.0  0    0  0
+C6  N4  N7  500  0.013  0    0    0  0
+C7  N7  N8  500  0.013  0    0    0  0
+C8  N8  N9  480  0.013  0    0    0  0
+C9  N10 N8  300  0.014  0.5  0    0  0
+C10 N9  N11 520  0.013  0    0    0  0
+C11 N11 N12 400  0.013  0    0    0  0
+C12 N13 N11 380  0.020  0    0.3  0  0
+C13 N12 N14 450  0.013  0    0    0  0
+C14 N14 N15 400  0.013  0    0    0  0
+C15 N15 O1  300  0.013  0    0    0  0
+C16 N14 O2  350  0.016  0.8  0    0  0
+C17 N7  N10 260  0.013  0    0    0  0
+C18 N12 N13 250  0.015  0    0    0  0
+C19 N3  N6  300  0.013  0    0    0  0
+C20 N9  N13 300  0.013  0    0    0  0
+
+[XSECTIONS]
+;;Link Shape Geom1 Geom2 Geom3 Geom4 Barrels
+C1  CIRCULAR     1.5  0    0    0  1
+C2  CIRCULAR     1.5  0    0    0  1
+C3  CIRCULAR     2.0  0    0    0  1
+C4  RECT_OPEN    2.0  3.0  0    0  1
+C5  RECT_OPEN    2.0  3.0  0    0  1
+C6  CIRCULAR     2.5  0    0    0  1
+C7  RECT_CLOSED  3.0  3.0  0    0  1
+C8  RECT_CLOSED  3.0  3.0  0    0  2
+C9  TRAPEZOIDAL  2.0  2.0  1.5  1.5 1
+C10 CIRCULAR     3.0  0    0    0  1
+C11 CIRCULAR     3.0  0    0    0  1
+C12 TRIANGULAR   2.0  4.0  0    0  1
+C13 CIRCULAR     3.5  0    0    0  1
+C14 TRAPEZOIDAL  4.0  4.0  2.0  2.0 1
+C15 CIRCULAR     4.0  0    0    0  1
+C16 RECT_OPEN    3.0  4.0  0    0  1
+C17 CIRCULAR     1.0  0    0    0  1
+C18 CIRCULAR     1.25 0    0    0  2
+C19 CIRCULAR     1.0  0    0    0  1
+C20 TRIANGULAR   2.5  5.0  0    0  1
+
+[LOSSES]
+;;Link Inlet Outlet Average FlapGate
+C6   0.5  0.3  0.1  NO
+C13  0.2  0.2  0.0  NO
+
+[INFLOWS]
+;;Node Constituent TimeSeries Type Mfactor Sfactor Baseline Pattern
+N1   FLOW  HYD1  FLOW  1.0  1.0  0.5
+N5   FLOW  HYD2  FLOW  1.0  1.0
+{qual_inflow}
+[TIMESERIES]
+;;Name Date Time Value
+HYD1  0:00  0.0
+HYD1  0:15  4.0
+HYD1  0:30  9.0
+HYD1  1:00  6.0
+HYD1  1:30  2.0
+HYD1  3:00  0.0
+HYD2  0:00  0.0
+HYD2  0:20  3.0
+HYD2  0:50  5.5
+HYD2  1:40  1.0
+HYD2  2:30  0.0
+
+[DWF]
+;;Node Constituent Baseline
+N1   FLOW  0.2
+N2   FLOW  0.15
+N3   FLOW  0.1
+N5   FLOW  0.12
+N8   FLOW  0.3
+N10  FLOW  0.05
+N13  FLOW  0.08
+{qual_dwf}
+[REPORT]
+INPUT NO
+CONTROLS NO
+NODES ALL
+LINKS ALL
+"""
+
+
+def write_example(path: str, *, route_step: float = 5.0,
+                  variable_step: float = 0.0, end_time: str = "04:00:00",
+                  pollutants: bool = False) -> None:
+    """Write the authored Example network (see module docstring)."""
+    if pollutants:
+        pollut = ("TSS MG/L 0 0 0 0.5 NO * 0 20 0\n"
+                  "BOD MG/L 0 0 0 0 NO * 0 10 0\n")
+        qual_inflow = "N1   TSS  HYD1  CONCEN  1.0  1.0  30\n"
+        qual_dwf = "N8   BOD  25\n"
+    else:
+        pollut = qual_inflow = qual_dwf = ""
+    txt = _EXAMPLE.format(route_step=route_step, variable_step=variable_step,
+                          end_time=end_time, pollut=pollut,
+                          qual_inflow=qual_inflow, qual_dwf=qual_dwf,
+                          pollut_opt="")
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    with open(path, "w") as f:
+        f.write(txt)
