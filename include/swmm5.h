@@ -1,0 +1,152 @@
+/*
+ * swmm5.h -- public C ABI of the MI355X dynamic-wave routing engine.
+ *
+ * Drop-in for the reference engine's API: every entry point below has the
+ * name, argument meaning, return convention and enum values of the reference
+ * header src/solver/include/swmm5.h (declarations at swmm5.h:129-151, enums at
+ * swmm5.h:40-127), so a caller built against the reference (runswmm, pyswmm-
+ * style ctypes wrappers, cgo/JNI stubs -- see INTEGRATION.md) links against
+ * libswmm5_mi355x.so unchanged.  Plain C linkage, plain pointers and sizes.
+ *
+ * Semantics follow the reference (src/solver/swmm5.c):
+ *   swmm_open   swmm5.c:256   parse + validate (host only, no GPU touched)
+ *   swmm_start  swmm5.c:314   initial state, upload to HBM, output file open
+ *   swmm_step   swmm5.c:410   one routing step; *elapsedTime in days, 0 at end
+ *   swmm_stride swmm5.c:466   advance strideStep seconds
+ *   swmm_end    swmm5.c:618   final records, mass balance, statistics
+ *   swmm_report swmm5.c:664   write report file
+ *   swmm_close  swmm5.c:682   release everything
+ * Error codes are the reference's (src/solver/error.h); a set error code is
+ * sticky and returned by every later call, as in the reference.
+ * Single project per process, not thread-safe (same contract as the reference).
+ */
+#ifndef SWMM5_MI355X_PUBLIC_H
+#define SWMM5_MI355X_PUBLIC_H
+
+#define DLLEXPORT __attribute__((visibility("default")))
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    swmm_GAGE     = 0,
+    swmm_SUBCATCH = 1,
+    swmm_NODE     = 2,
+    swmm_LINK     = 3,
+    swmm_SYSTEM   = 100
+} swmm_Object;
+
+typedef enum {
+    swmm_JUNCTION = 0,
+    swmm_OUTFALL  = 1,
+    swmm_STORAGE  = 2,
+    swmm_DIVIDER  = 3
+} swmm_NodeType;
+
+typedef enum {
+    swmm_CONDUIT = 0,
+    swmm_PUMP    = 1,
+    swmm_ORIFICE = 2,
+    swmm_WEIR    = 3,
+    swmm_OUTLET  = 4
+} swmm_LinkType;
+
+typedef enum {
+    swmm_GAGE_RAINFALL = 100
+} swmm_GageProperty;
+
+typedef enum {
+    swmm_SUBCATCH_AREA      = 200,
+    swmm_SUBCATCH_RAINGAGE  = 201,
+    swmm_SUBCATCH_RAINFALL  = 202,
+    swmm_SUBCATCH_EVAP      = 203,
+    swmm_SUBCATCH_INFIL     = 204,
+    swmm_SUBCATCH_RUNOFF    = 205,
+    swmm_SUBCATCH_RPTFLAG   = 206
+} swmm_SubcatchProperty;
+
+typedef enum {
+    swmm_NODE_TYPE     = 300,
+    swmm_NODE_ELEV     = 301,
+    swmm_NODE_MAXDEPTH = 302,
+    swmm_NODE_DEPTH    = 303,
+    swmm_NODE_HEAD     = 304,
+    swmm_NODE_VOLUME   = 305,
+    swmm_NODE_LATFLOW  = 306,
+    swmm_NODE_INFLOW   = 307,
+    swmm_NODE_OVERFLOW = 308,
+    swmm_NODE_RPTFLAG  = 309
+} swmm_NodeProperty;
+
+typedef enum {
+    swmm_LINK_TYPE       = 400,
+    swmm_LINK_NODE1      = 401,
+    swmm_LINK_NODE2      = 402,
+    swmm_LINK_LENGTH     = 403,
+    swmm_LINK_SLOPE      = 404,
+    swmm_LINK_FULLDEPTH  = 405,
+    swmm_LINK_FULLFLOW   = 406,
+    swmm_LINK_SETTING    = 407,
+    swmm_LINK_TIMEOPEN   = 408,
+    swmm_LINK_TIMECLOSED = 409,
+    swmm_LINK_FLOW       = 410,
+    swmm_LINK_DEPTH      = 411,
+    swmm_LINK_VELOCITY   = 412,
+    swmm_LINK_TOPWIDTH   = 413,
+    swmm_LINK_RPTFLAG    = 414
+} swmm_LinkProperty;
+
+typedef enum {
+    swmm_STARTDATE    = 0,
+    swmm_CURRENTDATE  = 1,
+    swmm_ELAPSEDTIME  = 2,
+    swmm_ROUTESTEP    = 3,
+    swmm_MAXROUTESTEP = 4,
+    swmm_REPORTSTEP   = 5,
+    swmm_TOTALSTEPS   = 6,
+    swmm_NOREPORT     = 7,
+    swmm_FLOWUNITS    = 8
+} swmm_SystemProperty;
+
+typedef enum {
+    swmm_CFS = 0,
+    swmm_GPM = 1,
+    swmm_MGD = 2,
+    swmm_CMS = 3,
+    swmm_LPS = 4,
+    swmm_MLD = 5
+} swmm_FlowUnitsProperty;
+
+/* lifecycle -- reference swmm5.h:129-136 */
+int    DLLEXPORT swmm_run(const char *f1, const char *f2, const char *f3);
+int    DLLEXPORT swmm_open(const char *f1, const char *f2, const char *f3);
+int    DLLEXPORT swmm_start(int saveFlag);
+int    DLLEXPORT swmm_step(double *elapsedTime);
+int    DLLEXPORT swmm_stride(int strideStep, double *elapsedTime);
+int    DLLEXPORT swmm_end(void);
+int    DLLEXPORT swmm_report(void);
+int    DLLEXPORT swmm_close(void);
+
+/* diagnostics -- reference swmm5.h:138-141 */
+int    DLLEXPORT swmm_getMassBalErr(float *runoffErr, float *flowErr, float *qualErr);
+int    DLLEXPORT swmm_getVersion(void);
+int    DLLEXPORT swmm_getError(char *errMsg, int msgLen);
+int    DLLEXPORT swmm_getWarnings(void);
+
+/* object access -- reference swmm5.h:143-151 */
+int    DLLEXPORT swmm_getCount(int objType);
+void   DLLEXPORT swmm_getName(int objType, int index, char *name, int size);
+int    DLLEXPORT swmm_getIndex(int objType, const char *name);
+double DLLEXPORT swmm_getValue(int property, int index);
+void   DLLEXPORT swmm_setValue(int property, int index,  double value);
+double DLLEXPORT swmm_getSavedValue(int property, int index, int period);
+void   DLLEXPORT swmm_writeLine(const char *line);
+void   DLLEXPORT swmm_decodeDate(double date, int *year, int *month, int *day,
+                 int *hour, int *minute, int *second, int *dayOfWeek);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

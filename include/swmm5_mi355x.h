@@ -1,0 +1,64 @@
+/*
+ * swmm5_mi355x.h -- extension entry points of libswmm5_mi355x.so that have no
+ * counterpart in the reference API.  They exist for measurement, testing and
+ * the multi-GPU driver; a drop-in caller never needs them.
+ */
+#ifndef SWMM5_MI355X_EXT_H
+#define SWMM5_MI355X_EXT_H
+
+#include "swmm5.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Host-only start: builds the initial state exactly as swmm_start would
+ * (project_init + routing init, reference swmm5.c:345-393) but never touches
+ * the GPU.  Lets CPU-only tests compare parsing/validation/initialisation
+ * against the reference.  swmm_step is an error after this call. */
+int    DLLEXPORT swmmx_startHost(void);
+
+/* Write the engine's full-precision state (static parameters + current
+ * dynamic state, synchronised from HBM) as a SWDUMP1 record file, the format
+ * of oracle/refdump.c.  Returns 0 or an error code. */
+int    DLLEXPORT swmmx_exportState(const char *path);
+
+/* Copy one named fp64 state array (e.g. "node.newDepth", "link.newFlow")
+ * from the engine (device-synchronised) into dst[0..n).  Returns the number of
+ * elements copied or -1 if the name is unknown. */
+long   DLLEXPORT swmmx_getArray(const char *name, double *dst, long n);
+
+/* Overwrite one named fp64 state array (host mirror and HBM). */
+long   DLLEXPORT swmmx_setArray(const char *name, const double *src, long n);
+
+/* Run n routing steps back to back (same as n calls of swmm_step). */
+int    DLLEXPORT swmmx_runSteps(int n, double *elapsedTime);
+
+/* Counters: [0] total routing steps, [1] total Picard iterations,
+ * [2] non-converging steps, [3] Picard iterations of the last step,
+ * [4] true conduits, [5] nodes.  Synchronises with the device. */
+int    DLLEXPORT swmmx_getCounters(long long *out, int n);
+
+/* Device kernel timing (HIP events on the routing stream).  mode=1 enables,
+ * 0 disables; swmmx_getKernelTimes returns, per kernel class, the number of
+ * timed launches and their total milliseconds:
+ *   out[2*k] = launches, out[2*k+1] = ms;  k: 0 link momentum, 1 node update,
+ *   2 step end, 3 quality.  Returns the number of classes written. */
+int    DLLEXPORT swmmx_setTiming(int mode);
+int    DLLEXPORT swmmx_getKernelTimes(double *out, int n);
+
+/* Algorithmic bytes per launch of each kernel class for the current network
+ * (the byte model of DESIGN.md), same class order as above. */
+int    DLLEXPORT swmmx_getKernelBytes(double *out, int n);
+
+/* Name of the compute backend ("hip:gfx950:<device name>" or "none"). */
+int    DLLEXPORT swmmx_getBackend(char *buf, int size);
+
+/* Select the HIP device ordinal used by swmm_start (default 0 / LOCAL_RANK). */
+int    DLLEXPORT swmmx_setDevice(int ordinal);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,846 @@
+// api.cpp -- the C ABI (include/swmm5.h, include/swmm5_mi355x.h).
+//
+// Lifecycle and step driver restate the reference's supervisor
+// (src/solver/swmm5.c): swmm_open 256-310, swmm_start 314-407, swmm_step
+// 410-462 with execRouting 514-575 and saveResults 579-613, swmm_end 618-660,
+// swmm_close 682-702, getters/setters 842-1213.  The routing itself is
+// delegated to the HBM-resident Router (dw_kernels.hip); the host keeps a
+// lazily synchronised mirror of the state for getValue, report-time output
+// and the report file.  There is deliberately no CPU routing path: without a
+// HIP device swmm_start fails with ERR_SYSTEM.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "../../include/swmm5_mi355x.h"
+#include "output.h"
+#include "project.h"
+#include "router.h"
+#include "xsect.h"
+
+using namespace swx;
+
+namespace {
+
+struct Engine {
+    std::unique_ptr<Project> prj;
+    std::unique_ptr<Router> router;
+    OutFile out;
+    std::string inpPath, rptPath, outPath;
+    FILE* rpt = nullptr;
+    bool isOpen = false, isStarted = false, hostOnly = false, saveFlag = true;
+    bool mirrorValid = true;         // host mirror equals device state
+    int errorCode = 0;
+    std::string errorMsg;
+    double newRoutingTime = 0.0, oldRoutingTime = 0.0, reportTime = 0.0;
+    double routingDuration = 0.0, elapsedTime = 0.0;
+    long long totalStepCount = 0;
+    double flowError = 0.0, qualError = 0.0;
+    double flowTot[8] = {0};
+    double initStorage = 0.0, finalStorage = 0.0;
+    double sysStep[6] = {0};
+    double apiExtTouched = 0;
+    std::vector<double> apiExtInflow;
+    int device = -1;
+    bool constantInflow = true;
+};
+
+Engine* G = nullptr;
+int gDevice = -1;                    // swmmx_setDevice (survives swmm_open)
+
+int setErr(int code, const std::string& msg)
+{
+    if (G && !G->errorCode) {
+        G->errorCode = code;
+        G->errorMsg = msg;
+        if (G->rpt) fprintf(G->rpt, "\n  %s\n", msg.c_str());
+    }
+    return code;
+}
+
+int syncMirror()
+{
+    if (!G || !G->router || G->mirrorValid) return 0;
+    if (G->router->download(*G->prj)) return setErr(G->router->lastError(), G->router->lastErrorMsg());
+    G->mirrorValid = true;
+    return 0;
+}
+
+int defaultDevice()
+{
+    const char* s = getenv("LOCAL_RANK");
+    if (s) return atoi(s);
+    return 0;
+}
+
+void writeReportHeader()
+{
+    if (!G->rpt) return;
+    fprintf(G->rpt, "\n  EPA STORM WATER MANAGEMENT MODEL - VERSION 5.2 (Build 5.2.4)\n");
+    fprintf(G->rpt, "  --------------------------------------------------------------\n");
+    fprintf(G->rpt, "  MI355X dynamic-wave routing engine (libswmm5_mi355x)\n\n");
+    if (!G->prj->net.title.empty()) fprintf(G->rpt, "  %s\n\n", G->prj->net.title.c_str());
+}
+
+}  // namespace
+
+extern "C" {
+
+int DLLEXPORT swmm_open(const char* f1, const char* f2, const char* f3)
+{
+    delete G;
+    G = new Engine();
+    G->prj.reset(new Project());
+    if (!f1 || !f2 || !f3) return setErr(301, "ERROR 301: files share same names.");
+    G->inpPath = f1; G->rptPath = f2; G->outPath = f3;
+    if (!strcasecmp(f1, f2) || !strcasecmp(f1, f3) || !strcasecmp(f2, f3))
+        return setErr(301, "ERROR 301: files share same names.");
+    G->rpt = fopen(f2, "wt");
+    if (!G->rpt) return setErr(305, "ERROR 305: cannot open report file.");
+    G->isOpen = true;
+    writeReportHeader();
+    if (G->prj->open(f1)) return setErr(G->prj->errorCode, G->prj->errorMsg);
+    return G->errorCode;
+}
+
+int DLLEXPORT swmmx_startHost(void)
+{
+    if (!G) return 501;
+    if (G->errorCode) return G->errorCode;
+    if (!G->isOpen) return (G->errorCode = 501);
+    if (G->isStarted) return (G->errorCode = 503);
+    G->prj->initState();
+    G->hostOnly = true;
+    G->isStarted = true;
+    G->mirrorValid = true;
+    return 0;
+}
+
+int DLLEXPORT swmm_start(int saveFlag)
+{
+    if (!G) return 501;
+    if (G->errorCode) return G->errorCode;
+    if (!G->isOpen) return (G->errorCode = 501);
+    if (G->isStarted) return (G->errorCode = 503);
+    Project& prj = *G->prj;
+    G->saveFlag = saveFlag != 0;
+    G->newRoutingTime = 0.0;
+    G->oldRoutingTime = 0.0;
+    G->reportTime = 1000.0 * (double)prj.opt.reportStep;
+    G->routingDuration = prj.opt.totalDuration;
+    G->totalStepCount = 0;
+    G->elapsedTime = 0.0;
+    prj.initState();
+    G->apiExtInflow.assign(prj.net.nNodes(), 0.0);
+    G->constantInflow = prj.inflowsAreConstant();
+    // output_open (swmm5.c:379) -- the reference always opens the binary file
+    if (G->out.open(G->outPath, prj)) return setErr(307, "ERROR 307: cannot open binary results file.");
+    // massbal_open: initial storage
+    double s = 0.0;
+    for (int j = 0; j < prj.net.nNodes(); j++) s += prj.st.newVolume[j];
+    for (int j = 0; j < prj.net.nLinks(); j++) s += prj.st.lNewVolume[j];
+    G->initStorage = s;
+    G->router.reset(new Router());
+    int dev = (gDevice >= 0) ? gDevice : defaultDevice();
+    if (G->router->init(prj, dev)) return setErr(G->router->lastError(), G->router->lastErrorMsg());
+    G->isStarted = true;
+    G->mirrorValid = true;
+    return G->errorCode;
+}
+
+static int execRouting()   // swmm5.c:514-575 + routing.c:203-265 on the device
+{
+    Project& prj = *G->prj;
+    Router& r = *G->router;
+    G->totalStepCount++;
+    double currentDate = prj.getDateTime(G->newRoutingTime);
+    int rc;
+    if (G->constantInflow) {
+        rc = r.step(nullptr, nullptr, nullptr);
+    } else {
+        std::vector<double> lat, qual;
+        double tot[3];
+        int P = prj.opt.ignoreQuality ? 0 : prj.net.nPollut();
+        prj.evalInflows(currentDate, lat, P ? &qual : nullptr, &tot[0], &tot[1], &tot[2]);
+        // apiExtInflow (swmm_setValue NODE_LATFLOW) is added by addExternalInflows
+        for (int j = 0; j < prj.net.nNodes(); j++) {
+            double q = G->apiExtInflow[j];
+            if (q == 0.0) continue;
+            if (fabs(q) < kFlowTol) q = 0.0;
+            lat[j] += q;
+            if (q >= 0.0) tot[1] += q; else tot[2] += -q;
+        }
+        rc = r.step(lat.data(), P ? qual.data() : nullptr, tot);
+    }
+    if (rc) return setErr(r.lastError(), r.lastErrorMsg());
+    G->mirrorValid = false;
+    // clock: identical arithmetic to the device's k_finalize; fixed steps are
+    // mirrored on the host, variable steps are read back (one sync per step)
+    G->oldRoutingTime = G->newRoutingTime;
+    if (prj.opt.courantFactor == 0.0 || prj.opt.routeStep < 0.001) {
+        double dt = prj.opt.routeStep;
+        if (G->newRoutingTime + 1000.0 * dt > G->routingDuration) {
+            dt = (G->routingDuration - G->newRoutingTime) / 1000.0;
+            dt = (dt >= 1. / 1000.0) ? dt : 1. / 1000.0;
+        }
+        G->newRoutingTime = G->newRoutingTime + 1000.0 * dt;
+    } else {
+        double t;
+        if (r.readClock(&t, nullptr, nullptr)) return setErr(r.lastError(), r.lastErrorMsg());
+        G->newRoutingTime = t;
+    }
+    return 0;
+}
+
+static void saveResults()   // swmm5.c:579-613
+{
+    if (G->newRoutingTime >= G->reportTime) {
+        if (syncMirror()) return;
+        double sys[6];
+        // StepFlowTotals of this step: {flooding, outflow, dw, gw, ii, ex}
+        sys[0] = G->sysStep[2];
+        sys[1] = G->sysStep[3];
+        sys[2] = G->sysStep[0];
+        sys[3] = 0.0;
+        sys[4] = 0.0;
+        sys[5] = G->sysStep[1];
+        int e = G->out.saveResults(*G->prj, G->reportTime, G->oldRoutingTime, G->newRoutingTime, sys);
+        if (e) setErr(e, "ERROR 309: cannot write to binary results file.");
+        G->reportTime = G->reportTime + 1000 * (double)G->prj->opt.reportStep;
+    }
+}
+
+int DLLEXPORT swmm_step(double* elapsedTime)
+{
+    if (elapsedTime) *elapsedTime = 0.0;
+    if (!G) return 501;
+    if (G->errorCode) return G->errorCode;
+    if (!G->isOpen) return (G->errorCode = 501);
+    if (!G->isStarted || G->hostOnly) return (G->errorCode = 502);
+    if (G->newRoutingTime < G->routingDuration) {
+        if (execRouting()) return G->errorCode;
+    }
+    if (G->saveFlag && G->newRoutingTime >= G->reportTime) {
+        G->router->stepTotals(G->sysStep);
+        saveResults();
+    }
+    if (G->newRoutingTime < G->routingDuration) G->elapsedTime = G->newRoutingTime / kMsecPerDay;
+    else G->elapsedTime = 0.0;
+    if (elapsedTime) *elapsedTime = G->elapsedTime;
+    return G->errorCode;
+}
+
+int DLLEXPORT swmmx_runSteps(int n, double* elapsedTime)
+{
+    double e = 0.0;
+    for (int i = 0; i < n; i++) {
+        int rc = swmm_step(&e);
+        if (rc) return rc;
+        if (e <= 0.0) break;
+    }
+    if (elapsedTime) *elapsedTime = e;
+    return G ? G->errorCode : 501;
+}
+
+int DLLEXPORT swmm_stride(int strideStep, double* elapsedTime)   // swmm5.c:466-510
+{
+    if (elapsedTime) *elapsedTime = 0.0;
+    if (!G) return 501;
+    if (G->errorCode) return G->errorCode;
+    if (!G->isOpen) return (G->errorCode = 501);
+    if (!G->isStarted || G->hostOnly) return (G->errorCode = 502);
+    Project& prj = *G->prj;
+    double realRouteStep = prj.opt.routeStep;
+    double dur = G->newRoutingTime + 1000.0 * strideStep;
+    if (prj.opt.totalDuration < dur) dur = prj.opt.totalDuration;
+    G->routingDuration = dur;
+    if (G->router->setDuration(dur)) return setErr(G->router->lastError(), G->router->lastErrorMsg());
+    if (strideStep < prj.opt.routeStep)
+        return setErr(500, "ERROR 500: swmm_stride shorter than the routing step is not supported by the MI355X engine");
+    double e = 0.0;
+    do {
+        swmm_step(&e);
+    } while (e > 0.0 && !G->errorCode);
+    prj.opt.routeStep = realRouteStep;
+    G->routingDuration = prj.opt.totalDuration;
+    G->router->setDuration(G->routingDuration);
+    if (G->newRoutingTime < prj.opt.totalDuration) G->elapsedTime = G->newRoutingTime / kMsecPerDay;
+    else G->elapsedTime = 0.0;
+    if (elapsedTime) *elapsedTime = G->elapsedTime;
+    return G->errorCode;
+}
+
+static double computeFlowError()   // massbal.c:858-902
+{
+    Project& prj = *G->prj;
+    double fs = 0.0;
+    for (int j = 0; j < prj.net.nNodes(); j++) fs += prj.st.newVolume[j];
+    for (int j = 0; j < prj.net.nLinks(); j++) fs += prj.st.lNewVolume[j];
+    G->finalStorage = fs;
+    double* T = G->flowTot;   // dw, ex, flooding, outflow, evap, seep
+    double totalInflow = G->initStorage + 0.0 + 0.0;
+    double totalOutflow = fs + T[2] + T[4] + T[5] + 0.0;
+    if (T[0] >= 0.0) totalInflow += T[0]; else totalOutflow -= T[0];
+    if (T[1] >= 0.0) totalInflow += T[1]; else totalOutflow -= T[1];
+    if (T[3] >= 0.0) totalOutflow += T[3]; else totalInflow -= T[3];
+    double pct = 0.0;
+    if (fabs(totalInflow - totalOutflow) < 1.0) pct = kTiny;
+    else if (fabs(totalInflow) > 0.0) pct = 100.0 * (1.0 - totalOutflow / totalInflow);
+    else if (fabs(totalOutflow) > 0.0) pct = 100.0 * (totalInflow / totalOutflow - 1.0);
+    return pct;
+}
+
+static void writeReportSummary()
+{
+    FILE* f = G->rpt;
+    if (!f || G->prj->rpt.disabled) return;
+    Project& prj = *G->prj;
+    double uV = prj.ucfVolume();
+    double* T = G->flowTot;
+    const double ac = prj.opt.unitSystem ? 1.0e4 : 43560.0;   // acre-ft or ha-m volume units
+    const double mg = prj.opt.unitSystem ? 1.0e3 : 7.48052e-6 * 1.0e6 / 1.0e6 * 1.0;
+    (void)mg;
+    double vcf = prj.opt.unitSystem ? 1.0e-4 : 1.0 / 43560.0;   // ft3 -> ac-ft / m3 -> ha-m
+    auto line = [&](const char* name, double v) {
+        fprintf(f, "  %-27s %9.3f\n", name, v * uV * vcf);
+    };
+    (void)ac;
+    fprintf(f, "\n  **************************\n");
+    fprintf(f, "  Flow Routing Continuity     %s\n", prj.opt.unitSystem ? "hectare-m" : "acre-feet");
+    fprintf(f, "  **************************  ---------\n");
+    line("Dry Weather Inflow .......", T[0]);
+    line("Wet Weather Inflow .......", 0.0);
+    line("Groundwater Inflow .......", 0.0);
+    line("RDII Inflow ..............", 0.0);
+    line("External Inflow ..........", T[1]);
+    line("External Outflow .........", T[3]);
+    line("Flooding Loss ............", T[2]);
+    line("Evaporation Loss .........", T[4]);
+    line("Exfiltration Loss ........", T[5]);
+    line("Initial Stored Volume ....", G->initStorage);
+    line("Final Stored Volume ......", G->finalStorage);
+    fprintf(f, "  Continuity Error (%%) ..... %9.3f\n", G->flowError);
+    long long iters = 0, nonConv = 0;
+    int last = 0;
+    G->router->counters(&iters, &nonConv, &last);
+    long long steps = G->totalStepCount > 0 ? G->totalStepCount : 1;
+    fprintf(f, "\n  *************************\n  Routing Time Step Summary\n  *************************\n");
+    fprintf(f, "  Average Iterations per Step : %8.2f\n", (double)iters / (double)steps);
+    fprintf(f, "  %% of Steps Not Converging   : %8.2f\n", 100.0 * (double)nonConv / (double)steps);
+    std::string dev = G->router->deviceName();
+    fprintf(f, "  Routing device              : %s\n", dev.c_str());
+}
+
+int DLLEXPORT swmm_end(void)   // swmm5.c:618-660
+{
+    if (!G || !G->isOpen) return 501;
+    if (G->isStarted) {
+        if (!G->hostOnly) {
+            syncMirror();
+            G->router->flowTotals(G->flowTot);
+            G->flowError = computeFlowError();
+            G->out.end(G->errorCode);
+            if (!G->errorCode) writeReportSummary();
+        }
+        G->isStarted = false;
+    }
+    return G->errorCode;
+}
+
+int DLLEXPORT swmm_report(void) { return G ? G->errorCode : 501; }
+
+int DLLEXPORT swmm_close(void)
+{
+    if (!G) return 0;
+    G->out.close();
+    if (G->rpt) fclose(G->rpt);
+    G->rpt = nullptr;
+    G->router.reset();
+    delete G;
+    G = nullptr;
+    return 0;
+}
+
+int DLLEXPORT swmm_run(const char* f1, const char* f2, const char* f3)   // swmm5.c:186-252
+{
+    double elapsed = 0.0;
+    swmm_open(f1, f2, f3);
+    if (G && !G->errorCode) {
+        swmm_start(1);
+        if (!G->errorCode) {
+            do {
+                swmm_step(&elapsed);
+            } while (elapsed > 0.0 && !G->errorCode);
+        }
+        swmm_end();
+    }
+    int err = G ? G->errorCode : 501;
+    swmm_close();
+    return err;
+}
+
+int DLLEXPORT swmm_getMassBalErr(float* runoffErr, float* flowErr, float* qualErr)
+{
+    if (runoffErr) *runoffErr = 0.0f;
+    if (flowErr) *flowErr = 0.0f;
+    if (qualErr) *qualErr = 0.0f;
+    if (G && G->isOpen && !G->isStarted) {
+        if (flowErr) *flowErr = (float)G->flowError;
+        if (qualErr) *qualErr = (float)G->qualError;
+    }
+    return 0;
+}
+
+int DLLEXPORT swmm_getVersion(void) { return 52004; }
+
+int DLLEXPORT swmm_getError(char* errMsg, int msgLen)
+{
+    if (!errMsg || msgLen <= 0) return G ? G->errorCode : 0;
+    std::string m = G ? G->errorMsg : std::string();
+    snprintf(errMsg, (size_t)msgLen, "%s", m.c_str());
+    return G ? G->errorCode : 0;
+}
+
+int DLLEXPORT swmm_getWarnings(void) { return G ? G->prj->warnings : 0; }
+
+int DLLEXPORT swmm_getCount(int objType)
+{
+    if (!G || !G->isOpen) return 0;
+    switch (objType) {
+    case swmm_GAGE: case swmm_SUBCATCH: return 0;
+    case swmm_NODE: return G->prj->net.nNodes();
+    case swmm_LINK: return G->prj->net.nLinks();
+    default: return 0;
+    }
+}
+
+void DLLEXPORT swmm_getName(int objType, int index, char* name, int size)
+{
+    if (!name || size <= 0) return;
+    name[0] = '\0';
+    if (!G || !G->isOpen) return;
+    const Network& n = G->prj->net;
+    if (objType == swmm_NODE && index >= 0 && index < n.nNodes()) snprintf(name, (size_t)size, "%s", n.nodeId[index].c_str());
+    if (objType == swmm_LINK && index >= 0 && index < n.nLinks()) snprintf(name, (size_t)size, "%s", n.linkId[index].c_str());
+}
+
+int DLLEXPORT swmm_getIndex(int objType, const char* name)
+{
+    if (!G || !G->isOpen || !name) return -1;
+    const Network& n = G->prj->net;
+    if (objType == swmm_NODE) { auto it = n.nodeIndex.find(name); return it == n.nodeIndex.end() ? -1 : it->second; }
+    if (objType == swmm_LINK) { auto it = n.linkIndex.find(name); return it == n.linkIndex.end() ? -1 : it->second; }
+    return -1;
+}
+
+double DLLEXPORT swmm_getValue(int property, int index)   // swmm5.c:842-1213
+{
+    if (!G || !G->isOpen) return 0;
+    Project& prj = *G->prj;
+    if (property < 100) {
+        switch (property) {
+        case swmm_STARTDATE: return prj.opt.startDateTime;
+        case swmm_CURRENTDATE: return prj.opt.startDateTime + G->elapsedTime;
+        case swmm_ELAPSEDTIME: return G->elapsedTime;
+        case swmm_ROUTESTEP: return prj.opt.routeStep;
+        case swmm_MAXROUTESTEP: return prj.opt.routeStep;
+        case swmm_REPORTSTEP: return prj.opt.reportStep;
+        case swmm_TOTALSTEPS: return G->out.periods();
+        case swmm_NOREPORT: return prj.rpt.disabled;
+        case swmm_FLOWUNITS: return prj.opt.flowUnits;
+        default: return 0;
+        }
+    }
+    if (property >= 300 && property < 400) {
+        if (index < 0 || index >= prj.net.nNodes()) return 0;
+        if (property >= swmm_NODE_DEPTH && property <= swmm_NODE_OVERFLOW && G->isStarted) syncMirror();
+        const Network& n = prj.net;
+        const State& s = prj.st;
+        double uL = prj.ucfLength(), uQ = prj.ucfFlow();
+        bool st = !s.newDepth.empty();
+        switch (property) {
+        case swmm_NODE_TYPE: return n.nodeType[index];
+        case swmm_NODE_ELEV: return n.invertElev[index] * uL;
+        case swmm_NODE_MAXDEPTH: return n.fullDepth[index] * uL;
+        case swmm_NODE_DEPTH: return st ? s.newDepth[index] * uL : 0.0;
+        case swmm_NODE_HEAD: return st ? (s.newDepth[index] + n.invertElev[index]) * uL : 0.0;
+        case swmm_NODE_VOLUME: return st ? s.newVolume[index] * prj.ucfVolume() : 0.0;
+        case swmm_NODE_LATFLOW: return st ? s.newLatFlow[index] * uQ : 0.0;
+        case swmm_NODE_INFLOW: return st ? s.inflow[index] * uQ : 0.0;
+        case swmm_NODE_OVERFLOW: return st ? s.overflow[index] * uQ : 0.0;
+        case swmm_NODE_RPTFLAG: return n.rptFlag[index] > 0;
+        default: return 0;
+        }
+    }
+    if (property >= 400 && property < 500) {
+        if (index < 0 || index >= prj.net.nLinks()) return 0;
+        if (property >= swmm_LINK_FLOW && property <= swmm_LINK_TOPWIDTH && G->isStarted) syncMirror();
+        const Network& n = prj.net;
+        const State& s = prj.st;
+        double uL = prj.ucfLength(), uQ = prj.ucfFlow();
+        bool st = !s.lNewDepth.empty();
+        const Xsect& x = n.xsect[index];
+        Geom g{x.type, x.yFull, x.wMax, x.ywMax, x.aFull, x.rFull, x.sFull, x.sMax, x.yBot, x.aBot, x.sBot, x.rBot};
+        const double* ct = &SWX_CIRC_TABLES[0][0];
+        switch (property) {
+        case swmm_LINK_TYPE: return n.linkType[index];
+        case swmm_LINK_NODE1: return n.node1[index];
+        case swmm_LINK_NODE2: return n.node2[index];
+        case swmm_LINK_LENGTH: return n.length[index] * uL;
+        case swmm_LINK_SLOPE: return n.slope[index];
+        case swmm_LINK_FULLDEPTH: return x.yFull * uL;
+        case swmm_LINK_FULLFLOW: return n.qFull[index] * uQ;
+        case swmm_LINK_FLOW: return st ? s.lNewFlow[index] * uQ * (double)n.direction[index] : 0.0;
+        case swmm_LINK_VELOCITY: {
+            if (!st) return 0.0;
+            double depth = s.lNewDepth[index], v = 0.0;
+            if (depth > 0.01) {
+                double fl = fabs(s.lNewFlow[index]) / n.barrels[index];
+                double area = getAofY(g, depth, ct);
+                if (area > kFudge) v = fl / area;
+            }
+            return v * uL;
+        }
+        case swmm_LINK_DEPTH: return st ? s.lNewDepth[index] * uL : 0.0;
+        case swmm_LINK_TOPWIDTH: return st ? getWofY(g, s.lNewDepth[index], ct) * uL : 0.0;
+        case swmm_LINK_SETTING: return st ? s.setting[index] : 1.0;
+        case swmm_LINK_RPTFLAG: return n.linkRpt[index] > 0;
+        default: return 0;
+        }
+    }
+    return 0;
+}
+
+void DLLEXPORT swmm_setValue(int property, int index, double value)
+{
+    if (!G || !G->isOpen) return;
+    Project& prj = *G->prj;
+    switch (property) {
+    case swmm_NODE_LATFLOW:
+        if (index < 0 || index >= prj.net.nNodes()) return;
+        if (G->apiExtInflow.size() != (size_t)prj.net.nNodes()) G->apiExtInflow.assign(prj.net.nNodes(), 0.0);
+        G->apiExtInflow[index] = value / prj.ucfFlow();
+        G->constantInflow = false;
+        return;
+    case swmm_NODE_RPTFLAG:
+        if (!G->isStarted && index >= 0 && index < prj.net.nNodes()) prj.net.rptFlag[index] = value > 0.0;
+        return;
+    case swmm_LINK_RPTFLAG:
+        if (!G->isStarted && index >= 0 && index < prj.net.nLinks()) prj.net.linkRpt[index] = value > 0.0;
+        return;
+    case swmm_LINK_SETTING:
+        return;   // conduit settings cannot be changed (swmm5.c:1323)
+    case swmm_REPORTSTEP:
+        if (!G->isStarted && value > 0) prj.opt.reportStep = (int)value;
+        return;
+    case swmm_NOREPORT:
+        if (!G->isStarted) prj.rpt.disabled = value > 0.0;
+        return;
+    case swmm_ROUTESTEP:
+        if (!G->isStarted && value > 0.0) { prj.opt.courantFactor = 0.0; prj.opt.routeStep = value; }
+        return;
+    default:
+        return;
+    }
+}
+
+double DLLEXPORT swmm_getSavedValue(int property, int index, int period)   // swmm5.c:919-946
+{
+    if (!G || !G->isOpen || G->isStarted) return 0;
+    if (period < 1 || period > G->out.periods()) return 0;
+    if (property == swmm_CURRENTDATE) {
+        double d = 0;
+        G->out.readDate(period, &d);
+        return d;
+    }
+    Network& n = G->prj->net;
+    float v = 0.0f;
+    if (property >= 300 && property < 400) {
+        if (index < 0 || index >= n.nNodes() || !n.rptFlag[index]) return 0;
+        int k = 0;
+        for (int j = 0; j < index; j++) if (n.rptFlag[j]) k++;
+        int var = -1;
+        switch (property) {
+        case swmm_NODE_DEPTH: var = 0; break;
+        case swmm_NODE_HEAD: var = 1; break;
+        case swmm_NODE_VOLUME: var = 2; break;
+        case swmm_NODE_LATFLOW: var = 3; break;
+        case swmm_NODE_INFLOW: var = 4; break;
+        case swmm_NODE_OVERFLOW: var = 5; break;
+        default: return 0;
+        }
+        G->out.readNodeVar(period, k, var, &v);
+        return v;
+    }
+    if (property >= 400 && property < 500) {
+        if (index < 0 || index >= n.nLinks() || !n.linkRpt[index]) return 0;
+        int k = 0;
+        for (int j = 0; j < index; j++) if (n.linkRpt[j]) k++;
+        int var = -1;
+        switch (property) {
+        case swmm_LINK_FLOW: var = 0; break;
+        case swmm_LINK_DEPTH: var = 1; break;
+        case swmm_LINK_VELOCITY: var = 2; break;
+        default: return 0;
+        }
+        G->out.readLinkVar(period, k, var, &v);
+        return v;
+    }
+    return 0;
+}
+
+void DLLEXPORT swmm_writeLine(const char* line)
+{
+    if (G && G->isOpen && G->rpt && line) fprintf(G->rpt, "%s\n", line);
+}
+
+void DLLEXPORT swmm_decodeDate(double date, int* year, int* month, int* day, int* hour, int* minute,
+                               int* second, int* dayOfWeek)
+{
+    decodeDate(date, year, month, day);
+    decodeTime(date, hour, minute, second);
+    *dayOfWeek = swx::dayOfWeek(date);
+}
+
+// ---------------------------------------------------------------- extensions
+long DLLEXPORT swmmx_getArray(const char* name, double* dst, long n)
+{
+    if (!G || !G->isOpen || !name) return -1;
+    if (G->isStarted && !G->hostOnly) syncMirror();
+    Project& prj = *G->prj;
+    State& s = prj.st;
+    Network& net = prj.net;
+    std::vector<double> tmp;
+    const std::vector<double>* v = nullptr;
+    std::string k(name);
+#define ARR(nm, vec) if (k == nm) v = &vec;
+    ARR("node.newDepth", s.newDepth) ARR("node.oldDepth", s.oldDepth) ARR("node.newVolume", s.newVolume)
+    ARR("node.oldVolume", s.oldVolume) ARR("node.inflow", s.inflow) ARR("node.outflow", s.outflow)
+    ARR("node.overflow", s.overflow) ARR("node.newLatFlow", s.newLatFlow) ARR("node.oldLatFlow", s.oldLatFlow)
+    ARR("node.oldNetInflow", s.oldNetInflow) ARR("node.oldFlowInflow", s.oldFlowInflow)
+    ARR("node.oldSurfArea", s.oldSurfArea) ARR("node.dYdT", s.dYdT)
+    ARR("link.newFlow", s.lNewFlow) ARR("link.oldFlow", s.lOldFlow) ARR("link.newDepth", s.lNewDepth)
+    ARR("link.oldDepth", s.lOldDepth) ARR("link.newVolume", s.lNewVolume) ARR("link.oldVolume", s.lOldVolume)
+    ARR("link.surfArea1", s.surfArea1) ARR("link.surfArea2", s.surfArea2) ARR("link.froude", s.froude)
+    ARR("link.dqdh", s.dqdh) ARR("link.a1", s.a1) ARR("link.a2", s.a2) ARR("link.q1", s.q1)
+    ARR("link.q2", s.q1)   // under DW q2 == q1 (dwflow.c:285-286)
+    ARR("link.setting", s.setting) ARR("link.evapLossRate", s.evapLossRate) ARR("link.seepLossRate", s.seepLossRate)
+    ARR("node.newQual", s.nNewQual) ARR("node.oldQual", s.nOldQual) ARR("link.newQual", s.lNewQual)
+    ARR("link.oldQual", s.lOldQual)
+    ARR("node.invertElev", net.invertElev) ARR("node.fullDepth", net.fullDepth) ARR("node.surDepth", net.surDepth)
+    ARR("node.pondedArea", net.pondedArea) ARR("node.crownElev", net.crownElev) ARR("node.fullVolume", net.fullVolume)
+    ARR("node.fixedStage", net.fixedStage) ARR("node.initDepth", net.initDepth)
+    ARR("link.offset1", net.offset1) ARR("link.offset2", net.offset2) ARR("link.q0", net.q0) ARR("link.qLimit", net.qLimit)
+    ARR("link.cLossInlet", net.cLossInlet) ARR("link.cLossOutlet", net.cLossOutlet) ARR("link.cLossAvg", net.cLossAvg)
+    ARR("link.seepRate", net.seepRate) ARR("link.length", net.length) ARR("link.roughness", net.roughness)
+    ARR("link.modLength", net.modLength) ARR("link.roughFactor", net.roughFactor) ARR("link.slope", net.slope)
+    ARR("link.beta", net.beta) ARR("link.qMax", net.qMax) ARR("link.qFull", net.qFull)
+#undef ARR
+    auto fromInt = [&](const std::vector<int>& iv) { tmp.assign(iv.begin(), iv.end()); v = &tmp; };
+    if (k == "node.type") fromInt(net.nodeType);
+    if (k == "node.degree") fromInt(net.degree);
+    if (k == "node.outfallType") fromInt(net.outfallType);
+    if (k == "node.outfallFlap") fromInt(net.outfallFlap);
+    if (k == "link.type") fromInt(net.linkType);
+    if (k == "link.node1") fromInt(net.node1);
+    if (k == "link.node2") fromInt(net.node2);
+    if (k == "link.hasFlapGate") fromInt(net.hasFlapGate);
+    if (k == "link.direction") fromInt(net.direction);
+    if (k == "link.barrels") fromInt(net.barrels);
+    if (k == "link.hasLosses") fromInt(net.hasLosses);
+    if (k == "link.superCritical") fromInt(net.superCritical);
+    if (k == "link.flowClass") fromInt(s.flowClass);
+    if (k == "link.fullState") fromInt(s.fullState);
+    if (k == "link.normalFlow") fromInt(s.normalFlow);
+    if (k == "link.capacityLimited") fromInt(s.capacityLimited);
+    if (k == "node.converged") fromInt(s.converged);
+    if (k.rfind("link.x", 0) == 0) {
+        std::string f = k.substr(6);
+        tmp.resize(net.nLinks());
+        bool okf = true;
+        for (int j = 0; j < net.nLinks(); j++) {
+            const Xsect& x = net.xsect[j];
+            if (f == "type") tmp[j] = x.type; else if (f == "yFull") tmp[j] = x.yFull;
+            else if (f == "wMax") tmp[j] = x.wMax; else if (f == "ywMax") tmp[j] = x.ywMax;
+            else if (f == "aFull") tmp[j] = x.aFull; else if (f == "rFull") tmp[j] = x.rFull;
+            else if (f == "sFull") tmp[j] = x.sFull; else if (f == "sMax") tmp[j] = x.sMax;
+            else if (f == "yBot") tmp[j] = x.yBot; else if (f == "aBot") tmp[j] = x.aBot;
+            else if (f == "sBot") tmp[j] = x.sBot; else if (f == "rBot") tmp[j] = x.rBot;
+            else if (f == "culvertCode") tmp[j] = x.culvertCode;
+            else { okf = false; break; }
+        }
+        if (okf) v = &tmp;
+    }
+    if (k == "opt") {
+        const Options& o = prj.opt;
+        tmp = {o.routeStep, o.courantFactor, o.minRouteStep, o.minSurfArea, o.headTol, o.crownCutoff,
+               o.lengtheningStep, o.evapRate, o.totalDuration, (double)o.reportStep, o.startDateTime,
+               (double)o.maxTrials, (double)o.surchargeMethod, (double)o.inertDamping,
+               (double)o.normalFlowLtd, (double)o.allowPonding};
+        v = &tmp;
+    }
+    if (!v) return -1;
+    long m = (long)v->size();
+    if (dst) for (long i = 0; i < m && i < n; i++) dst[i] = (*v)[i];
+    return m;
+}
+
+long DLLEXPORT swmmx_setArray(const char* name, const double* src, long n)
+{
+    if (!G || !G->isOpen || !name || !src) return -1;
+    if (G->isStarted && !G->hostOnly) syncMirror();
+    State& s = G->prj->st;
+    std::vector<double>* v = nullptr;
+    std::string k(name);
+    if (k == "node.newDepth") v = &s.newDepth;
+    if (k == "link.newFlow") v = &s.lNewFlow;
+    if (k == "link.q1") v = &s.q1;
+    if (!v) return -1;
+    long m = std::min<long>((long)v->size(), n);
+    for (long i = 0; i < m; i++) (*v)[i] = src[i];
+    if (G->isStarted && !G->hostOnly) G->router->upload(*G->prj);
+    return m;
+}
+
+int DLLEXPORT swmmx_exportState(const char* path)
+{
+    if (!G || !G->isOpen || !path) return 501;
+    if (G->isStarted && !G->hostOnly) syncMirror();
+    FILE* f = fopen(path, "wb");
+    if (!f) return 303;
+    fwrite("SWDUMP1\0", 1, 8, f);
+    auto rec = [&](const std::string& name, char dt, const void* data, long long cnt) {
+        char nm[48] = {0};
+        snprintf(nm, sizeof nm, "%s", name.c_str());
+        fwrite(nm, 1, 48, f);
+        fwrite(&dt, 1, 1, f);
+        fwrite(&cnt, 8, 1, f);
+        fwrite(data, dt == 'd' ? 8 : 4, (size_t)cnt, f);
+    };
+    Project& prj = *G->prj;
+    int counts[4] = {prj.net.nNodes(), prj.net.nLinks(), prj.net.nPollut(), 0};
+    rec("counts", 'i', counts, 4);
+    {   // the option records of oracle/refdump.c (same order)
+        const Options& o = prj.opt;
+        double od[12] = {o.routeStep, o.courantFactor, o.minRouteStep, o.minSurfArea, o.headTol,
+                         o.crownCutoff, o.lengtheningStep, o.evapRate, o.totalDuration,
+                         (double)o.reportStep, o.startDateTime, 0.0};
+        int oi[12] = {o.maxTrials, o.surchargeMethod, o.inertDamping, o.normalFlowLtd,
+                      o.allowPonding, o.routeModel, o.forceMainEqn, o.flowUnits, o.unitSystem,
+                      o.ignoreQuality, 0, 0};
+        rec("opt.d", 'd', od, 12);
+        rec("opt.i", 'i', oi, 12);
+        int P = prj.net.nPollut();
+        if (P > 0) {
+            std::vector<double> kd(P), cd(P), ci(P);
+            for (int p = 0; p < P; p++) {
+                kd[p] = prj.net.pollut[p].kDecay;
+                cd[p] = prj.net.pollut[p].cDWF;
+                ci[p] = prj.net.pollut[p].cInit;
+            }
+            rec("pollut.kDecay", 'd', kd.data(), P);
+            rec("pollut.dwfConcen", 'd', cd.data(), P);
+            rec("pollut.initConcen", 'd', ci.data(), P);
+        }
+    }
+    static const char* names[] = {
+        "node.type", "node.degree", "node.outfallType", "node.outfallFlap", "node.invertElev",
+        "node.initDepth", "node.fullDepth", "node.surDepth", "node.pondedArea", "node.crownElev",
+        "node.fullVolume", "node.fixedStage", "node.newDepth", "node.oldDepth", "node.newVolume",
+        "node.oldVolume", "node.inflow", "node.outflow", "node.newLatFlow", "node.oldLatFlow",
+        "node.oldNetInflow", "node.oldFlowInflow", "node.overflow", "node.converged",
+        "node.oldSurfArea", "node.dYdT",
+        "link.type", "link.node1", "link.node2", "link.hasFlapGate", "link.direction", "link.flowClass",
+        "link.xtype", "link.culvertCode", "link.barrels", "link.hasLosses", "link.superCritical",
+        "link.offset1", "link.offset2", "link.q0", "link.qLimit", "link.cLossInlet", "link.cLossOutlet",
+        "link.cLossAvg", "link.seepRate", "link.setting", "link.qFull", "link.yFull", "link.wMax",
+        "link.ywMax", "link.aFull", "link.rFull", "link.sFull", "link.sMax", "link.yBot", "link.aBot",
+        "link.sBot", "link.rBot", "link.length", "link.roughness", "link.modLength", "link.roughFactor",
+        "link.slope", "link.beta", "link.qMax", "link.newFlow", "link.oldFlow", "link.newDepth",
+        "link.oldDepth", "link.newVolume", "link.oldVolume", "link.a1", "link.a2", "link.q1", "link.q2",
+        "link.froude", "link.dqdh", "link.surfArea1", "link.surfArea2", "link.fullState",
+        "link.normalFlow", "link.capacityLimited", "node.newQual", "node.oldQual", "link.newQual",
+        "link.oldQual", nullptr};
+    std::vector<double> buf;
+    for (int i = 0; names[i]; i++) {
+        std::string nm = names[i];
+        std::string q = nm;
+        if (nm.rfind("link.", 0) == 0) {
+            static const char* xf[] = {"yFull", "wMax", "ywMax", "aFull", "rFull", "sFull", "sMax",
+                                       "yBot", "aBot", "sBot", "rBot", "culvertCode", nullptr};
+            for (int k = 0; xf[k]; k++) if (nm == std::string("link.") + xf[k]) q = std::string("link.x") + xf[k];
+            if (nm == "link.xtype") q = "link.xtype";
+        }
+        long m = swmmx_getArray(q.c_str(), nullptr, 0);
+        if (m < 0) continue;
+        buf.resize(std::max<long>(m, 1));
+        swmmx_getArray(q.c_str(), buf.data(), m);
+        bool isInt = nm == "node.type" || nm == "node.degree" || nm == "node.outfallType" ||
+                     nm == "node.outfallFlap" || nm == "node.converged" || nm == "link.type" ||
+                     nm == "link.node1" || nm == "link.node2" || nm == "link.hasFlapGate" ||
+                     nm == "link.direction" || nm == "link.flowClass" || nm == "link.xtype" ||
+                     nm == "link.culvertCode" || nm == "link.barrels" || nm == "link.hasLosses" ||
+                     nm == "link.superCritical" || nm == "link.fullState" || nm == "link.normalFlow" ||
+                     nm == "link.capacityLimited";
+        if (isInt) {
+            std::vector<int> iv(m);
+            for (long j = 0; j < m; j++) iv[j] = (int)buf[j];
+            rec(nm, 'i', iv.data(), m);
+        } else {
+            rec(nm == "opt" ? "opt.engine" : nm, 'd', buf.data(), m);
+        }
+    }
+    fclose(f);
+    return 0;
+}
+
+int DLLEXPORT swmmx_getCounters(long long* out, int n)
+{
+    if (!G || !out) return 0;
+    long long v[6] = {G->totalStepCount, 0, 0, 0, G->prj->net.nLinks(), G->prj->net.nNodes()};
+    if (G->router && G->router->ok()) {
+        int last = 0;
+        G->router->counters(&v[1], &v[2], &last);
+        v[3] = last;
+    }
+    int m = n < 6 ? n : 6;
+    for (int i = 0; i < m; i++) out[i] = v[i];
+    return m;
+}
+
+int DLLEXPORT swmmx_setTiming(int mode)
+{
+    if (!G || !G->router) return 502;
+    G->router->setTiming(mode != 0);
+    return 0;
+}
+
+int DLLEXPORT swmmx_getKernelTimes(double* out, int n)
+{
+    if (!G || !G->router) return 0;
+    return G->router->kernelTimes(out, n);
+}
+
+int DLLEXPORT swmmx_getKernelBytes(double* out, int n)
+{
+    if (!G || !G->router) return 0;
+    return G->router->kernelBytes(out, n);
+}
+
+int DLLEXPORT swmmx_getBackend(char* buf, int size)
+{
+    std::string s = (G && G->router && G->router->ok()) ? G->router->deviceName() : std::string("none");
+    if (buf && size > 0) snprintf(buf, (size_t)size, "%s", s.c_str());
+    return 0;
+}
+
+int DLLEXPORT swmmx_setDevice(int ordinal)
+{
+    gDevice = ordinal;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,1590 @@
+// dw_kernels.hip -- gfx950 kernels and the HBM-resident router.
+//
+// One routing step (reference: routing_execute -> flowrout_execute ->
+// dynwave_execute, src/solver/routing.c:203-265, dynwave.c:224-262) is:
+//
+//   for k in 0 .. MaxTrials-1:                      (graph nodes, early exit)
+//     k_link<k==0>   one thread per conduit: Saint-Venant momentum update
+//                    (dwflow_findConduitFlow, dwflow.c:57-293); iteration 0
+//                    also rotates link state (link_setOldHydState, a2 <- a1)
+//     k_node<k==0>   one thread per node: CSR gather of incident-link flows in
+//                    link-index order (= the reference's serial scatter,
+//                    dynwave.c:398-411, 528-589, so node sums are bit-exact),
+//                    outfall depth (link.c:728-766) and continuity/depth update
+//                    (setNodeDepth, dynwave.c:636-762); wave-level ballot of the
+//                    convergence test (dynwave.c:618) into one flag per iteration
+//   k_qual_node / k_qual_link   pollutant advection (qualrout.c:100-142)
+//   k_step_end     capacity-limited links, outfall system outflow, flow totals
+//                  and Courant-step partials (dynwave.c:349-378, 799-921,
+//                  routing.c:841-925)
+//   k_finalize     one block: deterministic fixed-order reduction of the block
+//                  partials, Picard-step count, next variable step.
+//
+// Everything is fp64 and compiled with -ffp-contract=off: apart from OCML vs
+// glibc ulps in pow/exp/sqrt/sin/cos the arithmetic is the reference's.
+// No MFMA: the path is HBM-bandwidth bound (DESIGN.md has the byte model).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "router.h"
+#include "xsect.h"
+
+namespace swx {
+
+#define HIPCHECK(x)                                                                  \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            fail(std::string(#x) + ": " + hipGetErrorString(e_));                    \
+            return err_ ? err_ : 500;                                                \
+        }                                                                            \
+    } while (0)
+
+constexpr int kBlock = 256;
+constexpr int kMaxTrialsCap = 32;
+constexpr int kNumPartials = 8;   // per-block partial sums written by k_step_end
+
+// ---- packed per-link flags -------------------------------------------------
+enum : uint32_t {
+    LF_XTYPE = 0x1Fu,             // bits 0-4 cross-section type
+    LF_BARREL_SHIFT = 5,          // bits 5-12 barrels
+    LF_LOSSES = 1u << 13,
+    LF_FLAP = 1u << 14,
+    LF_N1_OUTFALL = 1u << 15,
+    LF_N2_OUTFALL = 1u << 16,
+    LF_N1_OFLAP = 1u << 17,       // node1 is an outfall with a flap gate
+    LF_N2_OFLAP = 1u << 18,
+    LF_SEEP = 1u << 19,           // seepage > 0 or evaporation active
+    LF_QLIMIT = 1u << 20,
+    LF_DIRNEG = 1u << 21,
+};
+// ---- packed per-node flags -------------------------------------------------
+enum : uint32_t {
+    NF_TYPE = 0x3u,               // node type
+    NF_OTYPE_SHIFT = 2,           // outfall type, 3 bits
+    NF_DEGNEG = 1u << 5,          // degree < 0 (upstream terminal)
+    NF_CANPOND = 1u << 6,
+};
+// ---- packed link state word ------------------------------------------------
+// bits 0-3 flowClass, 4-7 fullState code (0 / 8 / 9 / 10), 8 normalFlow,
+// 9 capacityLimited, 10 inletControl
+__host__ __device__ inline int stFlowClass(int s) { return s & 0xF; }
+__host__ __device__ inline int stFullState(int s) { return (s >> 4) & 0xF; }
+
+struct StepCtl {
+    double dt;                    // step length used by the current step
+    double dtNext;                // variable step computed at step end
+    double variableStep;          // dynwave.c:84 VariableStep
+    int unconv[kMaxTrialsCap];    // per-iteration "some node not converged" flag
+    int lastSteps;
+    int pad;
+    long long totalSteps, totalIters, nonConverge;
+    double stepTot[kNumPartials];     // this step's system totals (rates)
+    double prevStepTot[kNumPartials]; // previous step's totals (massbal half step)
+    double flowTot[kNumPartials];     // accumulated volumes
+    double latTot[4];                 // {dwInflow, exInflow, exOutflow} rates of this step
+    double newRoutingTime;            // msec (swmm5.c / routing.c clock mirror)
+    double routingDuration;           // msec
+    double routeStep;                 // fixed step (sec)
+};
+
+struct Params {
+    int nN, nL, P, maxTrials;
+    // options
+    int surchargeMethod, inertDamping, normalFlowLtd, allowPonding, varStep;
+    double crownCutoff, minSurfArea, headTol, evapRate, courantFactor, minRouteStep, routeStep;
+    // link static
+    const int2* lnodes;
+    const uint32_t* lflags;
+    const double *inv1, *inv2, *off1, *off2;
+    const double *yFull, *wMax, *ywMax, *aFull, *rFull, *sFull, *sMax, *yBot, *aBot, *sBot, *rBot;
+    const double *length, *modLength, *roughFactor, *beta, *qMax, *qLimit, *slope;
+    const double *cIn, *cOut, *cAvg, *seepRate;
+    // link dynamic
+    double *lNewFlow, *lOldFlow, *lNewDepth, *lOldDepth, *lNewVolume, *lOldVolume;
+    double *a1, *a2, *q1, *dqdh, *froude, *sa1, *sa2, *evapLoss, *seepLoss, *setting;
+    int* lstate;
+    // node static
+    const uint32_t* nflags;
+    const double *invert, *fullDepth, *surDepth, *pondedArea, *yCrown, *fullVolume, *fixedStage;
+    const double *crownElev;
+    const int* rowptr;
+    const int* csr;               // link index | (1<<31 if node is the link's node2)
+    const int* outfallLink;       // per node: its single link (outfalls) or -1
+    // node dynamic
+    double *nNewDepth, *nOldDepth, *nNewVolume, *nOldVolume, *inflow, *outflow, *overflow;
+    double *newLat, *oldLat, *oldNetInflow, *oldFlowInflow, *oldSurfArea, *dYdT;
+    int* conv;
+    const double* latIn;          // lateral inflow for this step
+    // quality [p][object]
+    double *nOldQual, *nNewQual, *lOldQual, *lNewQual;
+    const double* qualIn;         // mass loads for this step [p][node]
+    const double* kDecay;
+    // misc
+    const double* gTables;        // global copy of the 5x51 circular tables
+    double* partials;             // [nBlocksEnd][kNumPartials]
+    int nBlocksEnd;
+    StepCtl* ctl;
+};
+
+// ===========================================================================
+//  device helpers
+// ===========================================================================
+__device__ __forceinline__ Geom loadGeom(const Params& p, int j, uint32_t f)
+{
+    Geom g;
+    g.type = (int)(f & LF_XTYPE);
+    g.yFull = p.yFull[j];
+    g.wMax = p.wMax[j];
+    g.aFull = p.aFull[j];
+    g.rFull = p.rFull[j];
+    g.sFull = p.sFull[j];
+    g.sMax = p.sMax[j];
+    g.ywMax = p.ywMax[j];
+    if (g.type != G_CIRCULAR) {
+        g.yBot = p.yBot[j];
+        g.aBot = p.aBot[j];
+        g.sBot = p.sBot[j];
+        g.rBot = p.rBot[j];
+    } else {
+        g.yBot = g.aBot = g.sBot = g.rBot = 0.0;
+    }
+    return g;
+}
+
+// dwflow.c:575-588
+__device__ __forceinline__ double slotWidth(const Params& p, const Geom& x, double y)
+{
+    double yNorm = y / x.yFull;
+    if (p.surchargeMethod != SUR_SLOT || isOpen(x.type) || yNorm < p.crownCutoff) return 0.0;
+    if (yNorm > 1.78) return 0.01 * x.wMax;
+    return x.wMax * 0.5423 * exp(-pow(yNorm, 2.4));
+}
+// dwflow.c:592-605
+__device__ __forceinline__ double widthAt(const Params& p, const Geom& x, double y, const double* ct)
+{
+    double wSlot = slotWidth(p, x, y);
+    if (wSlot > 0.0) return wSlot;
+    if (y / x.yFull >= p.crownCutoff && !isOpen(x.type)) y = p.crownCutoff * x.yFull;
+    return getWofY(x, y, ct);
+}
+// dwflow.c:609-619, 623-633
+__device__ __forceinline__ double areaAt(const Geom& x, double y, double wSlot, const double* ct)
+{
+    if (y >= x.yFull) return x.aFull + (y - x.yFull) * wSlot;
+    return getAofY(x, y, ct);
+}
+__device__ __forceinline__ double hydRadAt(const Geom& x, double y, const double* ct)
+{
+    if (y >= x.yFull) return x.rFull;
+    return getRofY(x, y, ct);
+}
+
+// link.c:1334-1399 (DW branch); returns total loss rate, sets evap/seep
+__device__ double conduitLossRate(const Params& p, int j, const Geom& x, double tstep,
+                                  double* evapOut, double* seepOut, const double* ct)
+{
+    double depth = 0.5 * (p.lOldDepth[j] + p.lNewDepth[j]);
+    double evapLossRate = 0.0, seepLossRate = 0.0, totalLossRate = 0.0;
+    if (depth > 0.0001) {
+        double len = p.length[j];
+        if (isOpen(x.type) && p.evapRate > 0.0) {
+            double topWidth = getWofY(x, depth, ct);
+            evapLossRate = topWidth * len * p.evapRate;
+        }
+        double sr = p.seepRate[j];
+        if (sr > 0.0) {
+            double width;
+            if (x.type == G_RECT_CLOSED) width = x.wMax;
+            else {
+                if (depth >= x.ywMax) depth = x.ywMax;
+                width = getWofY(x, depth, ct);
+            }
+            seepLossRate = sr * width * len;
+            seepLossRate *= 1.0;
+        }
+        totalLossRate = evapLossRate + seepLossRate;
+        double q = p.lNewVolume[j] / tstep;
+        if (totalLossRate > q) {
+            evapLossRate = evapLossRate * q / totalLossRate;
+            seepLossRate = seepLossRate * q / totalLossRate;
+            totalLossRate = q;
+        }
+    }
+    *evapOut = evapLossRate;
+    *seepOut = seepLossRate;
+    return totalLossRate;
+}
+
+// dwflow.c:297-413
+__device__ int flowClassOf(const Params& p, int j, const Geom& x, uint32_t f, int n1, int n2,
+                           double q, double h1, double h2, double y1, double y2, double* yC,
+                           double* yN, double* fasnh, const double* ct)
+{
+    double z1 = p.off1[j], z2 = p.off2[j];
+    if (f & LF_N1_OUTFALL) z1 = gmax(0.0, (z1 - p.nNewDepth[n1]));
+    if (f & LF_N2_OUTFALL) z2 = gmax(0.0, (z2 - p.nNewDepth[n2]));
+    int fc = F_SUBCRIT;
+    *fasnh = 1.0;
+    if (y1 > 0.0001 && y2 > 0.0001) {
+        if (q < 0.0) {
+            if (z1 > 0.0) {
+                *yN = linkYnorm(x, fabs(q), p.qMax[j], p.beta[j], ct);
+                *yC = getYcrit(x, fabs(q), ct);
+                double ycMin = gmin(*yN, *yC);
+                if (y1 < ycMin) fc = F_UP_CRIT;
+            }
+        } else {
+            if (z2 > 0.0) {
+                *yN = linkYnorm(x, fabs(q), p.qMax[j], p.beta[j], ct);
+                *yC = getYcrit(x, fabs(q), ct);
+                double ycMin = gmin(*yN, *yC);
+                double ycMax = gmax(*yN, *yC);
+                if (y2 < ycMin) fc = F_DN_CRIT;
+                else if (y2 < ycMax) {
+                    if (ycMax - ycMin < 0.0001) *fasnh = 0.0;
+                    else *fasnh = (ycMax - y2) / (ycMax - ycMin);
+                }
+            }
+        }
+    } else if (y1 <= 0.0001 && y2 <= 0.0001) {
+        fc = F_DRY;
+    } else if (y2 > 0.0001) {
+        if (h2 < p.inv1[j] + p.off1[j]) fc = F_UP_DRY;
+        else if (z1 > 0.0) {
+            *yN = linkYnorm(x, fabs(q), p.qMax[j], p.beta[j], ct);
+            *yC = getYcrit(x, fabs(q), ct);
+            fc = F_UP_CRIT;
+        }
+    } else {
+        if (h1 < p.inv2[j] + p.off2[j]) fc = F_DN_DRY;
+        else if (z2 > 0.0) {
+            *yN = linkYnorm(x, fabs(q), p.qMax[j], p.beta[j], ct);
+            *yC = getYcrit(x, fabs(q), ct);
+            fc = F_DN_CRIT;
+        }
+    }
+    return fc;
+}
+
+// dwflow.c:57-293 -- one conduit, one Picard iteration.
+template <bool kFirst>
+__device__ void conduitFlow(const Params& p, int j, int steps, double dt, const double* ct)
+{
+    const double omega = 0.5;
+    uint32_t f = p.lflags[j];
+    int2 nn = p.lnodes[j];
+    int n1 = nn.x, n2 = nn.y;
+    Geom x = loadGeom(p, j, f);
+    double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
+
+    // iteration 0: link_setOldHydState (link.c:564-583), a2 <- a1 (dynwave.c:292)
+    double newFlowPrev = p.lNewFlow[j];
+    double oldFlow, oldDepth;
+    if (kFirst) {
+        oldFlow = newFlowPrev;
+        oldDepth = p.lNewDepth[j];
+        p.lOldFlow[j] = oldFlow;
+        p.lOldDepth[j] = oldDepth;
+        p.lOldVolume[j] = p.lNewVolume[j];
+        double a1v = p.a1[j];
+        p.a2[j] = a1v;
+    } else {
+        oldFlow = p.lOldFlow[j];
+    }
+    bool isClosed = (p.setting[j] == 0);
+    double qOld = oldFlow / barrels;
+    double qLast = p.q1[j];
+    double evapRate = 0.0, seepRate = 0.0;
+
+    double inv1 = p.inv1[j], inv2 = p.inv2[j];
+    double z1 = inv1 + p.off1[j];
+    double z2 = inv2 + p.off2[j];
+    double h1 = p.nNewDepth[n1] + inv1;
+    double h2 = p.nNewDepth[n2] + inv2;
+    h1 = gmax(h1, z1);
+    h2 = gmax(h2, z2);
+    double y1 = h1 - z1;
+    double y2 = h2 - z2;
+    y1 = gmax(y1, 0.0001);
+    y2 = gmax(y2, 0.0001);
+    if (p.surchargeMethod != SUR_SLOT) {
+        y1 = gmin(y1, x.yFull);
+        y2 = gmin(y2, x.yFull);
+    }
+    double aOld = kFirst ? p.a1[j] : p.a2[j];
+    aOld = gmax(aOld, 0.0001);
+    double length = p.modLength[j];
+
+    // ---- findSurfArea (dwflow.c:417-550) ----
+    int fc;
+    double sa1 = 0.0, sa2 = 0.0;
+    {
+        double d1 = y1, d2 = y2, dMid, w1, w2, wMid, fasnh = 1.0;
+        double yNorm = (d1 + d2) / 2.0;
+        double yCrit = yNorm;
+        if (d1 >= x.yFull && d2 >= x.yFull) fc = F_SUBCRIT;
+        else fc = flowClassOf(p, j, x, f, n1, n2, qLast, h1, h2, y1, y2, &yCrit, &yNorm, &fasnh, ct);
+        switch (fc) {
+        case F_SUBCRIT:
+            dMid = 0.5 * (d1 + d2);
+            if (dMid < 0.0001) dMid = 0.0001;
+            w1 = widthAt(p, x, d1, ct);
+            w2 = widthAt(p, x, d2, ct);
+            wMid = widthAt(p, x, dMid, ct);
+            sa1 = (w1 + wMid) * length / 4.;
+            sa2 = (wMid + w2) * length / 4. * fasnh;
+            break;
+        case F_UP_CRIT:
+            d1 = yCrit;
+            if (yNorm < yCrit) d1 = yNorm;
+            d1 = gmax(d1, 0.0001);
+            h1 = inv1 + p.off1[j] + d1;
+            dMid = 0.5 * (d1 + d2);
+            if (dMid < 0.0001) dMid = 0.0001;
+            w2 = widthAt(p, x, d2, ct);
+            wMid = widthAt(p, x, dMid, ct);
+            sa2 = (wMid + w2) * length * 0.5;
+            break;
+        case F_DN_CRIT:
+            d2 = yCrit;
+            if (yNorm < yCrit) d2 = yNorm;
+            d2 = gmax(d2, 0.0001);
+            h2 = inv2 + p.off2[j] + d2;
+            w1 = widthAt(p, x, d1, ct);
+            dMid = 0.5 * (d1 + d2);
+            if (dMid < 0.0001) dMid = 0.0001;
+            wMid = widthAt(p, x, dMid, ct);
+            sa1 = (w1 + wMid) * length * 0.5;
+            break;
+        case F_UP_DRY:
+            d1 = 0.0001;
+            dMid = 0.5 * (d1 + d2);
+            if (dMid < 0.0001) dMid = 0.0001;
+            w1 = widthAt(p, x, d1, ct);
+            w2 = widthAt(p, x, d2, ct);
+            wMid = widthAt(p, x, dMid, ct);
+            sa2 = (wMid + w2) * length / 4.;
+            if (p.off1[j] <= 0.0) sa1 = (w1 + wMid) * length / 4.;
+            break;
+        case F_DN_DRY:
+            d2 = 0.0001;
+            dMid = 0.5 * (d1 + d2);
+            if (dMid < 0.0001) dMid = 0.0001;
+            w1 = widthAt(p, x, d1, ct);
+            w2 = widthAt(p, x, d2, ct);
+            wMid = widthAt(p, x, dMid, ct);
+            sa1 = (wMid + w1) * length / 4.;
+            if (p.off2[j] <= 0.0) sa2 = (w2 + wMid) * length / 4.;
+            break;
+        default:  // F_DRY
+            sa1 = 0.0001 * length / 2.0;
+            sa2 = sa1;
+            break;
+        }
+        y1 = d1;
+        y2 = d2;
+    }
+    p.sa1[j] = sa1;
+    p.sa2[j] = sa2;
+
+    double wSlot = slotWidth(p, x, y1);
+    double a1 = areaAt(x, y1, wSlot, ct);
+    double r1 = hydRadAt(x, y1, ct);
+    wSlot = slotWidth(p, x, y2);
+    double a2 = areaAt(x, y2, wSlot, ct);
+    double yMid = 0.5 * (y1 + y2);
+    wSlot = slotWidth(p, x, yMid);
+    double aMid = areaAt(x, yMid, wSlot, ct);
+    double rMid = hydRadAt(x, yMid, ct);
+    bool isFull = (y1 >= x.yFull && y2 >= x.yFull);
+    double len0 = p.length[j];
+
+    if (fc == F_DRY || fc == F_UP_DRY || fc == F_DN_DRY || isClosed || aMid <= 0.0001) {
+        double a1n = 0.5 * (a1 + a2);
+        p.a1[j] = a1n;
+        p.q1[j] = 0.0;
+        p.dqdh[j] = 32.2 * dt * aMid / length * barrels;
+        p.froude[j] = 0.0;
+        p.lNewDepth[j] = gmin(yMid, x.yFull);
+        p.lNewVolume[j] = a1n * len0 * barrels;
+        p.lNewFlow[j] = 0.0;
+        p.evapLoss[j] = 0.0;
+        p.seepLoss[j] = 0.0;
+        int old = p.lstate[j];
+        p.lstate[j] = (old & ~0x40F) | fc;    // fullState / normalFlow untouched (dwflow.c:165-180)
+        return;
+    }
+
+    double v = qLast / aMid;
+    if (fabs(v) > 50.) v = 50. * gsgn(qLast);
+    double froude = linkFroude(x, v, yMid, ct);
+    p.froude[j] = froude;
+    if (fc == F_SUBCRIT && froude > 1.0) fc = F_SUPCRIT;
+
+    double sigma;
+    if (froude <= 0.5) sigma = 1.0;
+    else if (froude >= 1.0) sigma = 0.0;
+    else sigma = 2.0 * (1.0 - froude);
+
+    double rho = 1.0;
+    if (!isFull && qLast > 0.0 && h1 >= h2) rho = sigma;
+    double aWtd = a1 + (aMid - a1) * rho;
+    double rWtd = r1 + (rMid - r1) * rho;
+
+    if (p.inertDamping == DAMP_NO) sigma = 1.0;
+    else if (p.inertDamping == DAMP_FULL) sigma = 0.0;
+    if (isFull && !isOpen(x.type)) sigma = 0.0;
+
+    double dq1 = dt * p.roughFactor[j] / pow(rWtd, 1.33333) * fabs(v);
+    double dq2 = dt * 32.2 * aWtd * (h2 - h1) / length;
+    double dq3 = 0.0, dq4 = 0.0;
+    if (sigma > 0.0) {
+        dq3 = 2.0 * v * (aMid - aOld) * sigma;
+        dq4 = dt * v * v * (a2 - a1) / length * sigma;
+    }
+    double dq5 = 0.0;
+    if (f & LF_LOSSES) {                                        // dwflow.c:554-571
+        double losses = 0.0, qa = fabs(qLast);
+        if (a1 > 0.0001) losses += p.cIn[j] * (qa / a1);
+        if (a2 > 0.0001) losses += p.cOut[j] * (qa / a2);
+        if (aMid > 0.0001) losses += p.cAvg[j] * (qa / aMid);
+        dq5 = losses / 2.0 / length * dt;
+    }
+    double dq6 = 0.0;
+    if (f & LF_SEEP) {
+        if (!kFirst) oldDepth = p.lOldDepth[j];
+        (void)oldDepth;
+        dq6 = conduitLossRate(p, j, x, dt, &evapRate, &seepRate, ct) * 2.5 * dt * v / len0;
+    } else {
+        dq6 = 0.0 * 2.5 * dt * v / len0;
+    }
+
+    double denom = 1.0 + dq1 + dq5;
+    double q = (qOld - dq2 + dq3 + dq4 + dq6) / denom;
+    p.dqdh[j] = 1.0 / denom * 32.2 * dt * aWtd / length * barrels;
+
+    int normalFlow = 0;
+    if (q > 0.0) {
+        if (p.normalFlowLtd != NFL_NEITHER && y1 < x.yFull && (fc == F_SUBCRIT || fc == F_SUPCRIT)) {
+            // checkNormalFlow dwflow.c:637-686
+            bool hasOutfall = (f & (LF_N1_OUTFALL | LF_N2_OUTFALL)) != 0;
+            bool check = false;
+            if (p.normalFlowLtd == NFL_SLOPE || p.normalFlowLtd == NFL_BOTH || hasOutfall)
+                if (y1 < y2) check = true;
+            if (!check && (p.normalFlowLtd == NFL_FROUDE || p.normalFlowLtd == NFL_BOTH) && !hasOutfall) {
+                if (y1 > 0.0001 && y2 > 0.0001) {
+                    double f1 = linkFroude(x, q / a1, y1, ct);
+                    if (f1 >= 1.0) check = true;
+                }
+            }
+            if (check) {
+                double qNorm = p.beta[j] * a1 * pow(r1, 2. / 3.);
+                if (qNorm < q) {
+                    normalFlow = 1;
+                    q = qNorm;
+                }
+            }
+        }
+    }
+
+    if (steps > 0) {
+        q = (1.0 - omega) * qLast + omega * q;
+        if (q * qLast < 0.0) q = 0.001 * gsgn(q);
+    }
+    if (f & LF_QLIMIT) {
+        double ql = p.qLimit[j];
+        if (fabs(q) > ql) q = gsgn(q) * ql;
+    }
+    // link_setFlapGate (link.c:643-670)
+    {
+        bool closed = false;
+        if (f & LF_FLAP) {
+            double dir = (f & LF_DIRNEG) ? -1.0 : 1.0;
+            if (q * dir < 0.0) closed = true;
+        }
+        if (!closed) {
+            if (q < 0.0 && (f & LF_N2_OFLAP)) closed = true;
+            if (q > 0.0 && (f & LF_N1_OFLAP)) closed = true;
+        }
+        if (closed) q = 0.0;
+    }
+    if (q > 0.0001 && p.nNewDepth[n1] <= 0.0001) q = 0.0001;
+    if (q < -0.0001 && p.nNewDepth[n2] <= 0.0001) q = -0.0001;
+
+    p.a1[j] = aMid;
+    p.q1[j] = q;
+    p.lNewDepth[j] = gmin(yMid, x.yFull);
+    double aAvg = (a1 + a2) / 2.0;
+    int fs = 0;
+    if (a1 >= x.aFull) fs = (a2 >= x.aFull) ? FS_ALL_FULL : FS_UP_FULL;
+    else if (a2 >= x.aFull) fs = FS_DN_FULL;
+    p.lNewVolume[j] = aAvg * len0 * barrels;
+    p.lNewFlow[j] = q * barrels;
+    p.evapLoss[j] = evapRate;
+    p.seepLoss[j] = seepRate;
+    int old = p.lstate[j];
+    p.lstate[j] = (old & (1 << 9)) | fc | (fs << 4) | (normalFlow << 8);
+}
+
+// ===========================================================================
+//  kernels
+// ===========================================================================
+__device__ __forceinline__ void stageTables(double* ct, const double* g)
+{
+    for (int i = threadIdx.x; i < 5 * SWX_CIRC_N; i += blockDim.x) ct[i] = g[i];
+    __syncthreads();
+}
+
+template <bool kFirst>
+__global__ __launch_bounds__(kBlock) void k_link(Params p, int k)
+{
+    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;     // converged: dynwave.c:249-251
+    __shared__ double ct[5 * SWX_CIRC_N];
+    stageTables(ct, p.gTables);
+    double dt = p.ctl->dt;
+    for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nL; j += gridDim.x * kBlock) {
+        if (k >= 2) {                                      // findBypassedLinks dynwave.c:335-345
+            int2 nn = p.lnodes[j];
+            if (p.conv[nn.x] && p.conv[nn.y]) continue;
+        }
+        conduitFlow<kFirst>(p, j, k, dt, ct);
+    }
+}
+
+// link_setOutfallDepth + outfall_setOutletDepth (link.c:728-766, node.c:1413-1492)
+__device__ double outfallDepth(const Params& p, int i, uint32_t nf, int j)
+{
+    const double* ct = p.gTables;
+    uint32_t f = p.lflags[j];
+    Geom x = loadGeom(p, j, f);
+    double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
+    int2 nn = p.lnodes[j];
+    double z = (nn.y == i) ? p.off2[j] : p.off1[j];
+    double q = fabs(p.lNewFlow[j] / barrels);
+    double yNorm = linkYnorm(x, q, p.qMax[j], p.beta[j], ct);
+    double yCrit = getYcrit(x, q, ct);
+    int ot = (int)((nf >> NF_OTYPE_SHIFT) & 0x7);
+    double inv = p.invert[i];
+    if (ot == O_FREE) return (z > 0.0) ? 0.0 : gmin(yNorm, yCrit);
+    if (ot == O_NORMAL) return (z > 0.0) ? 0.0 : yNorm;
+    double stage = (ot == O_FIXED) ? p.fixedStage[i] : inv;
+    yCrit = gmin(yCrit, yNorm);
+    double yNew;
+    if (yCrit + z + inv < stage) yNew = stage - inv;
+    else if (z > 0.0) {
+        if (stage < inv + z) yNew = gmax(0.0, (stage - inv));
+        else yNew = z + yCrit;
+    } else yNew = yCrit;
+    return yNew;
+}
+
+template <bool kFirst>
+__global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
+{
+    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
+    const double dt = p.ctl->dt;
+    const double omega = 0.5;
+    bool anyUnconv = false;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
+        uint32_t nf = p.nflags[i];
+        int type = (int)(nf & NF_TYPE);
+        double yLast = p.nNewDepth[i];
+        double yOld, lat;
+        if (kFirst) {
+            // routing.c:328-332, node.c:293-304, 325-341 -- step-begin rotation
+            double inflowPrev = p.inflow[i], outflowPrev = p.outflow[i];
+            yOld = yLast;
+            p.nOldDepth[i] = yOld;
+            p.nOldVolume[i] = p.nNewVolume[i];
+            p.oldFlowInflow[i] = inflowPrev;
+            p.oldNetInflow[i] = inflowPrev - outflowPrev;
+            p.oldLat[i] = p.newLat[i];
+            lat = p.latIn[i];
+            p.newLat[i] = lat;
+        } else {
+            yOld = p.nOldDepth[i];
+            lat = p.newLat[i];
+        }
+        // initNodeStates (dynwave.c:297-331)
+        bool canPond = (nf & NF_CANPOND) != 0;
+        double fullDepth = p.fullDepth[i];
+        double surf = 0.0;
+        if (canPond && yLast > fullDepth) surf = p.pondedArea[i];
+        double inflow = 0.0, outflow = 0.0;   // node losses are 0 for non-storage nodes
+        if (lat >= 0.0) inflow += lat;
+        else outflow -= lat;
+        double sumdqdh = 0.0;
+        // CSR gather in link-index order == updateNodeFlows serial order
+        int e0 = p.rowptr[i], e1 = p.rowptr[i + 1];
+        for (int e = e0; e < e1; e++) {
+            int ent = p.csr[e];
+            int l = ent & 0x7FFFFFFF;
+            bool isN2 = ent < 0;
+            double q = p.lNewFlow[l];
+            uint32_t lf = p.lflags[l];
+            double barrels = (double)((lf >> LF_BARREL_SHIFT) & 0xFF);
+            if (!isN2) {
+                if (q >= 0.0) outflow += q; else inflow -= q;
+            } else {
+                if (q >= 0.0) inflow += q; else outflow -= q;
+            }
+            if (lf & LF_SEEP) {
+                double lossRate = (p.evapLoss[l] + p.seepLoss[l]) * barrels;
+                if (lossRate > 0.0) {
+                    bool o1 = (lf & LF_N1_OUTFALL) != 0, o2 = (lf & LF_N2_OUTFALL) != 0;
+                    if (!o1 && !o2) lossRate /= 2.0;
+                    if (!isN2 && !o1) outflow += lossRate;
+                    if (isN2 && !o2) outflow += lossRate;
+                }
+            }
+            surf += (isN2 ? p.sa2[l] : p.sa1[l]) * barrels;
+            sumdqdh += p.dqdh[l];
+        }
+        p.inflow[i] = inflow;
+        p.outflow[i] = outflow;
+        if (type == OUTFALL) {
+            int l = p.outfallLink[i];
+            if (l >= 0) p.nNewDepth[i] = outfallDepth(p, i, nf, l);
+            continue;
+        }
+        // setNodeDepth (dynwave.c:636-762)
+        bool isPonded = (canPond && yLast > fullDepth);
+        double yCrown = p.yCrown[i];
+        double overflow = 0.0;
+        double surfArea = gmax(surf, p.minSurfArea);
+        double dQ = inflow - outflow;
+        double dV = 0.5 * (p.oldNetInflow[i] + dQ) * dt;
+        bool isSurcharged = false;
+        if (p.surchargeMethod == SUR_EXTRAN) {
+            if (isPonded) isSurcharged = false;
+            else isSurcharged = (yCrown > 0.0 && yLast > yCrown);
+        }
+        double yNew, dy;
+        if (!isSurcharged) {
+            dy = dV / surfArea;
+            yNew = yOld + dy;
+            if (!isPonded) p.oldSurfArea[i] = surfArea;
+            if (k > 0) yNew = (1.0 - omega) * yLast + omega * yNew;
+            if (isPonded && yNew < fullDepth) yNew = fullDepth - 0.0001;
+        } else {
+            double corr = (nf & NF_DEGNEG) ? 0.6 : 1.0;
+            double denom = sumdqdh;
+            if (yLast < 1.25 * yCrown) {
+                double fr = (yLast - yCrown) / yCrown;
+                denom += (p.oldSurfArea[i] / dt - sumdqdh) * exp(-15.0 * fr);
+            }
+            if (denom == 0.0) dy = 0.0;
+            else dy = corr * dQ / denom;
+            yNew = yLast + dy;
+            if (yNew < yCrown) yNew = yCrown - 0.0001;
+            if (canPond && yNew > fullDepth) yNew = fullDepth + 0.0001;
+        }
+        if (yNew < 0) yNew = 0.0;
+        double yMax = fullDepth;
+        if (!canPond) yMax += p.surDepth[i];
+        double fullVolume = p.fullVolume[i];
+        if (yNew > yMax) {                                 // getFloodedDepth dynwave.c:766-795
+            double newVolume;
+            if (!canPond) {
+                overflow = dV / dt;
+                newVolume = fullVolume;
+                yNew = yMax;
+            } else {
+                double oldVolume = p.nOldVolume[i];
+                newVolume = gmax((oldVolume + dV), fullVolume);
+                overflow = (newVolume - gmax(oldVolume, fullVolume)) / dt;
+            }
+            if (overflow < 0.0001) overflow = 0.0;
+            p.nNewVolume[i] = newVolume;
+        } else {
+            p.nNewVolume[i] = (fullDepth > 0.0) ? fullVolume * (yNew / fullDepth) : 0.0;
+        }
+        p.overflow[i] = overflow;
+        p.dYdT[i] = fabs(yNew - yOld) / dt;
+        p.nNewDepth[i] = yNew;
+        int c = (fabs(yLast - yNew) > p.headTol) ? 0 : 1;  // dynwave.c:615-621
+        p.conv[i] = c;
+        if (!c) anyUnconv = true;
+    }
+    // one flag per iteration; any writer stores 1 (no atomics needed)
+    if (__any(anyUnconv) && (threadIdx.x & 63) == 0) p.ctl->unconv[k] = 1;
+}
+
+// qualrout.c:146-174, 498-518
+__device__ __forceinline__ double mixedQual(double c, double v1, double wIn, double qIn, double tStep)
+{
+    if (qIn <= 1.E-10) return c;
+    double vIn = qIn * tStep;
+    double cIn = wIn * tStep / vIn;
+    double cMax = gmax(c, cIn);
+    c = (c * v1 + wIn * tStep) / (v1 + vIn);
+    c = gmin(c, cMax);
+    c = gmax(c, 0.0);
+    return c;
+}
+__device__ __forceinline__ double reactedQual(double kDecay, double c, double tStep)
+{
+    if (kDecay == 0.0) return c;
+    double c2 = c * (1.0 - kDecay * tStep);
+    return gmax(0.0, c2);
+}
+
+// qualrout.c:100-142 -- node part: link mass flows (findLinkMassFlow, link
+// order) + node quality (findNodeQual / findStorageQual); rotates node quality.
+__global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
+{
+    const double dt = p.ctl->dt;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
+        double qIn = p.inflow[i];
+        double oldVol = p.nOldVolume[i];
+        int e0 = p.rowptr[i], e1 = p.rowptr[i + 1];
+        for (int pp = 0; pp < p.P; pp++) {
+            size_t ni = (size_t)pp * p.nN + i;
+            double cOld = p.nNewQual[ni];           // node_setOldQualState
+            p.nOldQual[ni] = cOld;
+            double w = p.qualIn[ni];
+            for (int e = e0; e < e1; e++) {
+                int ent = p.csr[e];
+                int l = ent & 0x7FFFFFFF;
+                bool isN2 = ent < 0;
+                double ql = p.lNewFlow[l];
+                bool down = isN2 ? !(ql < 0.0) : (ql < 0.0);
+                if (down) w += fabs(ql) * p.lNewQual[(size_t)pp * p.nL + l];
+            }
+            double c;
+            if (oldVol > 0.0353147) {
+                double c1 = reactedQual(p.kDecay[pp], cOld, dt);
+                c = mixedQual(c1, oldVol, w, qIn, dt);
+                if ((p.nNewVolume[i] <= 0.0353147 || p.nNewDepth[i] <= 0.003281) && qIn <= 1.E-10) c = 0.0;
+            } else if (qIn > 1.E-10) {
+                c = w / qIn;
+            } else {
+                c = (p.nNewDepth[i] > 0.003281) ? cOld : 0.0;
+            }
+            p.nNewQual[ni] = c;
+        }
+    }
+}
+
+// qualrout.c:253-353 (DW) -- link quality; rotates link quality.
+__global__ __launch_bounds__(kBlock) void k_qual_link(Params p)
+{
+    const double dt = p.ctl->dt;
+    for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nL; j += gridDim.x * kBlock) {
+        int2 nn = p.lnodes[j];
+        double nf = p.lNewFlow[j];
+        int up = (nf < 0.0) ? nn.y : nn.x;
+        uint32_t f = p.lflags[j];
+        double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
+        double qIn = fabs(p.q1[j]) * barrels;
+        double qSeep = p.seepLoss[j] * barrels;
+        double vEvap = p.evapLoss[j] * barrels * dt;
+        double v1 = p.lOldVolume[j], v2 = p.lNewVolume[j];
+        double vLosses = qSeep * dt + vEvap;
+        double fEvap = 1.0;
+        if (vEvap > 0.0 && v1 > 0.0353147) fEvap += vEvap / v1;
+        qIn = qIn + (v2 + vLosses - v1) / dt;
+        qIn = gmax(qIn, 0.0);
+        bool dry = (v2 < 0.0353147 || p.lNewDepth[j] <= 0.003281);
+        for (int pp = 0; pp < p.P; pp++) {
+            size_t li = (size_t)pp * p.nL + j;
+            double c1 = p.lNewQual[li];
+            p.lOldQual[li] = c1;
+            c1 *= fEvap;
+            double c2 = reactedQual(p.kDecay[pp], c1, dt);
+            double wIn = p.nNewQual[(size_t)pp * p.nN + up] * qIn;
+            c2 = mixedQual(c2, v1, wIn, qIn, dt);
+            if (dry) c2 = 0.0;
+            p.lNewQual[li] = c2;
+        }
+    }
+}
+
+// Step end: findLimitedLinks (dynwave.c:349-378), removeConduitLosses /
+// removeOutflows (routing.c:841-925, node.c:438-493), Courant partials
+// (dynwave.c:836-921).  Block partials:
+//   [0] outflow rate  [1] flooding rate  [2] extra external inflow
+//   [3] evap loss     [4] seep loss      [5] min link step  [6] min node step
+__global__ __launch_bounds__(kBlock) void k_step_end(Params p)
+{
+    __shared__ double red[kNumPartials][kBlock / 64];
+    double acc[kNumPartials];
+    for (int q = 0; q < kNumPartials; q++) acc[q] = 0.0;
+    double tLink = p.routeStep, tNode = p.routeStep;
+    int n = gridDim.x * kBlock;
+    int tid = blockIdx.x * kBlock + threadIdx.x;
+    // links (fixed order within a thread: j = tid, tid + n, ...)
+    for (int j = tid; j < p.nL; j += n) {
+        uint32_t f = p.lflags[j];
+        double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
+        int s = p.lstate[j] & ~(1 << 9);
+        double a1 = p.a1[j];
+        if (a1 >= p.aFull[j]) {
+            int2 nn = p.lnodes[j];
+            double h1 = p.nNewDepth[nn.x] + p.inv1[j];
+            double h2 = p.nNewDepth[nn.y] + p.inv2[j];
+            if ((h1 - h2) > fabs(p.slope[j]) * p.length[j]) s |= (1 << 9);
+        }
+        p.lstate[j] = s;
+        acc[3] += p.evapLoss[j] * barrels;
+        acc[4] += p.seepLoss[j] * barrels;
+        if (p.varStep) {
+            double q = fabs(p.lNewFlow[j]) / barrels;
+            double fr = p.froude[j];
+            if (!(q <= 0.0001 || a1 <= 0.0001 || fr <= 0.01)) {
+                double t = p.lNewVolume[j] / barrels / q;
+                t = t * p.modLength[j] / p.length[j];
+                t = t * fr / (1.0 + fr) * p.courantFactor;
+                if (t < tLink) tLink = t;
+            }
+        }
+    }
+    for (int i = tid; i < p.nN; i += n) {
+        uint32_t nf = p.nflags[i];
+        int type = (int)(nf & NF_TYPE);
+        double q = 0.0;
+        bool flooded = false;
+        if (type == OUTFALL) {
+            double in = p.inflow[i], out = p.outflow[i];
+            if (out == 0.0) q = in;
+            else if (in == 0.0) {
+                q = -out;
+                p.inflow[i] = fabs(q);
+            }
+            p.overflow[i] = 0.0;
+            p.nNewVolume[i] = 0.0;
+        } else {
+            if (p.nNewVolume[i] <= p.fullVolume[i]) q = p.overflow[i];
+            if (q > 0.0) flooded = true;
+        }
+        if (q > 0.0) {
+            if (flooded) acc[1] += q; else acc[0] += q;
+        } else {
+            acc[2] += -q;
+        }
+        if (p.varStep && type != OUTFALL) {
+            double y = p.nNewDepth[i];
+            double yc = p.crownElev[i] - p.invert[i];
+            if (!(y <= 0.0001) && !(y + 0.0001 >= yc)) {
+                double maxDepth = yc * 0.25;
+                double d = p.dYdT[i];
+                if (!(maxDepth < 0.0001) && !(d < 0.0001)) {
+                    double t1 = maxDepth / d;
+                    if (t1 < tNode) tNode = t1;
+                }
+            }
+        }
+    }
+    acc[5] = tLink;
+    acc[6] = tNode;
+    // wave reduction (fixed butterfly order), then wave partials in LDS
+    int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int q = 0; q < kNumPartials; q++) {
+        double v = acc[q];
+        for (int off = 32; off > 0; off >>= 1) {
+            double o = __shfl_down(v, off, 64);
+            if (q == 5 || q == 6) v = (o < v) ? o : v; else v += o;
+        }
+        if (lane == 0) red[q][wv] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kNumPartials) {
+        int q = threadIdx.x;
+        double v = red[q][0];
+        for (int w = 1; w < kBlock / 64; w++) {
+            if (q == 5 || q == 6) v = (red[q][w] < v) ? red[q][w] : v; else v += red[q][w];
+        }
+        p.partials[(size_t)blockIdx.x * kNumPartials + q] = v;
+    }
+}
+
+// single-block finalisation (fixed-order reductions -> deterministic)
+__global__ void k_finalize(Params p)
+{
+    __shared__ double sum[kNumPartials][kBlock];
+    int t = threadIdx.x;
+    double acc[kNumPartials];
+    for (int q = 0; q < kNumPartials; q++) acc[q] = (q == 5 || q == 6) ? 1.0e300 : 0.0;
+    for (int b = t; b < p.nBlocksEnd; b += kBlock)
+        for (int q = 0; q < kNumPartials; q++) {
+            double v = p.partials[(size_t)b * kNumPartials + q];
+            if (q == 5 || q == 6) acc[q] = (v < acc[q]) ? v : acc[q]; else acc[q] += v;
+        }
+    for (int q = 0; q < kNumPartials; q++) sum[q][t] = acc[q];
+    __syncthreads();
+    if (t != 0) return;
+    double tot[kNumPartials];
+    for (int q = 0; q < kNumPartials; q++) {
+        double v = sum[q][0];
+        for (int i = 1; i < kBlock; i++) {
+            if (q == 5 || q == 6) v = (sum[q][i] < v) ? sum[q][i] : v; else v += sum[q][i];
+        }
+        tot[q] = v;
+    }
+    StepCtl* c = p.ctl;
+    // Picard step count / convergence (dynwave.c:242-257)
+    int steps;
+    bool converged;
+    if (p.maxTrials <= 1) { steps = p.maxTrials < 1 ? 0 : 1; converged = false; }
+    else {
+        steps = 2;
+        while (steps < p.maxTrials && c->unconv[steps - 1]) steps++;
+        converged = (c->unconv[steps - 1] == 0);
+    }
+    c->lastSteps = steps;
+    c->totalSteps += 1;
+    c->totalIters += steps;
+    if (!converged) c->nonConverge += 1;
+    for (int k = 0; k < kMaxTrialsCap; k++) c->unconv[k] = 0;
+    // mass balance: massbal_updateRoutingTotals(dt/2) at both ends of the step
+    double half = c->dt / 2.;
+    double step[kNumPartials] = {c->latTot[0], c->latTot[1] + tot[2], tot[1], c->latTot[2] + tot[0],
+                                 tot[3], tot[4], 0, 0};
+    for (int q = 0; q < 6; q++) {
+        c->flowTot[q] += c->prevStepTot[q] * half;
+        c->flowTot[q] += step[q] * half;
+        c->prevStepTot[q] = step[q];
+    }
+    // advance the clock (routing.c:301-302)
+    c->newRoutingTime = c->newRoutingTime + 1000.0 * c->dt;
+    // step length of the next step: dynwave_getRoutingStep (dynwave.c:195-220,
+    // 799-832) then execRouting's end-of-run clamp (swmm5.c:538-546)
+    double dtn = c->routeStep;
+    if (p.varStep) {
+        double tMin = tot[5];
+        if (tot[6] < tMin) tMin = tot[6];
+        if (tMin < p.minRouteStep) tMin = p.minRouteStep;
+        c->variableStep = floor(1000.0 * tMin) / 1000.0;
+        dtn = c->variableStep;
+    }
+    c->dtNext = dtn;
+    if (c->newRoutingTime + 1000.0 * dtn > c->routingDuration) {
+        dtn = (c->routingDuration - c->newRoutingTime) / 1000.0;
+        dtn = (dtn >= 1. / 1000.0) ? dtn : 1. / 1000.0;
+    }
+    c->dt = dtn;
+}
+
+// ===========================================================================
+//  Router implementation
+// ===========================================================================
+struct Router::Impl {
+    Params p{};
+    hipStream_t stream = nullptr;
+    hipGraphExec_t graph = nullptr;
+    bool useGraph = true;
+    bool timing = false;
+    int gridL = 1, gridN = 1, gridEnd = 1;
+    std::vector<void*> allocs;
+    double* latBase = nullptr;       // constant lateral inflows
+    double* qualBase = nullptr;
+    double* hostPinned = nullptr;    // staging for uploads
+    size_t pinnedSize = 0;
+    StepCtl* ctl = nullptr;
+    StepCtl* hostCtl = nullptr;      // pinned
+    bool constantInflow = true;
+    std::vector<hipEvent_t> ev;      // timing events
+    double kms[4] = {0, 0, 0, 0};
+    long long kcnt[4] = {0, 0, 0, 0};
+    double kbytes[4] = {0, 0, 0, 0};
+    int nE = 0;
+    bool tableShapes = true;
+    static constexpr int kRing = 4;
+    hipEvent_t ringEv[kRing] = {};
+    int ringNext = 0;
+    size_t slotDoubles = 0;
+    double lastDtHost = 0.0;
+    double latTot0[3] = {0, 0, 0};
+};
+
+Router::Router() : d_(new Impl) {}
+Router::~Router()
+{
+    if (d_) {
+        if (d_->graph) hipGraphExecDestroy(d_->graph);
+        for (auto e : d_->ev) hipEventDestroy(e);
+        for (void* a : d_->allocs) hipFree(a);
+        if (d_->hostPinned) hipHostFree(d_->hostPinned);
+        if (d_->hostCtl) hipHostFree(d_->hostCtl);
+        if (d_->stream) hipStreamDestroy(d_->stream);
+        delete d_;
+    }
+}
+
+template <class T>
+static T* devAlloc(Router::Impl* d, size_t n, hipError_t* err)
+{
+    void* ptr = nullptr;
+    *err = hipMalloc(&ptr, std::max<size_t>(n, 1) * sizeof(T));
+    if (*err == hipSuccess) d->allocs.push_back(ptr);
+    return (T*)ptr;
+}
+
+static void launchIteration(Router::Impl* d, int k)
+{
+    Params& p = d->p;
+    if (k == 0) {
+        hipLaunchKernelGGL(k_link<true>, dim3(d->gridL), dim3(kBlock), 0, d->stream, p, k);
+    } else {
+        hipLaunchKernelGGL(k_link<false>, dim3(d->gridL), dim3(kBlock), 0, d->stream, p, k);
+    }
+    if (d->timing) hipEventRecord(d->ev[2 * k + 1], d->stream);
+    if (k == 0) {
+        hipLaunchKernelGGL(k_node<true>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
+    } else {
+        hipLaunchKernelGGL(k_node<false>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
+    }
+    if (d->timing) hipEventRecord(d->ev[2 * k + 2], d->stream);
+}
+
+static void launchStep(Router::Impl* d)
+{
+    Params& p = d->p;
+    if (d->timing) hipEventRecord(d->ev[0], d->stream);
+    for (int k = 0; k < p.maxTrials; k++) launchIteration(d, k);
+    int base = 2 * p.maxTrials + 1;
+    if (p.P > 0) {
+        hipLaunchKernelGGL(k_qual_node, dim3(d->gridN), dim3(kBlock), 0, d->stream, p);
+        hipLaunchKernelGGL(k_qual_link, dim3(d->gridL), dim3(kBlock), 0, d->stream, p);
+    }
+    if (d->timing) hipEventRecord(d->ev[base], d->stream);
+    hipLaunchKernelGGL(k_step_end, dim3(d->gridEnd), dim3(kBlock), 0, d->stream, p);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, d->stream, p);
+    if (d->timing) hipEventRecord(d->ev[base + 1], d->stream);
+}
+
+int Router::init(Project& prj, int device)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    Network& net = prj.net;
+    State& st = prj.st;
+    int nN = net.nNodes(), nL = net.nLinks(), P = prj.opt.ignoreQuality ? 0 : net.nPollut();
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        fail("no HIP device available (the MI355X engine has no CPU fallback)");
+        return err_;
+    }
+    if (device < 0 || device >= ndev) device = 0;
+    HIPCHECK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPCHECK(hipGetDeviceProperties(&prop, device));
+    devName_ = std::string("hip:") + prop.gcnArchName + ":" + prop.name;
+    HIPCHECK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+
+    Params& p = d->p;
+    p.nN = nN; p.nL = nL; p.P = P;
+    p.maxTrials = std::min(prj.opt.maxTrials, kMaxTrialsCap);
+    p.surchargeMethod = prj.opt.surchargeMethod;
+    p.inertDamping = prj.opt.inertDamping;
+    p.normalFlowLtd = prj.opt.normalFlowLtd;
+    p.allowPonding = prj.opt.allowPonding;
+    p.crownCutoff = prj.opt.crownCutoff;
+    p.minSurfArea = prj.opt.minSurfArea;
+    p.headTol = prj.opt.headTol;
+    p.evapRate = prj.opt.evapRate;
+    p.courantFactor = prj.opt.courantFactor;
+    p.minRouteStep = prj.opt.minRouteStep;
+    p.routeStep = prj.opt.routeStep;
+    p.varStep = (prj.opt.courantFactor != 0.0 && prj.opt.routeStep >= 0.001) ? 1 : 0;
+
+    hipError_t e;
+    auto upD = [&](const std::vector<double>& v, size_t n) -> double* {
+        double* ptr = devAlloc<double>(d, n, &e);
+        if (e == hipSuccess && n) e = hipMemcpy(ptr, v.data(), n * sizeof(double), hipMemcpyHostToDevice);
+        return ptr;
+    };
+    auto upI = [&](const std::vector<int>& v, size_t n) -> int* {
+        int* ptr = devAlloc<int>(d, n, &e);
+        if (e == hipSuccess && n) e = hipMemcpy(ptr, v.data(), n * sizeof(int), hipMemcpyHostToDevice);
+        return ptr;
+    };
+#define UPD(dst, vec, n) do { dst = upD(vec, n); if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; } } while (0)
+#define UPI(dst, vec, n) do { dst = upI(vec, n); if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; } } while (0)
+
+    // ---- link static ------------------------------------------------------
+    std::vector<int> nodes2((size_t)nL * 2);
+    std::vector<int> lflags(nL);
+    std::vector<double> inv1(nL), inv2(nL), xd[11];
+    for (auto& v : xd) v.resize(nL);
+    for (int j = 0; j < nL; j++) {
+        if (net.linkType[j] != CONDUIT) { fail("only conduit links are supported"); return err_; }
+        int n1 = net.node1[j], n2 = net.node2[j];
+        nodes2[2 * j] = n1;
+        nodes2[2 * j + 1] = n2;
+        inv1[j] = net.invertElev[n1];
+        inv2[j] = net.invertElev[n2];
+        const Xsect& x = net.xsect[j];
+        uint32_t f = (uint32_t)x.type & LF_XTYPE;
+        f |= ((uint32_t)net.barrels[j] & 0xFFu) << LF_BARREL_SHIFT;
+        if (net.hasLosses[j]) f |= LF_LOSSES;
+        if (net.hasFlapGate[j]) f |= LF_FLAP;
+        if (net.nodeType[n1] == OUTFALL) { f |= LF_N1_OUTFALL; if (net.outfallFlap[n1]) f |= LF_N1_OFLAP; }
+        if (net.nodeType[n2] == OUTFALL) { f |= LF_N2_OUTFALL; if (net.outfallFlap[n2]) f |= LF_N2_OFLAP; }
+        if (net.seepRate[j] > 0.0 || (prj.opt.evapRate > 0.0 && isOpen(x.type))) f |= LF_SEEP;
+        if (net.qLimit[j] > 0.0) f |= LF_QLIMIT;
+        if (net.direction[j] < 0) f |= LF_DIRNEG;
+        lflags[j] = (int)f;
+        xd[0][j] = x.yFull; xd[1][j] = x.wMax; xd[2][j] = x.ywMax; xd[3][j] = x.aFull;
+        xd[4][j] = x.rFull; xd[5][j] = x.sFull; xd[6][j] = x.sMax; xd[7][j] = x.yBot;
+        xd[8][j] = x.aBot; xd[9][j] = x.sBot; xd[10][j] = x.rBot;
+    }
+    {
+        int* ptr = upI(nodes2, nodes2.size());
+        if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+        p.lnodes = (const int2*)ptr;
+        int* fl;
+        UPI(fl, lflags, nL);
+        p.lflags = (const uint32_t*)fl;
+    }
+    double* tmp;
+    UPD(tmp, inv1, nL); p.inv1 = tmp;
+    UPD(tmp, inv2, nL); p.inv2 = tmp;
+    UPD(tmp, net.offset1, nL); p.off1 = tmp;
+    UPD(tmp, net.offset2, nL); p.off2 = tmp;
+    UPD(tmp, xd[0], nL); p.yFull = tmp;
+    UPD(tmp, xd[1], nL); p.wMax = tmp;
+    UPD(tmp, xd[2], nL); p.ywMax = tmp;
+    UPD(tmp, xd[3], nL); p.aFull = tmp;
+    UPD(tmp, xd[4], nL); p.rFull = tmp;
+    UPD(tmp, xd[5], nL); p.sFull = tmp;
+    UPD(tmp, xd[6], nL); p.sMax = tmp;
+    UPD(tmp, xd[7], nL); p.yBot = tmp;
+    UPD(tmp, xd[8], nL); p.aBot = tmp;
+    UPD(tmp, xd[9], nL); p.sBot = tmp;
+    UPD(tmp, xd[10], nL); p.rBot = tmp;
+    UPD(tmp, net.length, nL); p.length = tmp;
+    UPD(tmp, net.modLength, nL); p.modLength = tmp;
+    UPD(tmp, net.roughFactor, nL); p.roughFactor = tmp;
+    UPD(tmp, net.beta, nL); p.beta = tmp;
+    UPD(tmp, net.qMax, nL); p.qMax = tmp;
+    UPD(tmp, net.qLimit, nL); p.qLimit = tmp;
+    UPD(tmp, net.slope, nL); p.slope = tmp;
+    UPD(tmp, net.cLossInlet, nL); p.cIn = tmp;
+    UPD(tmp, net.cLossOutlet, nL); p.cOut = tmp;
+    UPD(tmp, net.cLossAvg, nL); p.cAvg = tmp;
+    UPD(tmp, net.seepRate, nL); p.seepRate = tmp;
+    // ---- link dynamic -----------------------------------------------------
+    UPD(p.lNewFlow, st.lNewFlow, nL);
+    UPD(p.lOldFlow, st.lOldFlow, nL);
+    UPD(p.lNewDepth, st.lNewDepth, nL);
+    UPD(p.lOldDepth, st.lOldDepth, nL);
+    UPD(p.lNewVolume, st.lNewVolume, nL);
+    UPD(p.lOldVolume, st.lOldVolume, nL);
+    UPD(p.a1, st.a1, nL);
+    UPD(p.a2, st.a2, nL);
+    UPD(p.q1, st.q1, nL);
+    UPD(p.dqdh, st.dqdh, nL);
+    UPD(p.froude, st.froude, nL);
+    UPD(p.sa1, st.surfArea1, nL);
+    UPD(p.sa2, st.surfArea2, nL);
+    UPD(p.evapLoss, st.evapLossRate, nL);
+    UPD(p.seepLoss, st.seepLossRate, nL);
+    UPD(p.setting, st.setting, nL);
+    {
+        std::vector<int> ls(nL);
+        for (int j = 0; j < nL; j++)
+            ls[j] = st.flowClass[j] | (st.fullState[j] << 4) | (st.normalFlow[j] << 8) |
+                    (st.capacityLimited[j] << 9);
+        UPI(p.lstate, ls, nL);
+    }
+    // ---- node static ------------------------------------------------------
+    std::vector<int> nflags(nN), outLink(nN, -1);
+    std::vector<double> yCrown(nN);
+    for (int i = 0; i < nN; i++) {
+        uint32_t f = (uint32_t)net.nodeType[i] & NF_TYPE;
+        if (net.nodeType[i] == OUTFALL) f |= ((uint32_t)net.outfallType[i] & 0x7u) << NF_OTYPE_SHIFT;
+        if (net.degree[i] < 0) f |= NF_DEGNEG;
+        if (prj.opt.allowPonding && net.pondedArea[i] > 0.0) f |= NF_CANPOND;
+        nflags[i] = (int)f;
+        yCrown[i] = net.crownElev[i] - net.invertElev[i];
+        if (net.nodeType[i] == OUTFALL && net.outfallType[i] > O_FIXED) {
+            fail("TIMESERIES outfalls are not supported on the device yet");
+            return err_;
+        }
+    }
+    // CSR: incident links per node, ascending link index (all links are true
+    // conduits, so this is exactly the order of dynwave.c:398-401)
+    std::vector<int> rowptr(nN + 1, 0), csr;
+    for (int j = 0; j < nL; j++) { rowptr[net.node1[j] + 1]++; rowptr[net.node2[j] + 1]++; }
+    for (int i = 0; i < nN; i++) rowptr[i + 1] += rowptr[i];
+    csr.resize(rowptr[nN]);
+    {
+        std::vector<int> fillp(rowptr.begin(), rowptr.end() - 1);
+        for (int j = 0; j < nL; j++) {
+            csr[fillp[net.node1[j]]++] = j;
+            csr[fillp[net.node2[j]]++] = (int)((unsigned)j | 0x80000000u);
+            // the reference's link_setOutfallDepth loop: last link touching an
+            // outfall wins (validateGeneralLayout allows only one)
+            if (net.nodeType[net.node2[j]] == OUTFALL) outLink[net.node2[j]] = j;
+            else if (net.nodeType[net.node1[j]] == OUTFALL) outLink[net.node1[j]] = j;
+        }
+    }
+    d->nE = (int)csr.size();
+    {
+        int* fl;
+        UPI(fl, nflags, nN);
+        p.nflags = (const uint32_t*)fl;
+        int* rp;
+        UPI(rp, rowptr, nN + 1); p.rowptr = rp;
+        UPI(rp, csr, csr.size()); p.csr = rp;
+        UPI(rp, outLink, nN); p.outfallLink = rp;
+    }
+    UPD(tmp, net.invertElev, nN); p.invert = tmp;
+    UPD(tmp, net.fullDepth, nN); p.fullDepth = tmp;
+    UPD(tmp, net.surDepth, nN); p.surDepth = tmp;
+    UPD(tmp, net.pondedArea, nN); p.pondedArea = tmp;
+    UPD(tmp, yCrown, nN); p.yCrown = tmp;
+    UPD(tmp, net.crownElev, nN); p.crownElev = tmp;
+    UPD(tmp, net.fullVolume, nN); p.fullVolume = tmp;
+    UPD(tmp, net.fixedStage, nN); p.fixedStage = tmp;
+    // ---- node dynamic -----------------------------------------------------
+    UPD(p.nNewDepth, st.newDepth, nN);
+    UPD(p.nOldDepth, st.oldDepth, nN);
+    UPD(p.nNewVolume, st.newVolume, nN);
+    UPD(p.nOldVolume, st.oldVolume, nN);
+    UPD(p.inflow, st.inflow, nN);
+    UPD(p.outflow, st.outflow, nN);
+    UPD(p.overflow, st.overflow, nN);
+    UPD(p.newLat, st.newLatFlow, nN);
+    UPD(p.oldLat, st.oldLatFlow, nN);
+    UPD(p.oldNetInflow, st.oldNetInflow, nN);
+    UPD(p.oldFlowInflow, st.oldFlowInflow, nN);
+    UPD(p.oldSurfArea, st.oldSurfArea, nN);
+    UPD(p.dYdT, st.dYdT, nN);
+    UPI(p.conv, st.converged, nN);
+    // ---- inflows ----------------------------------------------------------
+    d->constantInflow = prj.inflowsAreConstant();
+    {
+        std::vector<double> lat, qual;
+        double tot[3];
+        prj.evalInflows(prj.getDateTime(0.0), lat, P ? &qual : nullptr, &tot[0], &tot[1], &tot[2]);
+        d->latTot0[0] = tot[0]; d->latTot0[1] = tot[1]; d->latTot0[2] = tot[2];
+        UPD(d->latBase, lat, nN);
+        if (P) {
+            UPD(d->qualBase, qual, (size_t)P * nN);
+        } else {
+            d->qualBase = devAlloc<double>(d, 1, &e);
+        }
+    }
+    p.latIn = d->latBase;
+    p.qualIn = d->qualBase;
+    // ---- quality ----------------------------------------------------------
+    {
+        std::vector<double> kd(std::max(P, 1), 0.0);
+        for (int q = 0; q < P; q++) kd[q] = net.pollut[q].kDecay;
+        UPD(tmp, kd, kd.size()); p.kDecay = tmp;
+        size_t nq = (size_t)std::max(P, 0);
+        UPD(p.nOldQual, st.nOldQual, nq * nN);
+        UPD(p.nNewQual, st.nNewQual, nq * nN);
+        UPD(p.lOldQual, st.lOldQual, nq * nL);
+        UPD(p.lNewQual, st.lNewQual, nq * nL);
+    }
+    // ---- tables, partials, control ---------------------------------------
+    {
+        std::vector<double> t(&SWX_CIRC_TABLES[0][0], &SWX_CIRC_TABLES[0][0] + 5 * SWX_CIRC_N);
+        UPD(tmp, t, t.size()); p.gTables = tmp;
+    }
+    int maxBlocks = 8 * std::max(prop.multiProcessorCount, 1);
+    d->gridL = std::max(1, std::min((nL + kBlock - 1) / kBlock, maxBlocks));
+    d->gridN = std::max(1, std::min((nN + kBlock - 1) / kBlock, maxBlocks));
+    d->gridEnd = std::max(1, std::min((std::max(nN, nL) + kBlock - 1) / kBlock, 2 * prop.multiProcessorCount));
+    p.nBlocksEnd = d->gridEnd;
+    p.partials = devAlloc<double>(d, (size_t)d->gridEnd * kNumPartials, &e);
+    if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+    p.ctl = devAlloc<StepCtl>(d, 1, &e);
+    if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+    d->ctl = p.ctl;
+    HIPCHECK(hipHostMalloc((void**)&d->hostCtl, sizeof(StepCtl), hipHostMallocDefault));
+    memset(d->hostCtl, 0, sizeof(StepCtl));
+    StepCtl* hc = d->hostCtl;
+    hc->routeStep = prj.opt.routeStep;
+    hc->routingDuration = prj.opt.totalDuration;
+    hc->newRoutingTime = 0.0;
+    // first step: dynwave_getRoutingStep returns MinRouteStep while VariableStep == 0
+    double dt0 = p.varStep ? floor(1000.0 * prj.opt.minRouteStep) / 1000.0 : prj.opt.routeStep;
+    if (!p.varStep) { /* fixed step */ }
+    if (1000.0 * dt0 > hc->routingDuration) {
+        dt0 = hc->routingDuration / 1000.0;
+        dt0 = (dt0 >= 1. / 1000.0) ? dt0 : 1. / 1000.0;
+    }
+    hc->dt = dt0;
+    hc->latTot[0] = d->latTot0[0];
+    hc->latTot[1] = d->latTot0[1];
+    hc->latTot[2] = d->latTot0[2];
+    HIPCHECK(hipMemcpy(d->ctl, d->hostCtl, sizeof(StepCtl), hipMemcpyHostToDevice));
+    d->slotDoubles = (size_t)nN * (1 + P) + 8;
+    d->pinnedSize = d->slotDoubles * Impl::kRing;
+    HIPCHECK(hipHostMalloc((void**)&d->hostPinned, d->pinnedSize * sizeof(double), hipHostMallocDefault));
+    for (auto& ev : d->ringEv) { HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming)); HIPCHECK(hipEventRecord(ev, d->stream)); }
+    d->ev.resize(2 * kMaxTrialsCap + 4);
+    for (auto& ev : d->ev) HIPCHECK(hipEventCreate(&ev));
+
+    // algorithmic bytes per launch (DESIGN.md byte model; per kernel class)
+    {
+        double L = nL, N = nN, E = d->nE;
+        // link momentum: static 8 (nodes) + 4 (flags) + 4x8 (inv/off) + 7x8 (geom)
+        //   + 3x8 (lengths, roughFactor) ; dynamic reads newFlow/oldFlow, q1,
+        //   a1/a2, setting, lstate (8x5 + 4) ; 2 node depth gathers (16) ;
+        //   writes a1 q1 newDepth newVolume newFlow dqdh froude sa1 sa2 evap seep + lstate (11x8+4)
+        d->kbytes[0] = L * (8 + 4 + 32 + 56 + 24 + 44 + 16 + 92);
+        // node update: per node static (flags, fullDepth, surDepth, yCrown,
+        //   fullVolume, ponded: 4+5x8) + rowptr 4 + dynamic reads (newDepth,
+        //   oldDepth, oldNetInflow, newLat, oldSurfArea: 40) + writes (inflow,
+        //   outflow, newDepth, newVolume, overflow, dYdT, oldSurfArea, conv:
+        //   7x8+4) ; per CSR entry: index 4 + newFlow, sa, dqdh 24 + flags 4
+        d->kbytes[1] = N * (44 + 4 + 40 + 60) + E * (4 + 24 + 4);
+        d->kbytes[2] = L * (4 + 8 + 8 + 8 + 8 + 8 + 4) + N * (4 + 8 * 6);
+        d->kbytes[3] = P ? (N * (24 + 16.0 * P) + E * (4 + 8 + 8.0 * P) + L * (72 + 24.0 * P)) : 0.0;
+    }
+
+    // ---- capture the step graph ----------------------------------------------
+    d->useGraph = true;
+    hipGraph_t g;
+    HIPCHECK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
+    launchStep(d);
+    HIPCHECK(hipStreamEndCapture(d->stream, &g));
+    HIPCHECK(hipGraphInstantiate(&d->graph, g, nullptr, nullptr, 0));
+    hipGraphDestroy(g);
+    HIPCHECK(hipStreamSynchronize(d->stream));
+    ok_ = true;
+    return 0;
+#undef UPD
+#undef UPI
+}
+
+int Router::step(const double* latFlow, const double* qualLoad, const double tot[3])
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    Params& p = d->p;
+    if (latFlow) {
+        // pinned ring slot: wait until the DMA that last read this slot is done
+        int s = d->ringNext;
+        d->ringNext = (d->ringNext + 1) % Impl::kRing;
+        HIPCHECK(hipEventSynchronize(d->ringEv[s]));
+        double* slot = d->hostPinned + (size_t)s * d->slotDoubles;
+        size_t nN = p.nN, nq = (size_t)p.P * nN;
+        memcpy(slot, latFlow, nN * sizeof(double));
+        if (nq) {
+            if (qualLoad) memcpy(slot + nN, qualLoad, nq * sizeof(double));
+            else memset(slot + nN, 0, nq * sizeof(double));
+        }
+        slot[nN + nq + 0] = tot[0];
+        slot[nN + nq + 1] = tot[1];
+        slot[nN + nq + 2] = tot[2];
+        HIPCHECK(hipMemcpyAsync(d->latBase, slot, nN * sizeof(double), hipMemcpyHostToDevice, d->stream));
+        if (nq)
+            HIPCHECK(hipMemcpyAsync(d->qualBase, slot + nN, nq * sizeof(double), hipMemcpyHostToDevice, d->stream));
+        HIPCHECK(hipMemcpyAsync(&d->ctl->latTot[0], slot + nN + nq, 3 * sizeof(double),
+                                hipMemcpyHostToDevice, d->stream));
+        HIPCHECK(hipEventRecord(d->ringEv[s], d->stream));
+    }
+    if (d->timing) {
+        launchStep(d);
+        HIPCHECK(hipStreamSynchronize(d->stream));
+        int ran = 0;
+        HIPCHECK(hipMemcpy(&ran, &d->ctl->lastSteps, sizeof(int), hipMemcpyDeviceToHost));
+        for (int k = 0; k < ran; k++) {    // early-exited iterations are not counted
+            float ms1 = 0, ms2 = 0;
+            hipEventElapsedTime(&ms1, d->ev[2 * k], d->ev[2 * k + 1]);
+            hipEventElapsedTime(&ms2, d->ev[2 * k + 1], d->ev[2 * k + 2]);
+            d->kms[0] += ms1; d->kcnt[0]++;
+            d->kms[1] += ms2; d->kcnt[1]++;
+        }
+        int base = 2 * p.maxTrials + 1;
+        float ms3 = 0, msq = 0;
+        hipEventElapsedTime(&ms3, d->ev[base], d->ev[base + 1]);
+        hipEventElapsedTime(&msq, d->ev[2 * p.maxTrials], d->ev[base]);
+        d->kms[2] += ms3; d->kcnt[2]++;
+        if (p.P) { d->kms[3] += msq; d->kcnt[3]++; }
+    } else {
+        HIPCHECK(hipGraphLaunch(d->graph, d->stream));
+    }
+    return 0;
+}
+
+int Router::readClock(double* t, double* lastDt, double* nextDt)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    HIPCHECK(hipMemcpyAsync(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost, d->stream));
+    HIPCHECK(hipStreamSynchronize(d->stream));
+    if (t) *t = d->hostCtl->newRoutingTime;
+    if (nextDt) *nextDt = d->hostCtl->dt;
+    if (lastDt) *lastDt = d->lastDtHost;
+    return 0;
+}
+
+int Router::setDuration(double msec)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    HIPCHECK(hipStreamSynchronize(d->stream));
+    HIPCHECK(hipMemcpy(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost));
+    d->hostCtl->routingDuration = msec;
+    // re-apply the clamp for the step about to run
+    double dtn = d->hostCtl->dtNext > 0 ? d->hostCtl->dtNext : d->hostCtl->dt;
+    if (d->hostCtl->newRoutingTime + 1000.0 * dtn > msec) {
+        dtn = (msec - d->hostCtl->newRoutingTime) / 1000.0;
+        dtn = (dtn >= 1. / 1000.0) ? dtn : 1. / 1000.0;
+    }
+    d->hostCtl->dt = dtn;
+    HIPCHECK(hipMemcpy(d->ctl, d->hostCtl, sizeof(StepCtl), hipMemcpyHostToDevice));
+    return 0;
+}
+
+int Router::sync()
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    HIPCHECK(hipStreamSynchronize(d_->stream));
+    return 0;
+}
+
+int Router::download(Project& prj)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    Params& p = d->p;
+    State& st = prj.st;
+    size_t nN = p.nN, nL = p.nL;
+    auto dn = [&](std::vector<double>& v, const double* src, size_t n) {
+        v.resize(n);
+        return hipMemcpyAsync(v.data(), src, n * sizeof(double), hipMemcpyDeviceToHost, d->stream);
+    };
+    HIPCHECK(dn(st.newDepth, p.nNewDepth, nN));
+    HIPCHECK(dn(st.oldDepth, p.nOldDepth, nN));
+    HIPCHECK(dn(st.newVolume, p.nNewVolume, nN));
+    HIPCHECK(dn(st.oldVolume, p.nOldVolume, nN));
+    HIPCHECK(dn(st.inflow, p.inflow, nN));
+    HIPCHECK(dn(st.outflow, p.outflow, nN));
+    HIPCHECK(dn(st.overflow, p.overflow, nN));
+    HIPCHECK(dn(st.newLatFlow, p.newLat, nN));
+    HIPCHECK(dn(st.oldLatFlow, p.oldLat, nN));
+    HIPCHECK(dn(st.oldNetInflow, p.oldNetInflow, nN));
+    HIPCHECK(dn(st.oldFlowInflow, p.oldFlowInflow, nN));
+    HIPCHECK(dn(st.oldSurfArea, p.oldSurfArea, nN));
+    HIPCHECK(dn(st.dYdT, p.dYdT, nN));
+    HIPCHECK(dn(st.lNewFlow, p.lNewFlow, nL));
+    HIPCHECK(dn(st.lOldFlow, p.lOldFlow, nL));
+    HIPCHECK(dn(st.lNewDepth, p.lNewDepth, nL));
+    HIPCHECK(dn(st.lOldDepth, p.lOldDepth, nL));
+    HIPCHECK(dn(st.lNewVolume, p.lNewVolume, nL));
+    HIPCHECK(dn(st.lOldVolume, p.lOldVolume, nL));
+    HIPCHECK(dn(st.a1, p.a1, nL));
+    HIPCHECK(dn(st.a2, p.a2, nL));
+    HIPCHECK(dn(st.q1, p.q1, nL));
+    HIPCHECK(dn(st.dqdh, p.dqdh, nL));
+    HIPCHECK(dn(st.froude, p.froude, nL));
+    HIPCHECK(dn(st.surfArea1, p.sa1, nL));
+    HIPCHECK(dn(st.surfArea2, p.sa2, nL));
+    HIPCHECK(dn(st.evapLossRate, p.evapLoss, nL));
+    HIPCHECK(dn(st.seepLossRate, p.seepLoss, nL));
+    HIPCHECK(dn(st.setting, p.setting, nL));
+    size_t P = p.P;
+    if (P) {
+        HIPCHECK(dn(st.nOldQual, p.nOldQual, P * nN));
+        HIPCHECK(dn(st.nNewQual, p.nNewQual, P * nN));
+        HIPCHECK(dn(st.lOldQual, p.lOldQual, P * nL));
+        HIPCHECK(dn(st.lNewQual, p.lNewQual, P * nL));
+    }
+    std::vector<int> ls(nL), cv(nN);
+    HIPCHECK(hipMemcpyAsync(ls.data(), p.lstate, nL * sizeof(int), hipMemcpyDeviceToHost, d->stream));
+    HIPCHECK(hipMemcpyAsync(cv.data(), p.conv, nN * sizeof(int), hipMemcpyDeviceToHost, d->stream));
+    HIPCHECK(hipMemcpyAsync(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost, d->stream));
+    HIPCHECK(hipStreamSynchronize(d->stream));
+    st.flowClass.resize(nL); st.fullState.resize(nL); st.normalFlow.resize(nL); st.capacityLimited.resize(nL);
+    for (size_t j = 0; j < nL; j++) {
+        st.flowClass[j] = ls[j] & 0xF;
+        st.fullState[j] = (ls[j] >> 4) & 0xF;
+        st.normalFlow[j] = (ls[j] >> 8) & 1;
+        st.capacityLimited[j] = (ls[j] >> 9) & 1;
+    }
+    st.converged = cv;
+    st.variableStep = d->hostCtl->variableStep;
+    return 0;
+}
+
+int Router::upload(Project& prj)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    Params& p = d->p;
+    State& st = prj.st;
+    size_t nN = p.nN, nL = p.nL;
+    auto up = [&](double* dst, const std::vector<double>& v, size_t n) {
+        return hipMemcpyAsync(dst, v.data(), n * sizeof(double), hipMemcpyHostToDevice, d->stream);
+    };
+    HIPCHECK(up(p.nNewDepth, st.newDepth, nN));
+    HIPCHECK(up(p.nOldDepth, st.oldDepth, nN));
+    HIPCHECK(up(p.nNewVolume, st.newVolume, nN));
+    HIPCHECK(up(p.inflow, st.inflow, nN));
+    HIPCHECK(up(p.outflow, st.outflow, nN));
+    HIPCHECK(up(p.newLat, st.newLatFlow, nN));
+    HIPCHECK(up(p.lNewFlow, st.lNewFlow, nL));
+    HIPCHECK(up(p.lNewDepth, st.lNewDepth, nL));
+    HIPCHECK(up(p.lNewVolume, st.lNewVolume, nL));
+    HIPCHECK(up(p.q1, st.q1, nL));
+    HIPCHECK(up(p.a1, st.a1, nL));
+    HIPCHECK(up(p.setting, st.setting, nL));
+    HIPCHECK(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+void Router::counters(long long* totalIters, long long* nonConv, int* lastSteps)
+{
+    Impl* d = d_;
+    hipMemcpyAsync(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost, d->stream);
+    hipStreamSynchronize(d->stream);
+    *totalIters = d->hostCtl->totalIters;
+    *nonConv = d->hostCtl->nonConverge;
+    *lastSteps = d->hostCtl->lastSteps;
+}
+
+void Router::flowTotals(double out[8])
+{
+    Impl* d = d_;
+    hipMemcpyAsync(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost, d->stream);
+    hipStreamSynchronize(d->stream);
+    for (int q = 0; q < 8; q++) out[q] = d->hostCtl->flowTot[q];
+}
+
+void Router::stepTotals(double out[6])
+{
+    Impl* d = d_;
+    hipMemcpyAsync(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost, d->stream);
+    hipStreamSynchronize(d->stream);
+    for (int q = 0; q < 6; q++) out[q] = d->hostCtl->prevStepTot[q];
+}
+
+void Router::setTiming(bool on)
+{
+    d_->timing = on;
+    for (int k = 0; k < 4; k++) { d_->kms[k] = 0; d_->kcnt[k] = 0; }
+}
+
+int Router::kernelTimes(double* out, int n)
+{
+    int m = std::min(n / 2, 4);
+    for (int k = 0; k < m; k++) {
+        out[2 * k] = (double)d_->kcnt[k];
+        out[2 * k + 1] = d_->kms[k];
+    }
+    return m;
+}
+
+int Router::kernelBytes(double* out, int n)
+{
+    int m = std::min(n, 4);
+    for (int k = 0; k < m; k++) out[k] = d_->kbytes[k];
+    return m;
+}
+
+}  // namespace swx

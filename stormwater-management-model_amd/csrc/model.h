@@ -1,0 +1,184 @@
+// model.h -- host-side data model of the MI355X dynamic-wave engine.
+//
+// Objects are held as structure-of-arrays (one std::vector per attribute),
+// which is also the layout the device arrays are uploaded from.  Attribute
+// meanings and units follow the reference's TNode / TLink / TConduit /
+// TXsect structs (src/solver/objects.h:491-731): internal units are US
+// customary (ft, cfs, s) whatever FLOW_UNITS the input uses.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace swx {
+
+// ---- enums (values match src/solver/enums.h so dumps compare 1:1) --------
+enum NodeType { JUNCTION = 0, OUTFALL = 1, STORAGE = 2, DIVIDER = 3 };
+enum LinkType { CONDUIT = 0, PUMP = 1, ORIFICE = 2, WEIR = 3, OUTLET = 4 };
+enum XsectType {
+    X_DUMMY = 0, X_CIRCULAR, X_FILLED_CIRCULAR, X_RECT_CLOSED, X_RECT_OPEN, X_TRAPEZOIDAL,
+    X_TRIANGULAR, X_PARABOLIC, X_POWERFUNC, X_RECT_TRIANG, X_RECT_ROUND, X_MOD_BASKET,
+    X_HORIZ_ELLIPSE, X_VERT_ELLIPSE, X_ARCH, X_EGGSHAPED, X_HORSESHOE, X_GOTHIC, X_CATENARY,
+    X_SEMIELLIPTICAL, X_BASKETHANDLE, X_SEMICIRCULAR, X_IRREGULAR, X_CUSTOM, X_FORCE_MAIN,
+    X_STREET
+};
+enum FlowClass { F_DRY = 0, F_UP_DRY, F_DN_DRY, F_SUBCRIT, F_SUPCRIT, F_UP_CRIT, F_DN_CRIT };
+enum FullState { FS_NONE = 0, FS_UP_FULL = 8, FS_DN_FULL = 9, FS_ALL_FULL = 10 };
+enum OutfallType { O_FREE = 0, O_NORMAL = 1, O_FIXED = 2, O_TIDAL = 3, O_TSERIES = 4 };
+enum SurchargeMethod { SUR_EXTRAN = 0, SUR_SLOT = 1 };
+enum InertDamping { DAMP_NO = 0, DAMP_PARTIAL = 1, DAMP_FULL = 2 };
+enum NormalFlowLtd { NFL_SLOPE = 0, NFL_FROUDE = 1, NFL_BOTH = 2, NFL_NEITHER = 3 };
+enum FlowUnits { CFS = 0, GPM, MGD, CMS, LPS, MLD };
+enum RouteModel { RM_NONE = 0, RM_SF = 1, RM_KW = 2, RM_EKW = 3, RM_DW = 4 };
+enum PatternType { PAT_MONTHLY = 0, PAT_DAILY = 1, PAT_HOURLY = 2, PAT_WEEKEND = 3 };
+enum ConcUnits { CU_MG = 0, CU_UG = 1, CU_COUNT = 2 };
+
+// ---- constants: src/solver/consts.h:33-93 ---------------------------------
+constexpr double kFudge = 0.0001;
+constexpr double kTiny = 1.e-6;
+constexpr double kZero = 1.e-10;
+constexpr double kMissing = -1.e10;
+constexpr double kPi = 3.141592654;
+constexpr double kGravity = 32.2;
+constexpr double kPhi = 1.486;
+constexpr double kFlowTol = 0.00001;
+constexpr double kMinDeltaZ = 0.001;
+constexpr double kLperFT3 = 28.317;
+constexpr double kSecPerDay = 86400.0;
+constexpr double kMsecPerDay = 8.64e7;
+
+struct Options {
+    int flowUnits = CFS;
+    int unitSystem = 0;              // 0 US, 1 SI
+    int routeModel = RM_DW;
+    int surchargeMethod = SUR_EXTRAN;
+    int inertDamping = DAMP_PARTIAL;
+    int normalFlowLtd = NFL_BOTH;
+    int allowPonding = 0;
+    int ignoreQuality = 0;
+    int ignoreRouting = 0;
+    int skipSteadyState = 0;
+    int linkOffsetsElev = 0;         // 0 DEPTH, 1 ELEVATION
+    int forceMainEqn = 0;
+    int numThreads = 1;
+    int maxTrials = 0;
+    double routeStep = 20.0;
+    double minRouteStep = 0.5;
+    double lengtheningStep = 0.0;
+    double courantFactor = 0.75;
+    double minSurfArea = 0.0;
+    double minSlope = 0.0;
+    double headTol = 0.0;
+    double sysFlowTol = 0.05;
+    double latFlowTol = 0.05;
+    double crownCutoff = 0.96;
+    int wetStep = 300, dryStep = 3600, reportStep = 900, ruleStep = 0;
+    double startDate = 0, startTime = 0, endDate = 0, endTime = 0;
+    double reportStartDate = -693594, reportStartTime = -693594;
+    bool haveReportStartDate = false, haveReportStartTime = false;
+    double evapRate = 0.0;           // constant evaporation (ft/s)
+    // derived
+    double startDateTime = 0, endDateTime = 0, reportStart = 0, totalDuration = 0; // msec
+};
+
+struct ReportFlags {
+    int input = 0, controls = 0, continuity = 1, flowStats = 1, averages = 0;
+    int nodesAll = 0, linksAll = 0, subcatchAll = 0;  // 1 ALL, 0 NONE / list
+    int disabled = 0;
+};
+
+struct Pattern {
+    std::string id;
+    int type = -1;
+    int count = 0;
+    double factor[24];
+};
+
+struct Tseries {
+    std::string id;
+    std::vector<double> x, y;
+    double lastDate = 0.0;
+    // lookup cursor (table.c:730-806)
+    double x1 = 0, y1 = 0, x2 = 0, y2 = 0;
+    size_t cur = 0;
+};
+
+struct ExtInflow {       // TExtInflow (objects.h) -- node's external inflow
+    int node = -1, param = -1, type = 0;  // param -1 = FLOW; type 0 CONCEN,1 MASS,2 FLOW
+    int tseries = -1, basePat = -1;
+    double cFactor = 1.0, baseline = 0.0, sFactor = 1.0;
+};
+enum { EXT_CONCEN = 0, EXT_MASS = 1, EXT_FLOW = 2 };
+
+struct DwfInflow {       // TDwfInflow
+    int node = -1, param = -1;
+    double avgValue = 0.0;
+    int patterns[4] = {-1, -1, -1, -1};
+};
+
+struct Pollutant {
+    std::string id;
+    int units = CU_MG;
+    double mcf = 1.0;
+    double cRain = 0, cGW = 0, cRDII = 0, kDecay = 0, cDWF = 0, cInit = 0;
+};
+
+struct Xsect {
+    int type = -1, culvertCode = 0;
+    double yFull = 0, wMax = 0, ywMax = 0, aFull = 0, rFull = 0, sFull = 0, sMax = 0;
+    double yBot = 0, aBot = 0, sBot = 0, rBot = 0;
+};
+
+// ---- the network --------------------------------------------------------
+struct Network {
+    // nodes
+    std::vector<std::string> nodeId;
+    std::vector<int> nodeType, nodeSub, degree, rptFlag;
+    std::vector<double> invertElev, initDepth, fullDepth, surDepth, pondedArea, crownElev,
+        fullVolume;
+    // outfall parameters (indexed by node; unused for other types)
+    std::vector<int> outfallType, outfallFlap, outfallSeries;
+    std::vector<double> fixedStage;
+    // links
+    std::vector<std::string> linkId;
+    std::vector<int> linkType, node1, node2, hasFlapGate, direction, barrels, hasLosses,
+        superCritical, linkRpt;
+    std::vector<double> offset1, offset2, q0, qLimit, cLossInlet, cLossOutlet, cLossAvg,
+        seepRate, length, roughness, modLength, roughFactor, slope, beta, qMax, qFull;
+    std::vector<Xsect> xsect;
+    // inflows / quality inputs
+    std::vector<ExtInflow> extInflows;
+    std::vector<DwfInflow> dwfInflows;
+    std::vector<Pollutant> pollut;
+    std::vector<Pattern> patterns;
+    std::vector<Tseries> tseries;
+    std::unordered_map<std::string, int> nodeIndex, linkIndex, pollutIndex, patternIndex,
+        tseriesIndex;
+    std::string title;
+
+    int nNodes() const { return (int)nodeId.size(); }
+    int nLinks() const { return (int)linkId.size(); }
+    int nPollut() const { return (int)pollut.size(); }
+};
+
+// ---- dynamic state (host mirror of HBM-resident state) --------------------
+struct State {
+    // node
+    std::vector<double> newDepth, oldDepth, newVolume, oldVolume, inflow, outflow, overflow,
+        losses, newLatFlow, oldLatFlow, oldNetInflow, oldFlowInflow;
+    // link
+    std::vector<double> lNewFlow, lOldFlow, lNewDepth, lOldDepth, lNewVolume, lOldVolume,
+        surfArea1, surfArea2, froude, dqdh, setting, a1, a2, q1, q2, evapLossRate,
+        seepLossRate;
+    std::vector<int> flowClass, fullState, normalFlow, capacityLimited;
+    // Xnode (dynwave.c:72-79)
+    std::vector<double> oldSurfArea, dYdT;
+    std::vector<int> converged;
+    // quality [p][object]
+    std::vector<double> nOldQual, nNewQual, lOldQual, lNewQual;
+    double variableStep = 0.0;
+};
+
+}  // namespace swx

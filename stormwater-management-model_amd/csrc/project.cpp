@@ -1,0 +1,1530 @@
+// project.cpp -- .inp reader, validation and initial state (host only).
+//
+// Restates the parts of the reference's input/project/link/node/xsect/
+// flowrout modules that define every constant and initial value the routing
+// kernels read.  The reader is our own two-pass,
+// hash-map based design (O(N) -- the reference's fixed 1999-bucket ID hash
+// makes swmm_open O(N^2): 157 s at 1M conduits); the derived values follow
+// the reference arithmetic exactly so that tests/test_host_init.py can assert
+// bit-equality of every parameter and initial state value.
+//
+// Supported input: [TITLE] [OPTIONS] [EVAPORATION] (CONSTANT) [JUNCTIONS]
+// [OUTFALLS] (FREE/NORMAL/FIXED/TIMESERIES) [CONDUITS] [XSECTIONS]
+// (CIRCULAR, FORCE_MAIN excluded, RECT_CLOSED, RECT_OPEN, TRAPEZOIDAL,
+// TRIANGULAR) [LOSSES] [POLLUTANTS] [INFLOWS] [DWF] [PATTERNS] [TIMESERIES]
+// [REPORT]; map/graphics sections are skipped.  Anything else fails loudly
+// with ERR_INPUT naming the section (never silently ignored).
+#include "project.h"
+
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <algorithm>
+
+#include "xsect.h"
+
+namespace swx {
+
+// ===================================================================== dates
+static const int kDateDelta = 693594;          // datetime.c:40
+static const double kSecsPerDay = 86400.;      // datetime.c:41
+static const int kDaysPerMonth[2][12] = {{31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31},
+                                         {31, 29, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31}};
+static int isLeap(int y) { return ((y % 4 == 0) && ((y % 100 != 0) || (y % 400 == 0))) ? 1 : 0; }
+
+double encodeDate(int year, int month, int day)  // datetime.c:108-132
+{
+    int i = isLeap(year);
+    if (year >= 1 && year <= 9999 && month >= 1 && month <= 12 && day >= 1 &&
+        day <= kDaysPerMonth[i][month - 1]) {
+        for (int j = 0; j < month - 1; j++) day += kDaysPerMonth[i][j];
+        i = year - 1;
+        i = i * 365 + i / 4 - i / 100 + i / 400 + day - kDateDelta;
+        return i;
+    }
+    return -kDateDelta;
+}
+
+double encodeTime(int hour, int minute, int second)  // datetime.c:136-152
+{
+    if (hour >= 0 && minute >= 0 && second >= 0) {
+        int s = hour * 3600 + minute * 60 + second;
+        return (double)s / kSecsPerDay;
+    }
+    return 0.0;
+}
+
+static int findMonth(const char* m)
+{
+    static const char* names[] = {"JAN", "FEB", "MAR", "APR", "MAY", "JUN",
+                                  "JUL", "AUG", "SEP", "OCT", "NOV", "DEC"};
+    for (int i = 0; i < 12; i++)
+        if (strncasecmp(m, names[i], 3) == 0) return i + 1;
+    return -1;
+}
+
+bool strToDate(const char* s, double* d)  // datetime.c:284-334 (M/D/Y format)
+{
+    int yr = 0, mon = 0, day = 0;
+    char month[4] = {0};
+    char sep1, sep2;
+    *d = -kDateDelta;
+    if (strchr(s, '-') || strchr(s, '/')) {
+        int n = sscanf(s, "%d%c%d%c%d", &mon, &sep1, &day, &sep2, &yr);
+        if (n < 3) {
+            mon = 0;
+            n = sscanf(s, "%3s%c%d%c%d", month, &sep1, &day, &sep2, &yr);
+            if (n < 3) return false;
+        }
+        if (mon == 0) mon = findMonth(month);
+        *d = encodeDate(yr, mon, day);
+    }
+    return *d != -kDateDelta;
+}
+
+bool strToTime(const char* s, double* t)  // datetime.c:338-365
+{
+    char* endptr;
+    *t = strtod(s, &endptr);
+    if (*endptr == 0) {
+        *t /= 24.0;
+        return true;
+    }
+    int hr = 0, min = 0, sec = 0;
+    *t = 0.0;
+    int n = sscanf(s, "%d:%d:%d", &hr, &min, &sec);
+    if (n == 0) return false;
+    *t = encodeTime(hr, min, sec);
+    return hr >= 0 && min >= 0 && sec >= 0;
+}
+
+static void divMod(int n, int d, int* result, int* remainder)
+{
+    if (d == 0) { *result = 0; *remainder = 0; }
+    else { *result = n / d; *remainder = n - d * (*result); }
+}
+
+void decodeDate(double date, int* year, int* month, int* day)  // datetime.c:158-220
+{
+    const int D1 = 365, D4 = D1 * 4 + 1, D100 = D4 * 25 - 1, D400 = D100 * 4 + 1;
+    int t = (int)(floor(date)) + kDateDelta, y, m, d, i, k;
+    if (t <= 0) { *year = 0; *month = 1; *day = 1; return; }
+    t--;
+    y = 1;
+    while (t >= D400) { t -= D400; y += 400; }
+    divMod(t, D100, &i, &d);
+    if (i == 4) { i--; d += D100; }
+    y += i * 100;
+    divMod(d, D4, &i, &d);
+    y += i * 4;
+    divMod(d, D1, &i, &d);
+    if (i == 4) { i--; d += D1; }
+    y += i;
+    k = isLeap(y);
+    m = 1;
+    for (;;) {
+        i = kDaysPerMonth[k][m - 1];
+        if (d < i) break;
+        d -= i;
+        m++;
+    }
+    *year = y; *month = m; *day = d + 1;
+}
+
+void decodeTime(double time, int* h, int* m, int* s)  // datetime.c:224-241
+{
+    double fracDay = (time - floor(time)) * kSecsPerDay;
+    int secs = (int)(floor(fracDay + 0.5)), mins;
+    if (secs >= 86400) secs = 86399;
+    divMod(secs, 60, &mins, s);
+    divMod(mins, 60, h, m);
+    if (*h > 23) *h = 0;
+}
+
+double addSeconds(double date1, double seconds)  // datetime.c:381-393
+{
+    double d = floor(date1);
+    int h, m, s;
+    decodeTime(date1, &h, &m, &s);
+    return d + (3600.0 * h + 60.0 * m + s + seconds) / kSecsPerDay;
+}
+
+int monthOfYear(double date) { int y, m, d; decodeDate(date, &y, &m, &d); return m; }
+int dayOfWeek(double date) { int t = (int)(floor(date)) + kDateDelta; return (t % 7) + 1; }
+int hourOfDay(double date) { int h, m, s; decodeTime(date, &h, &m, &s); return h; }
+
+// ============================================================== tokenising
+// input.c:getTokens semantics: ';' starts a comment, whitespace separates,
+// a double quote starts a token that runs to the next quote.
+static int tokenize(char* s, std::vector<char*>& tok)
+{
+    tok.clear();
+    char* c = strchr(s, ';');
+    if (c) *c = '\0';
+    int len = (int)strlen(s);
+    const char* sep = " \t\n\r";
+    while (len > 0) {
+        int m = (int)strcspn(s, sep);
+        if (m == 0) {
+            s++;
+        } else {
+            if (*s == '"') {
+                s++;
+                len--;
+                m = (int)strcspn(s, "\"\n");
+            }
+            s[m] = '\0';
+            tok.push_back(s);
+            s += m + 1;
+        }
+        len -= m + 1;
+    }
+    return (int)tok.size();
+}
+
+// input.c:match -- keyword is a case-insensitive prefix of str
+static bool kmatch(const char* str, const char* kw)
+{
+    if (!kw[0]) return false;
+    while (*str == ' ') str++;
+    for (; *kw; kw++, str++)
+        if (!*str || toupper((unsigned char)*str) != toupper((unsigned char)*kw)) return false;
+    return true;
+}
+static int kfind(const char* s, const char* const* kws)
+{
+    for (int i = 0; kws[i]; i++)
+        if (kmatch(s, kws[i])) return i;
+    return -1;
+}
+static bool getDouble(const char* s, double* y)
+{
+    char* e;
+    *y = strtod(s, &e);
+    if (*e > 0) return false;
+    return true;
+}
+
+enum Sect {
+    S_NONE = -1, S_TITLE, S_OPTION, S_EVAP, S_JUNC, S_OUTFALL, S_CONDUIT, S_XSECT, S_LOSS,
+    S_POLLUT, S_INFLOW, S_DWF, S_PATTERN, S_TSERIES, S_REPORT, S_SKIP, S_UNSUPPORTED
+};
+static const char* const kSectWords[] = {
+    "[TITLE", "[OPTION", "[EVAP", "[JUNC", "[OUTFALL", "[CONDUIT", "[XSECT", "[LOSS",
+    "[POLLUT", "[INFLOW", "[DWF", "[PATTERN", "[TIMESERIES", "[REPORT", nullptr};
+static const char* const kSkipWords[] = {
+    "[MAP", "[COORDINATE", "[VERTICES", "[POLYGON", "[SYMBOL", "[LABEL", "[BACKDROP", "[TAG",
+    "[PROFILE", nullptr};
+
+static const char* const kFlowUnitWords[] = {"CFS", "GPM", "MGD", "CMS", "LPS", "MLD", nullptr};
+static const char* const kNoYes[] = {"NO", "YES", nullptr};
+static const char* const kRouteWords[] = {"NONE", "STEADY", "KINWAVE", "XKINWAVE", "DYNWAVE", nullptr};
+static const char* const kOldRouteWords[] = {"NONE", "NF", "KW", "EKW", "DW", nullptr};
+static const char* const kInertWords[] = {"NONE", "PARTIAL", "FULL", nullptr};
+static const char* const kNormalWords[] = {"SLOPE", "FROUDE", "BOTH", "NONE", nullptr};
+static const char* const kSurchargeWords[] = {"EXTRAN", "SLOT", nullptr};
+static const char* const kOffsetWords[] = {"DEPTH", "ELEVATION", nullptr};
+static const char* const kForceMainWords[] = {"H-W", "D-W", nullptr};
+static const char* const kOutfallWords[] = {"FREE", "NORMAL", "FIXED", "TIDAL", "TIMESERIES", nullptr};
+static const char* const kPatternWords[] = {"MONTHLY", "DAILY", "HOURLY", "WEEKEND", nullptr};
+static const char* const kQualUnitWords[] = {"MG/L", "UG/L", "#/L", nullptr};
+static const char* const kXsectWords[] = {
+    "DUMMY", "CIRCULAR", "FILLED_CIRCULAR", "RECT_CLOSED", "RECT_OPEN", "TRAPEZOIDAL",
+    "TRIANGULAR", "PARABOLIC", "POWER", "RECT_TRIANGULAR", "RECT_ROUND", "MODBASKETHANDLE",
+    "HORIZ_ELLIPSE", "VERT_ELLIPSE", "ARCH", "EGG", "HORSESHOE", "GOTHIC", "CATENARY",
+    "SEMIELLIPTICAL", "BASKETHANDLE", "SEMICIRCULAR", "IRREGULAR", "CUSTOM", "FORCE_MAIN",
+    "STREET", nullptr};
+// option keywords, in the reference's order (keywords.c:75-98)
+enum {
+    O_FLOW_UNITS, O_INFIL_MODEL, O_ROUTE_MODEL, O_START_DATE, O_START_TIME, O_END_DATE,
+    O_END_TIME, O_REPORT_START_DATE, O_REPORT_START_TIME, O_SWEEP_START, O_SWEEP_END,
+    O_START_DRY_DAYS, O_WET_STEP, O_DRY_STEP, O_ROUTE_STEP, O_RULE_STEP, O_REPORT_STEP,
+    O_ALLOW_PONDING, O_INERT_DAMPING, O_SLOPE_WEIGHTING, O_VARIABLE_STEP, O_NORMAL_FLOW_LTD,
+    O_LENGTHENING_STEP, O_MIN_SURFAREA, O_COMPATIBILITY, O_SKIP_STEADY_STATE, O_TEMPDIR,
+    O_IGNORE_RAINFALL, O_FORCE_MAIN_EQN, O_LINK_OFFSETS, O_MIN_SLOPE, O_IGNORE_SNOWMELT,
+    O_IGNORE_GWATER, O_IGNORE_ROUTING, O_IGNORE_QUALITY, O_MAX_TRIALS, O_HEAD_TOL,
+    O_SYS_FLOW_TOL, O_LAT_FLOW_TOL, O_IGNORE_RDII, O_MIN_ROUTE_STEP, O_NUM_THREADS,
+    O_SURCHARGE_METHOD
+};
+static const char* const kOptionWords[] = {
+    "FLOW_UNITS", "INFILTRATION", "FLOW_ROUTING", "START_DATE", "START_TIME", "END_DATE",
+    "END_TIME", "REPORT_START_DATE", "REPORT_START_TIME", "SWEEP_START", "SWEEP_END",
+    "DRY_DAYS", "WET_STEP", "DRY_STEP", "ROUTING_STEP", "RULE_STEP", "REPORT_STEP",
+    "ALLOW_PONDING", "INERTIAL_DAMPING", "SLOPE_WEIGHTING", "VARIABLE_STEP",
+    "NORMAL_FLOW_LIMITED", "LENGTHENING_STEP", "MIN_SURFAREA", "COMPATIBILITY",
+    "SKIP_STEADY_STATE", "TEMPDIR", "IGNORE_RAINFALL", "FORCE_MAIN_EQUATION", "LINK_OFFSETS",
+    "MIN_SLOPE", "IGNORE_SNOWMELT", "IGNORE_GROUNDWATER", "IGNORE_ROUTING", "IGNORE_QUALITY",
+    "MAX_TRIALS", "HEAD_TOLERANCE", "SYS_FLOW_TOL", "LAT_FLOW_TOL", "IGNORE_RDII",
+    "MINIMUM_STEP", "THREADS", "SURCHARGE_METHOD", nullptr};
+
+// ========================================================= unit conversion
+// swmm5.c:105-120 (Ucf / Qcf) and UCF() swmm5.c:1378-1388
+double Project::ucfLength() const { return opt.unitSystem ? 0.3048 : 1.0; }
+double Project::ucfVolume() const { return opt.unitSystem ? 0.02832 : 1.0; }
+double Project::ucfRainfall() const { return opt.unitSystem ? 1097280.0 : 43200.0; }
+double Project::ucfEvapRate() const { return opt.unitSystem ? 26334720.0 : 1036800.0; }
+double Project::ucfFlow() const
+{
+    static const double qcf[6] = {1.0, 448.831, 0.64632, 0.02832, 28.317, 2.4466};
+    return qcf[opt.flowUnits];
+}
+
+int Project::setError(int code, const std::string& msg)
+{
+    if (!errorCode) {
+        errorCode = code;
+        errorMsg = msg;
+    }
+    return code;
+}
+
+// ============================================================ .inp reading
+int Project::open(const char* path)
+{
+    if (readFile(path)) return errorCode;
+    // project.c:147-181 -- run dates and durations
+    opt.startDateTime = opt.startDate + opt.startTime;
+    opt.endDateTime = opt.endDate + opt.endTime;
+    opt.reportStart = gmax(opt.reportStartDate + opt.reportStartTime, opt.startDateTime);
+    if (opt.endDateTime <= opt.startDateTime) return setError(191, "ERROR 191: simulation start date comes after ending date.");
+    if (opt.endDateTime <= opt.reportStart) return setError(193, "ERROR 193: report start date comes after ending date.");
+    opt.totalDuration = floor((opt.endDateTime - opt.startDateTime) * kSecPerDay);
+    if ((double)opt.reportStep > opt.totalDuration) opt.reportStep = (int)opt.totalDuration;
+    if ((double)opt.reportStep < opt.routeStep) return setError(195, "ERROR 195: reporting time step or duration is less than routing time step.");
+    opt.totalDuration *= 1000.0;
+    validate();
+    return errorCode;
+}
+
+int Project::readFile(const char* path)
+{
+    FILE* f = fopen(path, "rb");
+    if (!f) return setError(303, std::string("ERROR 303: cannot open input file ") + path);
+    std::vector<char> buf;
+    fseek(f, 0, SEEK_END);
+    long sz = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    buf.resize((size_t)sz + 2);
+    size_t got = fread(buf.data(), 1, (size_t)sz, f);
+    fclose(f);
+    buf[got] = '\n';
+    buf[got + 1] = '\0';
+
+    // split into lines once; each pass tokenises its own copy
+    std::vector<std::pair<size_t, size_t>> lines;
+    lines.reserve(got / 32 + 16);
+    size_t st0 = 0;
+    for (size_t i = 0; i <= got; i++)
+        if (buf[i] == '\n') { lines.push_back({st0, i}); st0 = i + 1; }
+
+    std::vector<char> work;
+    std::vector<char*> tok;
+    for (int pass = 1; pass <= 2; pass++) {
+        int sect = S_NONE;
+        for (size_t li = 0; li < lines.size(); li++) {
+            size_t a = lines[li].first, b = lines[li].second;
+            work.assign(buf.begin() + a, buf.begin() + b);
+            work.push_back('\0');
+            int nt = tokenize(work.data(), tok);
+            if (nt == 0 || tok[0][0] == ';') continue;
+            if (tok[0][0] == '[') {
+                int s = kfind(tok[0], kSectWords);
+                if (s >= 0) { sect = s; continue; }
+                if (kfind(tok[0], kSkipWords) >= 0) { sect = S_SKIP; continue; }
+                return setError(200, std::string("ERROR 200: input section ") + tok[0] +
+                                          " is not supported by the MI355X dynamic-wave engine");
+            }
+            if (sect == S_TITLE) {
+                if (pass == 2 && net.title.empty()) {
+                    std::string t(buf.begin() + a, buf.begin() + b);
+                    while (!t.empty() && (t.back() == '\r' || t.back() == '\n')) t.pop_back();
+                    net.title = t;
+                }
+                continue;
+            }
+            if (sect == S_SKIP || sect == S_NONE) continue;
+            int err = parseLine(sect, tok, pass);
+            if (err) {
+                if (!errorCode) {
+                    char msg[512];
+                    snprintf(msg, sizeof msg, "ERROR %d: input error at line %zu", err, li + 1);
+                    setError(200, msg);
+                }
+                return errorCode;
+            }
+        }
+        if (pass == 1) {
+            // allocate per-object arrays (createObjects, project.c) -- filled in pass 2
+            int nn = (int)net.nodeId.size(), nl = (int)net.linkId.size();
+            net.nodeType.assign(nn, JUNCTION); net.nodeSub.assign(nn, 0); net.degree.assign(nn, 0);
+            net.rptFlag.assign(nn, 0); net.invertElev.assign(nn, 0); net.initDepth.assign(nn, 0);
+            net.fullDepth.assign(nn, 0); net.surDepth.assign(nn, 0); net.pondedArea.assign(nn, 0);
+            net.crownElev.assign(nn, 0); net.fullVolume.assign(nn, 0); net.outfallType.assign(nn, -1);
+            net.outfallFlap.assign(nn, 0); net.outfallSeries.assign(nn, -1); net.fixedStage.assign(nn, 0);
+            net.linkType.assign(nl, CONDUIT); net.node1.assign(nl, 0); net.node2.assign(nl, 0);
+            net.hasFlapGate.assign(nl, 0); net.direction.assign(nl, 1); net.barrels.assign(nl, 1);
+            net.hasLosses.assign(nl, 0); net.superCritical.assign(nl, 0); net.linkRpt.assign(nl, 0);
+            for (auto* v : {&net.offset1, &net.offset2, &net.q0, &net.qLimit, &net.cLossInlet,
+                            &net.cLossOutlet, &net.cLossAvg, &net.seepRate, &net.length,
+                            &net.roughness, &net.modLength, &net.roughFactor, &net.slope,
+                            &net.beta, &net.qMax, &net.qFull})
+                v->assign(nl, 0.0);
+            net.xsect.assign(nl, Xsect());
+            for (auto& ts : net.tseries) ts.lastDate = opt.startDate + opt.startTime;  // input.c:168-171
+            for (auto& p : net.patterns) { p.type = -1; p.count = 0; for (double& x : p.factor) x = 1.0; }
+        }
+    }
+    return errorCode;
+}
+
+static int addId(std::unordered_map<std::string, int>& idx, std::vector<std::string>& ids,
+                 const char* id)
+{
+    auto it = idx.find(id);
+    if (it != idx.end()) return -1;
+    int n = (int)ids.size();
+    idx.emplace(id, n);
+    ids.push_back(id);
+    return n;
+}
+
+int Project::parseLine(int sect, std::vector<char*>& tok, int pass)
+{
+    int nt = (int)tok.size();
+    if (pass == 1) {
+        switch (sect) {
+        case S_OPTION:
+            if (nt < 2) return 203;
+            return readOption(tok[0], tok[1]);
+        case S_JUNC:
+        case S_OUTFALL:
+            if (addId(net.nodeIndex, net.nodeId, tok[0]) < 0) return setError(207, std::string("ERROR 207: duplicate ID name ") + tok[0]);
+            return 0;
+        case S_CONDUIT:
+            if (addId(net.linkIndex, net.linkId, tok[0]) < 0) return setError(207, std::string("ERROR 207: duplicate ID name ") + tok[0]);
+            return 0;
+        case S_POLLUT: {
+            std::vector<std::string> ids;
+            for (auto& p : net.pollut) ids.push_back(p.id);
+            if (net.pollutIndex.count(tok[0])) return setError(207, std::string("ERROR 207: duplicate ID name ") + tok[0]);
+            net.pollutIndex.emplace(tok[0], (int)net.pollut.size());
+            Pollutant p;
+            p.id = tok[0];
+            net.pollut.push_back(p);
+            return 0;
+        }
+        case S_PATTERN:
+            if (!net.patternIndex.count(tok[0])) {
+                net.patternIndex.emplace(tok[0], (int)net.patterns.size());
+                Pattern p;
+                p.id = tok[0];
+                net.patterns.push_back(p);
+            }
+            return 0;
+        case S_TSERIES:
+            if (!net.tseriesIndex.count(tok[0])) {
+                net.tseriesIndex.emplace(tok[0], (int)net.tseries.size());
+                Tseries t;
+                t.id = tok[0];
+                net.tseries.push_back(t);
+            }
+            return 0;
+        default:
+            return 0;
+        }
+    }
+    switch (sect) {
+    case S_OPTION: return 0;
+    case S_EVAP: return readEvap(tok);
+    case S_JUNC: return readJunction(tok);
+    case S_OUTFALL: return readOutfall(tok);
+    case S_CONDUIT: return readConduit(tok);
+    case S_XSECT: return readXsect(tok);
+    case S_LOSS: return readLoss(tok);
+    case S_POLLUT: return readPollutant(tok);
+    case S_INFLOW: return readInflow(tok);
+    case S_DWF: return readDwf(tok);
+    case S_PATTERN: return readPattern(tok);
+    case S_TSERIES: return readTimeseries(tok);
+    case S_REPORT: return readReport(tok);
+    default: return 0;
+    }
+}
+
+static int hmsSeconds(double aTime)
+{
+    int h, m, s;
+    decodeTime(aTime, &h, &m, &s);
+    h += 24 * (int)aTime;
+    return s + 60 * m + 3600 * h;
+}
+
+int Project::readOption(const char* s1, const char* s2)  // project.c:445-769
+{
+    int k = kfind(s1, kOptionWords), m;
+    double t, aTime;
+    if (k < 0) return 205;
+    switch (k) {
+    case O_FLOW_UNITS:
+        m = kfind(s2, kFlowUnitWords);
+        if (m < 0) return 205;
+        opt.flowUnits = m;
+        opt.unitSystem = (m <= MGD) ? 0 : 1;
+        break;
+    case O_ROUTE_MODEL:
+        m = kfind(s2, kRouteWords);
+        if (m < 0) m = kfind(s2, kOldRouteWords);
+        if (m < 0) return 205;
+        if (m == 0) opt.ignoreRouting = 1;
+        else opt.routeModel = m;
+        if (opt.routeModel != RM_DW || opt.ignoreRouting)
+            return setError(200, "ERROR 200: only FLOW_ROUTING DYNWAVE is supported by the MI355X engine");
+        break;
+    case O_START_DATE: if (!strToDate(s2, &opt.startDate)) return 213; break;
+    case O_START_TIME: if (!strToTime(s2, &opt.startTime)) return 213; break;
+    case O_END_DATE: if (!strToDate(s2, &opt.endDate)) return 213; break;
+    case O_END_TIME: if (!strToTime(s2, &opt.endTime)) return 213; break;
+    case O_REPORT_START_DATE:
+        if (!strToDate(s2, &opt.reportStartDate)) return 213;
+        opt.haveReportStartDate = true;
+        break;
+    case O_REPORT_START_TIME:
+        if (!strToTime(s2, &opt.reportStartTime)) return 213;
+        opt.haveReportStartTime = true;
+        break;
+    case O_WET_STEP: case O_DRY_STEP: case O_REPORT_STEP: case O_RULE_STEP: {
+        if (!strToTime(s2, &aTime)) return 213;
+        int s = hmsSeconds(aTime);
+        if (k == O_RULE_STEP) { if (s < 0) return 211; }
+        else if (s <= 0) return 211;
+        if (k == O_WET_STEP) opt.wetStep = s;
+        else if (k == O_DRY_STEP) opt.dryStep = s;
+        else if (k == O_REPORT_STEP) opt.reportStep = s;
+        else opt.ruleStep = s;
+        if (k == O_RULE_STEP && s > 0)
+            return setError(200, "ERROR 200: RULE_STEP (control rules) is not supported by the MI355X engine");
+        break;
+    }
+    case O_INERT_DAMPING:
+        m = kfind(s2, kInertWords);
+        if (m < 0) return 205;
+        opt.inertDamping = m;
+        break;
+    case O_ALLOW_PONDING: case O_SLOPE_WEIGHTING: case O_SKIP_STEADY_STATE:
+    case O_IGNORE_RAINFALL: case O_IGNORE_SNOWMELT: case O_IGNORE_GWATER:
+    case O_IGNORE_ROUTING: case O_IGNORE_QUALITY: case O_IGNORE_RDII:
+        m = kfind(s2, kNoYes);
+        if (m < 0) return 205;
+        if (k == O_ALLOW_PONDING) opt.allowPonding = m;
+        else if (k == O_SKIP_STEADY_STATE) opt.skipSteadyState = m;
+        else if (k == O_IGNORE_ROUTING) opt.ignoreRouting = m;
+        else if (k == O_IGNORE_QUALITY) opt.ignoreQuality = m;
+        if (opt.skipSteadyState)
+            return setError(200, "ERROR 200: SKIP_STEADY_STATE is not supported by the MI355X engine");
+        if (opt.ignoreRouting)
+            return setError(200, "ERROR 200: IGNORE_ROUTING leaves nothing for the routing engine to do");
+        break;
+    case O_NORMAL_FLOW_LTD:
+        m = kfind(s2, kNormalWords);
+        if (m < 0) return 205;
+        opt.normalFlowLtd = m;
+        break;
+    case O_FORCE_MAIN_EQN:
+        m = kfind(s2, kForceMainWords);
+        if (m < 0) return 205;
+        opt.forceMainEqn = m;
+        break;
+    case O_LINK_OFFSETS:
+        m = kfind(s2, kOffsetWords);
+        if (m < 0) return 205;
+        opt.linkOffsetsElev = m;
+        break;
+    case O_ROUTE_STEP: case O_LENGTHENING_STEP:
+        if (!getDouble(s2, &t)) {
+            if (!strToTime(s2, &aTime)) return 211;
+            t = hmsSeconds(aTime);
+        }
+        if (k == O_ROUTE_STEP) {
+            if (t <= 0.0) return 211;
+            opt.routeStep = t;
+        } else {
+            opt.lengtheningStep = gmax(0.0, t);
+        }
+        break;
+    case O_MIN_ROUTE_STEP:
+        if (!getDouble(s2, &opt.minRouteStep) || opt.minRouteStep < 0.0) return 211;
+        break;
+    case O_NUM_THREADS:
+        m = atoi(s2);
+        if (m < 0) return 211;
+        opt.numThreads = m;
+        break;
+    case O_VARIABLE_STEP:
+        if (!getDouble(s2, &opt.courantFactor)) return 211;
+        if (opt.courantFactor < 0.0 || opt.courantFactor > 2.0) return 211;
+        break;
+    case O_MIN_SURFAREA:
+        if (!getDouble(s2, &opt.minSurfArea) || opt.minSurfArea < 0.0) return 211;
+        break;
+    case O_MIN_SLOPE:
+        if (!getDouble(s2, &opt.minSlope)) return 211;
+        if (opt.minSlope < 0.0 || opt.minSlope >= 100) return 211;
+        opt.minSlope /= 100.0;
+        break;
+    case O_MAX_TRIALS:
+        m = atoi(s2);
+        if (m < 0) return 211;
+        opt.maxTrials = m;
+        break;
+    case O_HEAD_TOL:
+        if (!getDouble(s2, &opt.headTol)) return 211;
+        break;
+    case O_SYS_FLOW_TOL:
+        if (!getDouble(s2, &opt.sysFlowTol)) return 211;
+        opt.sysFlowTol /= 100.0;
+        break;
+    case O_LAT_FLOW_TOL:
+        if (!getDouble(s2, &opt.latFlowTol)) return 211;
+        opt.latFlowTol /= 100.0;
+        break;
+    case O_SURCHARGE_METHOD:
+        m = kfind(s2, kSurchargeWords);
+        if (m < 0) return 205;
+        opt.surchargeMethod = m;
+        break;
+    default:
+        break;  // INFILTRATION, SWEEP_*, DRY_DAYS, COMPATIBILITY, TEMPDIR: no routing effect
+    }
+    return 0;
+}
+
+int Project::readEvap(std::vector<char*>& tok)  // climate.c:285 (CONSTANT only)
+{
+    if (tok.size() < 2) return 203;
+    if (kmatch(tok[0], "CONSTANT")) {
+        double x;
+        if (!getDouble(tok[1], &x) || x < 0.0) return 211;
+        opt.evapRate = x / ucfEvapRate();
+        return 0;
+    }
+    if (kmatch(tok[0], "DRY_ONLY")) return 0;
+    return setError(200, std::string("ERROR 200: EVAPORATION option ") + tok[0] +
+                             " is not supported by the MI355X engine (CONSTANT only)");
+}
+
+int Project::readJunction(std::vector<char*>& tok)  // node.c:606-648, 125-196
+{
+    int nt = (int)tok.size();
+    if (nt < 2) return 203;
+    int j = net.nodeIndex.at(tok[0]);
+    double x[6];
+    for (int i = 1; i <= 5; i++) {
+        x[i - 1] = 0.0;
+        if (i < nt && !getDouble(tok[i], &x[i - 1])) return 211;
+    }
+    for (int i = 1; i <= 4; i++)
+        if (x[i] < 0.0) return 211;
+    double u = ucfLength();
+    net.nodeType[j] = JUNCTION;
+    net.invertElev[j] = x[0] / u;
+    net.crownElev[j] = net.invertElev[j];
+    net.fullDepth[j] = x[1] / u;
+    net.initDepth[j] = x[2] / u;
+    net.surDepth[j] = x[3] / u;
+    net.pondedArea[j] = x[4] / (u * u);
+    return 0;
+}
+
+int Project::readOutfall(std::vector<char*>& tok)  // node.c:1333-1409
+{
+    int nt = (int)tok.size();
+    if (nt < 3) return 203;
+    int j = net.nodeIndex.at(tok[0]);
+    double elev;
+    if (!getDouble(tok[1], &elev)) return 211;
+    int i = kfind(tok[2], kOutfallWords);
+    if (i < 0) return 205;
+    double stage = 0.0;
+    int series = -1, flap = 0, n = 4;
+    if (i >= O_FIXED) {
+        if (nt < 4) return 203;
+        n = 5;
+        if (i == O_FIXED) {
+            if (!getDouble(tok[3], &stage)) return 211;
+        } else if (i == O_TSERIES) {
+            auto it = net.tseriesIndex.find(tok[3]);
+            if (it == net.tseriesIndex.end()) return 209;
+            series = it->second;
+        } else {
+            return setError(200, "ERROR 200: TIDAL outfalls are not supported by the MI355X engine");
+        }
+    }
+    if (nt == n) {
+        int m = kfind(tok[n - 1], kNoYes);
+        if (m < 0) return 205;
+        flap = m;
+    }
+    if (nt == n + 1)
+        return setError(200, "ERROR 200: outfalls routed to subcatchments are not supported");
+    double u = ucfLength();
+    net.nodeType[j] = OUTFALL;
+    net.invertElev[j] = elev / u;
+    net.crownElev[j] = net.invertElev[j];
+    net.outfallType[j] = i;
+    net.fixedStage[j] = stage / u;
+    net.outfallSeries[j] = series;
+    net.outfallFlap[j] = flap;
+    return 0;
+}
+
+int Project::readConduit(std::vector<char*>& tok)  // link.c:933-988, 315-399
+{
+    int nt = (int)tok.size();
+    if (nt < 7) return 203;
+    int j = net.linkIndex.at(tok[0]);
+    auto a = net.nodeIndex.find(tok[1]);
+    auto b = net.nodeIndex.find(tok[2]);
+    if (a == net.nodeIndex.end() || b == net.nodeIndex.end()) return 209;
+    double x[6];
+    if (!getDouble(tok[3], &x[0])) return 211;
+    if (!getDouble(tok[4], &x[1])) return 211;
+    if (opt.linkOffsetsElev && *tok[5] == '*') x[2] = kMissing;
+    else if (!getDouble(tok[5], &x[2])) return 211;
+    if (opt.linkOffsetsElev && *tok[6] == '*') x[3] = kMissing;
+    else if (!getDouble(tok[6], &x[3])) return 211;
+    x[4] = 0.0;
+    if (nt >= 8 && !getDouble(tok[7], &x[4])) return 211;
+    x[5] = 0.0;
+    if (nt >= 9 && !getDouble(tok[8], &x[5])) return 211;
+    double u = ucfLength(), uq = ucfFlow();
+    net.node1[j] = a->second;
+    net.node2[j] = b->second;
+    net.linkType[j] = CONDUIT;
+    net.length[j] = x[0] / u;
+    net.modLength[j] = net.length[j];
+    net.roughness[j] = x[1];
+    net.offset1[j] = x[2] / u;
+    net.offset2[j] = x[3] / u;
+    net.q0[j] = x[4] / uq;
+    net.qLimit[j] = x[5] / uq;
+    net.hasFlapGate[j] = 0;
+    net.direction[j] = 1;
+    return 0;
+}
+
+// xsect.c:216-634 for the supported shapes
+bool setXsectParams(Xsect& x, int type, double p[4], double ucf)
+{
+    if (type != X_DUMMY && p[0] <= 0.0) return false;
+    x.type = type;
+    switch (type) {
+    case X_DUMMY:
+        x.yFull = x.wMax = x.aFull = x.rFull = x.sFull = x.sMax = 1.E-6;
+        break;
+    case X_CIRCULAR:
+        x.yFull = p[0] / ucf;
+        x.wMax = x.yFull;
+        x.aFull = kPi / 4.0 * x.yFull * x.yFull;
+        x.rFull = 0.2500 * x.yFull;
+        x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
+        x.sMax = 1.08 * x.sFull;
+        x.ywMax = 0.5 * x.yFull;
+        break;
+    case X_RECT_CLOSED: {
+        if (p[1] <= 0.0) return false;
+        x.yFull = p[0] / ucf;
+        x.wMax = p[1] / ucf;
+        x.aFull = x.yFull * x.wMax;
+        x.rFull = x.aFull / (2.0 * (x.yFull + x.wMax));
+        x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
+        double aMax = 0.97 * x.aFull;
+        Geom g{x.type, x.yFull, x.wMax, x.ywMax, x.aFull, x.rFull, x.sFull, x.sMax,
+               x.yBot, x.aBot, x.sBot, x.rBot};
+        x.sMax = aMax * pow(rectClosedRofA(g, aMax), 2. / 3.);
+        x.ywMax = x.yFull;
+        break;
+    }
+    case X_RECT_OPEN:
+        if (p[1] <= 0.0) return false;
+        x.yFull = p[0] / ucf;
+        x.wMax = p[1] / ucf;
+        if (p[2] < 0.0 || p[2] > 2.0) return false;
+        x.sBot = p[2];
+        x.aFull = x.yFull * x.wMax;
+        x.rFull = x.aFull / ((2.0 - x.sBot) * x.yFull + x.wMax);
+        x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
+        x.sMax = x.sFull;
+        x.ywMax = x.yFull;
+        break;
+    case X_TRAPEZOIDAL:
+        if (p[1] < 0.0 || p[2] < 0.0 || p[3] < 0.0) return false;
+        x.yFull = p[0] / ucf;
+        x.ywMax = x.yFull;
+        x.yBot = p[1] / ucf;
+        x.sBot = (p[2] + p[3]) / 2.0;
+        if (x.yBot == 0.0 && x.sBot == 0.0) return false;
+        x.rBot = sqrt(1.0 + p[2] * p[2]) + sqrt(1.0 + p[3] * p[3]);
+        x.wMax = x.yBot + x.yFull * (p[2] + p[3]);
+        x.aFull = (x.yBot + x.sBot * x.yFull) * x.yFull;
+        x.rFull = x.aFull / (x.yBot + x.yFull * x.rBot);
+        x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
+        x.sMax = x.sFull;
+        break;
+    case X_TRIANGULAR:
+        if (p[1] <= 0.0) return false;
+        x.yFull = p[0] / ucf;
+        x.wMax = p[1] / ucf;
+        x.ywMax = x.yFull;
+        x.sBot = x.wMax / x.yFull / 2.;
+        x.rBot = sqrt(1. + x.sBot * x.sBot);
+        x.aFull = x.yFull * x.yFull * x.sBot;
+        x.rFull = x.aFull / (2.0 * x.yFull * x.rBot);
+        x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
+        x.sMax = x.sFull;
+        break;
+    default:
+        return false;
+    }
+    return true;
+}
+
+int Project::readXsect(std::vector<char*>& tok)  // link.c:162-267
+{
+    int nt = (int)tok.size();
+    if (nt < 3) return 203;
+    auto it = net.linkIndex.find(tok[0]);
+    if (it == net.linkIndex.end()) return 209;
+    int j = it->second;
+    int k = kfind(tok[1], kXsectWords);
+    if (k < 0) return 205;
+    net.barrels[j] = 1;
+    net.xsect[j].culvertCode = 0;
+    if (!(k == X_CIRCULAR || k == X_RECT_CLOSED || k == X_RECT_OPEN || k == X_TRAPEZOIDAL ||
+          k == X_TRIANGULAR))
+        return setError(200, std::string("ERROR 200: cross-section shape ") + tok[1] +
+                                 " is not supported by the MI355X engine yet");
+    if (nt < 6) return 203;
+    double x[4];
+    for (int i = 2; i <= 5; i++)
+        if (!getDouble(tok[i], &x[i - 2])) return 211;
+    if (!setXsectParams(net.xsect[j], k, x, ucfLength())) return 211;
+    if (nt >= 7) {
+        int i = atoi(tok[6]);
+        if (i <= 0) return 211;
+        net.barrels[j] = (int)(signed char)i;
+    }
+    if (nt >= 8) {
+        int i = atoi(tok[7]);
+        if (i < 0) return 211;
+        if (i > 0) return setError(200, "ERROR 200: culvert inlet control is not supported by the MI355X engine yet");
+        net.xsect[j].culvertCode = i;
+    }
+    return 0;
+}
+
+int Project::readLoss(std::vector<char*>& tok)  // link.c:271-311
+{
+    int nt = (int)tok.size();
+    if (nt < 4) return 203;
+    auto it = net.linkIndex.find(tok[0]);
+    if (it == net.linkIndex.end()) return 209;
+    int j = it->second;
+    double x[3], seep = 0.0;
+    for (int i = 1; i <= 3; i++)
+        if (!getDouble(tok[i], &x[i - 1]) || x[i - 1] < 0.0) return 211;
+    int k = 0;
+    if (nt >= 5) {
+        k = kfind(tok[4], kNoYes);
+        if (k < 0) return 205;
+    }
+    if (nt >= 6 && !getDouble(tok[5], &seep)) return 211;
+    net.cLossInlet[j] = x[0];
+    net.cLossOutlet[j] = x[1];
+    net.cLossAvg[j] = x[2];
+    net.hasFlapGate[j] = k;
+    net.seepRate[j] = seep / ucfRainfall();
+    return 0;
+}
+
+int Project::readPollutant(std::vector<char*>& tok)  // landuse.c:readPollutParams
+{
+    int nt = (int)tok.size();
+    if (nt < 6) return 203;
+    int j = net.pollutIndex.at(tok[0]);
+    int k = kfind(tok[1], kQualUnitWords);
+    if (k < 0) return 205;
+    double x[4];
+    for (int i = 2; i <= 4; i++)
+        if (!getDouble(tok[i], &x[i - 2]) || x[i - 2] < 0.0) return 211;
+    if (!getDouble(tok[5], &x[3])) return 211;
+    double cDWF = 0.0, cInit = 0.0;
+    if (nt >= 7 && kfind(tok[6], kNoYes) < 0) return 205;
+    if (nt >= 9 && strcmp(tok[7], "*") != 0)
+        return setError(200, "ERROR 200: co-pollutants are not supported by the MI355X engine");
+    if (nt >= 10 && (!getDouble(tok[9], &cDWF) || cDWF < 0.0)) return 211;
+    if (nt >= 11 && (!getDouble(tok[10], &cInit) || cInit < 0.0)) return 211;
+    Pollutant& p = net.pollut[j];
+    p.units = k;
+    double ucfMass = opt.unitSystem ? 1.0e-6 : 2.203e-6;
+    p.mcf = (k == CU_MG) ? ucfMass : (k == CU_UG ? ucfMass / 1000.0 : 1.0);
+    p.cRain = x[0];
+    p.cGW = x[1];
+    p.cRDII = x[2];
+    p.kDecay = x[3] / kSecPerDay;
+    p.cDWF = cDWF;
+    p.cInit = cInit;
+    return 0;
+}
+
+int Project::readInflow(std::vector<char*>& tok)  // inflow.c:41-134
+{
+    int nt = (int)tok.size();
+    if (nt < 3) return 203;
+    auto nit = net.nodeIndex.find(tok[0]);
+    if (nit == net.nodeIndex.end()) return 209;
+    ExtInflow in;
+    in.node = nit->second;
+    in.type = EXT_CONCEN;
+    auto pit = net.pollutIndex.find(tok[1]);
+    if (pit == net.pollutIndex.end()) {
+        if (kmatch(tok[1], "FLOW")) in.param = -1;
+        else return 209;
+    } else {
+        in.param = pit->second;
+    }
+    if (strlen(tok[2]) > 0) {
+        auto t = net.tseriesIndex.find(tok[2]);
+        if (t == net.tseriesIndex.end()) return 209;
+        in.tseries = t->second;
+    }
+    double cf = 1.0, sf = 1.0, baseline = 0.0;
+    if (in.param == -1) {
+        in.type = EXT_FLOW;
+        cf = 1.0 / ucfFlow();
+    }
+    if (nt >= 4 && in.param > -1) {
+        if (kmatch(tok[3], "CONCEN")) in.type = EXT_CONCEN;
+        else if (kmatch(tok[3], "MASS")) in.type = EXT_MASS;
+        else return 205;
+        if (nt >= 5 && in.type == EXT_MASS) {
+            if (!getDouble(tok[4], &cf)) return 211;
+            if (cf <= 0.0) return 211;
+        }
+    }
+    if (nt >= 6 && !getDouble(tok[5], &sf)) return 211;
+    if (nt >= 7 && !getDouble(tok[6], &baseline)) return 211;
+    if (nt >= 8) {
+        auto p = net.patternIndex.find(tok[7]);
+        if (p == net.patternIndex.end()) return 209;
+        in.basePat = p->second;
+    }
+    if (in.type == EXT_MASS) cf /= kLperFT3;
+    in.cFactor = cf;
+    in.sFactor = sf;
+    in.baseline = baseline;
+    // replace an existing inflow for the same constituent (inflow.c:153-184)
+    long long key = (long long)in.node * 1024 + (in.param + 1);
+    auto it = extKey_.find(key);
+    if (it != extKey_.end()) { net.extInflows[it->second] = in; return 0; }
+    extKey_.emplace(key, (int)net.extInflows.size());
+    net.extInflows.push_back(in);
+    return 0;
+}
+
+int Project::readDwf(std::vector<char*>& tok)  // inflow.c:237-306
+{
+    int nt = (int)tok.size();
+    if (nt < 3) return 203;
+    auto nit = net.nodeIndex.find(tok[0]);
+    if (nit == net.nodeIndex.end()) return 209;
+    DwfInflow in;
+    in.node = nit->second;
+    auto pit = net.pollutIndex.find(tok[1]);
+    if (pit == net.pollutIndex.end()) {
+        if (kmatch(tok[1], "FLOW")) in.param = -1;
+        else return 209;
+    } else {
+        in.param = pit->second;
+    }
+    double x;
+    if (!getDouble(tok[2], &x)) return 211;
+    if (in.param == -1) x /= ucfFlow();
+    in.avgValue = x;
+    for (int i = 3; i < 7 && i < nt; i++) {
+        if (strlen(tok[i]) == 0) continue;
+        auto p = net.patternIndex.find(tok[i]);
+        if (p == net.patternIndex.end()) return 209;
+        in.patterns[i - 3] = p->second;
+    }
+    long long key = (long long)in.node * 1024 + (in.param + 1);
+    auto it = dwfKey_.find(key);
+    if (it != dwfKey_.end()) { net.dwfInflows[it->second] = in; return 0; }
+    dwfKey_.emplace(key, (int)net.dwfInflows.size());
+    net.dwfInflows.push_back(in);
+    return 0;
+}
+
+int Project::readPattern(std::vector<char*>& tok)  // inflow.c:410-452
+{
+    int nt = (int)tok.size();
+    if (nt < 2) return 203;
+    Pattern& p = net.patterns[net.patternIndex.at(tok[0])];
+    int n = 1;
+    if (p.type < 0) {
+        int k = kfind(tok[1], kPatternWords);
+        if (k < 0) return 205;
+        p.type = k;
+        n = 2;
+    }
+    while (nt > n && p.count < 24) {
+        if (!getDouble(tok[n], &p.factor[p.count])) return 211;
+        p.count++;
+        n++;
+    }
+    return 0;
+}
+
+int Project::readTimeseries(std::vector<char*>& tok)  // table.c:113-202
+{
+    int nt = (int)tok.size();
+    if (nt < 3) return 203;
+    Tseries& ts = net.tseries[net.tseriesIndex.at(tok[0])];
+    if (kmatch(tok[1], "FILE"))
+        return setError(200, "ERROR 200: external time series files are not supported by the MI355X engine");
+    double x = 0.0, y, d, t;
+    int k = 1, state = 1;
+    while (k < nt) {
+        switch (state) {
+        case 1:
+            if (strToDate(tok[k], &d)) {
+                ts.lastDate = d;
+                k++;
+            }
+            state = 2;
+            break;
+        case 2:
+            if (k >= nt) return 203;
+            if (getDouble(tok[k], &t)) t /= 24.0;
+            else if (!strToTime(tok[k], &t)) return 211;
+            x = ts.lastDate + t;
+            k++;
+            state = 3;
+            break;
+        case 3:
+            if (k >= nt) return 203;
+            if (!getDouble(tok[k], &y)) return 211;
+            ts.x.push_back(x);
+            ts.y.push_back(y);
+            k++;
+            state = 1;
+            break;
+        }
+    }
+    return 0;
+}
+
+int Project::readReport(std::vector<char*>& tok)  // report.c:report_readOptions
+{
+    int nt = (int)tok.size();
+    if (nt < 2) return 203;
+    static const char* const kReportWords[] = {"DISABLED", "INPUT", "SUBCATCH", "NODE", "LINK",
+                                               "CONTINUITY", "FLOWSTATS", "CONTROL", "AVERAGES",
+                                               "NODESTATS", nullptr};
+    int k = kfind(tok[0], kReportWords);
+    if (k < 0) return 205;
+    if (k < 2 || k > 4) {
+        int m = kfind(tok[1], kNoYes);
+        if (m < 0) return 205;
+        switch (k) {
+        case 0: rpt.disabled = m; break;
+        case 1: rpt.input = m; break;
+        case 5: rpt.continuity = m; break;
+        case 6: rpt.flowStats = m; break;
+        case 7: rpt.controls = m; break;
+        case 8: rpt.averages = m; break;
+        default: break;
+        }
+        if (rpt.averages)
+            return setError(200, "ERROR 200: REPORT AVERAGES is not supported by the MI355X engine yet");
+        return 0;
+    }
+    int flag;
+    if (strcasecmp(tok[1], "NONE") == 0) flag = 0;
+    else if (strcasecmp(tok[1], "ALL") == 0) flag = 1;
+    else {
+        flag = 2;
+        for (int t = 1; t < nt; t++) {
+            if (k == 3) {
+                auto it = net.nodeIndex.find(tok[t]);
+                if (it == net.nodeIndex.end()) return 209;
+                net.rptFlag[it->second] = 1;
+            } else if (k == 4) {
+                auto it = net.linkIndex.find(tok[t]);
+                if (it == net.linkIndex.end()) return 209;
+                net.linkRpt[it->second] = 1;
+            }
+        }
+    }
+    if (k == 2) rpt.subcatchAll = flag;
+    else if (k == 3) rpt.nodesAll = flag;
+    else rpt.linksAll = flag;
+    return 0;
+}
+
+// ============================================================== validation
+// link.c:1258-1300
+static double conduitSlope(const Network& n, int j, const Options& o, int* warn)
+{
+    double length = n.length[j];
+    double elev1 = n.offset1[j] + n.invertElev[n.node1[j]];
+    double elev2 = n.offset2[j] + n.invertElev[n.node2[j]];
+    double delta = fabs(elev1 - elev2), slope;
+    if (delta < kMinDeltaZ) { (*warn)++; delta = kMinDeltaZ; }
+    if (delta >= length) { (*warn)++; slope = delta / length; }
+    else slope = delta / sqrt((length * length) - (delta * delta));
+    if (o.minSlope > 0.0 && slope < o.minSlope) { (*warn)++; slope = o.minSlope; }
+    if (elev1 < elev2) slope = -slope;
+    return slope;
+}
+
+void Project::validateConduit(int j)  // link.c:992-1154 (supported shapes)
+{
+    Xsect& xs = net.xsect[j];
+    if (xs.type < 0) { setError(117, "ERROR 117: no cross section defined for link " + net.linkId[j]); return; }
+    if (net.length[j] <= 0.0) { setError(111, "ERROR 111: invalid length for Conduit " + net.linkId[j]); return; }
+    if (net.roughness[j] <= 0.0) { setError(113, "ERROR 113: invalid roughness for Conduit " + net.linkId[j]); return; }
+    if (net.barrels[j] <= 0) { setError(114, "ERROR 114: invalid number of barrels for Conduit " + net.linkId[j]); return; }
+    if (xs.aFull <= 0.0) { setError(119, "ERROR 119: invalid cross section for link " + net.linkId[j]); return; }
+    if (net.offset1[j] < 0.0) { warnings++; net.offset1[j] = 0.0; }
+    if (net.offset2[j] < 0.0) { warnings++; net.offset2[j] = 0.0; }
+    double slope = conduitSlope(net, j, opt, &warnings);
+    net.slope[j] = slope;
+    if (slope < 0.0 && xs.type != X_DUMMY) {           // conduit_reverse link.c:1158-1191
+        std::swap(net.node1[j], net.node2[j]);
+        std::swap(net.offset1[j], net.offset2[j]);
+        std::swap(net.cLossInlet[j], net.cLossOutlet[j]);
+        net.slope[j] = -net.slope[j];
+        net.direction[j] *= -1;
+        net.q0[j] = -net.q0[j];
+    }
+    double roughness = net.roughness[j];
+    double lengthFactor = 1.0;
+    if (opt.lengtheningStep > 0.0 && xs.type != X_DUMMY) {   // link.c:1217-1254
+        Geom g{xs.type, xs.yFull, xs.wMax, xs.ywMax, xs.aFull, xs.rFull, xs.sFull, xs.sMax,
+               xs.yBot, xs.aBot, xs.sBot, xs.rBot};
+        double yFull = xs.yFull;
+        if (isOpen(xs.type)) yFull = xs.aFull / getWofY(g, yFull, &SWX_CIRC_TABLES[0][0]);
+        double vFull = kPhi / roughness * xs.sFull * sqrt(fabs(net.slope[j])) / xs.aFull;
+        double tStep = (opt.lengtheningStep == 0.0) ? opt.routeStep
+                                                    : gmin(opt.routeStep, opt.lengtheningStep);
+        double ratio = (sqrt(kGravity * yFull) + vFull) * tStep / net.length[j];
+        lengthFactor = ratio > 1.0 ? ratio : 1.0;
+    }
+    if (lengthFactor != 1.0) {
+        net.modLength[j] = lengthFactor * net.length[j];
+        slope /= lengthFactor;
+        roughness = roughness / sqrt(lengthFactor);
+    }
+    net.roughFactor[j] = kGravity * ((roughness / kPhi) * (roughness / kPhi));
+    net.beta[j] = (xs.type == X_DUMMY) ? 0.0 : kPhi * sqrt(fabs(slope)) / roughness;
+    net.qFull[j] = xs.sFull * net.beta[j];
+    net.qMax[j] = xs.sMax * net.beta[j];
+    double aa = net.beta[j] / sqrt(32.2) * pow(xs.yFull, 0.1666667) * 0.3;
+    net.superCritical[j] = (aa >= 1.0) ? 1 : 0;
+    net.hasLosses[j] = (net.cLossInlet[j] == 0.0 && net.cLossOutlet[j] == 0.0 &&
+                        net.cLossAvg[j] == 0.0) ? 0 : 1;
+}
+
+void Project::validate()  // project.c:186-270
+{
+    int nn = net.nNodes(), nl = net.nLinks();
+    for (auto& ts : net.tseries)
+        for (size_t i = 1; i < ts.x.size(); i++)
+            if (ts.x[i] <= ts.x[i - 1]) { setError(173, "ERROR 173: time series " + ts.id + " has its data out of sequence."); return; }
+    for (int j = 0; j < nl; j++) {
+        if (opt.linkOffsetsElev) {                       // link.c:468-504
+            for (int e = 0; e < 2; e++) {
+                double& off = e == 0 ? net.offset1[j] : net.offset2[j];
+                double elev = net.invertElev[e == 0 ? net.node1[j] : net.node2[j]];
+                if (off <= kMissing) { off = 0.0; continue; }
+                off -= elev;
+                if (off >= 0.0) continue;
+                if (off >= -kMinDeltaZ) { off = 0.0; continue; }
+                warnings++;
+                off = 0.0;
+            }
+        }
+        validateConduit(j);
+        if (errorCode) return;
+        int n = net.node1[j];                             // link.c:440-463
+        net.fullDepth[n] = gmax(net.fullDepth[n], net.offset1[j] + net.xsect[j].yFull);
+        n = net.node2[j];
+        net.fullDepth[n] = gmax(net.fullDepth[n], net.offset2[j] + net.xsect[j].yFull);
+    }
+    for (int j = 0; j < nn; j++)
+        if (net.initDepth[j] > net.fullDepth[j] + net.surDepth[j]) {
+            setError(138, "ERROR 138: initial depth greater than maximum depth for Node " + net.nodeId[j]);
+            return;
+        }
+    // DWF pattern ordering (inflow.c:331-354)
+    for (auto& d : net.dwfInflows) {
+        int tmp[4] = {-1, -1, -1, -1};
+        for (int i = 0; i < 4; i++)
+            if (d.patterns[i] >= 0) tmp[net.patterns[d.patterns[i]].type] = d.patterns[i];
+        for (int i = 0; i < 4; i++) d.patterns[i] = tmp[i];
+    }
+    if (opt.routeStep > (double)opt.wetStep) { warnings++; opt.routeStep = opt.wetStep; }
+    // report flags
+    if (rpt.nodesAll == 1) for (int j = 0; j < nn; j++) net.rptFlag[j] = 1;
+    if (rpt.linksAll == 1) for (int j = 0; j < nl; j++) net.linkRpt[j] = 1;
+    // dynwave_validate (dynwave.c:177-191)
+    if (opt.minRouteStep > opt.routeStep) opt.minRouteStep = opt.routeStep;
+    if (opt.minRouteStep < 0.001) opt.minRouteStep = 0.001;
+    if (opt.minSurfArea == 0.0) opt.minSurfArea = 12.566;
+    else opt.minSurfArea /= ucfLength() * ucfLength();
+    if (opt.headTol == 0.0) opt.headTol = 0.005;
+    else opt.headTol /= ucfLength();
+    if (opt.maxTrials == 0) opt.maxTrials = 8;
+    // toposort DW degree (toposort.c:57-90)
+    for (int j = 0; j < nn; j++) net.degree[j] = 0;
+    for (int i = 0; i < nl; i++) {
+        int n = net.node1[i];
+        if (net.direction[i] < 0) n = net.node2[i];
+        if (net.nodeType[n] == OUTFALL) {
+            n = (net.direction[i] < 0) ? net.node1[i] : net.node2[i];
+            net.degree[n]++;
+        } else {
+            net.degree[n]++;
+        }
+    }
+    // validateGeneralLayout (flowrout.c:274-333)
+    std::vector<double> inCount(nn, 0.0);
+    for (int j = 0; j < nl; j++) {
+        int i = net.node1[j];
+        if (net.nodeType[i] != OUTFALL) i = net.node2[j];
+        inCount[i] += 1.0;
+    }
+    int outletCount = 0;
+    for (int i = 0; i < nn; i++)
+        if (net.nodeType[i] == OUTFALL) {
+            if (net.degree[i] + (int)inCount[i] > 1) {
+                setError(141, "ERROR 141: Outfall " + net.nodeId[i] + " has more than 1 inlet link or an outlet link.");
+                return;
+            }
+            outletCount++;
+        }
+    if (outletCount == 0) { setError(145, "ERROR 145: drainage system has no acceptable outlet nodes."); return; }
+    for (int i = 0; i < nn; i++)
+        if (inCount[i] == 0.0) net.degree[i] = -net.degree[i];
+    // crown cutoff (dynwave.c:159-160)
+    opt.crownCutoff = (opt.surchargeMethod == SUR_SLOT) ? 0.985257 : 0.96;
+}
+
+// ===================================================== initial state (start)
+void Project::initState()
+{
+    int nn = net.nNodes(), nl = net.nLinks(), P = net.nPollut();
+    const double* ct = &SWX_CIRC_TABLES[0][0];
+    auto geom = [&](int j) {
+        const Xsect& x = net.xsect[j];
+        return Geom{x.type, x.yFull, x.wMax, x.ywMax, x.aFull, x.rFull, x.sFull, x.sMax,
+                    x.yBot, x.aBot, x.sBot, x.rBot};
+    };
+    // project_init runs table_tseriesInit before routing_open
+    for (auto& ts : net.tseries) {            // table_tseriesInit (table.c:730-740)
+        ts.cur = 0;
+        ts.x1 = ts.x.empty() ? 0.0 : ts.x[0];
+        ts.y1 = ts.y.empty() ? 0.0 : ts.y[0];
+        ts.x2 = ts.x1;
+        ts.y2 = ts.y1;
+        if (ts.x.size() > 1) { ts.cur = 1; ts.x2 = ts.x[1]; ts.y2 = ts.y[1]; }
+    }
+    State& s = st;
+    auto z = [](std::vector<double>& v, int n) { v.assign(n, 0.0); };
+    for (auto* v : {&s.newDepth, &s.oldDepth, &s.newVolume, &s.oldVolume, &s.inflow, &s.outflow,
+                    &s.overflow, &s.losses, &s.newLatFlow, &s.oldLatFlow, &s.oldNetInflow,
+                    &s.oldFlowInflow, &s.oldSurfArea, &s.dYdT}) z(*v, nn);
+    for (auto* v : {&s.lNewFlow, &s.lOldFlow, &s.lNewDepth, &s.lOldDepth, &s.lNewVolume,
+                    &s.lOldVolume, &s.surfArea1, &s.surfArea2, &s.froude, &s.dqdh, &s.setting,
+                    &s.a1, &s.a2, &s.q1, &s.q2, &s.evapLossRate, &s.seepLossRate}) z(*v, nl);
+    s.flowClass.assign(nl, F_DRY);
+    s.fullState.assign(nl, 0);
+    s.normalFlow.assign(nl, 0);
+    s.capacityLimited.assign(nl, 0);
+    s.converged.assign(nn, 0);
+    z(s.nOldQual, nn * P); z(s.nNewQual, nn * P); z(s.lOldQual, nl * P); z(s.lNewQual, nl * P);
+    s.variableStep = 0.0;
+
+    // node_initState (node.c:237-289): junction volume = 0 (fullVolume 0)
+    for (int j = 0; j < nn; j++) {
+        s.oldDepth[j] = net.initDepth[j];
+        s.newDepth[j] = s.oldDepth[j];
+        net.crownElev[j] = net.invertElev[j];
+        net.fullVolume[j] = 0.0;                    // node_getVolume(j, fullDepth) = 0
+        s.oldVolume[j] = 0.0;
+        s.newVolume[j] = 0.0;
+    }
+    // link_initState (link.c:508-539) + conduit_initState (1304-1316)
+    for (int j = 0; j < nl; j++) {
+        s.lOldFlow[j] = net.q0[j];
+        s.lNewFlow[j] = net.q0[j];
+        s.setting[j] = 1.0;
+        Geom g = geom(j);
+        s.lNewDepth[j] = linkYnorm(g, net.q0[j] / net.barrels[j], net.qMax[j], net.beta[j], ct);
+        s.lOldDepth[j] = s.lNewDepth[j];
+    }
+    // flowrout_init DW (flowrout.c:75-103): dynwave_init crown elevations
+    for (int i = 0; i < nl; i++) {
+        int j = net.node1[i];
+        double zz = net.invertElev[j] + net.offset1[i] + net.xsect[i].yFull;
+        net.crownElev[j] = gmax(net.crownElev[j], zz);
+        j = net.node2[i];
+        zz = net.invertElev[j] + net.offset2[i] + net.xsect[i].yFull;
+        net.crownElev[j] = gmax(net.crownElev[j], zz);
+        s.flowClass[i] = F_DRY;
+        s.dqdh[i] = 0.0;
+    }
+    // initNodeDepths (flowrout.c:337-385)
+    std::vector<double> acc(nn, 0.0), cnt(nn, 0.0);
+    for (int i = 0; i < nl; i++) {
+        double y = (s.lNewDepth[i] > kFudge) ? s.lNewDepth[i] + net.offset1[i] : 0.0;
+        acc[net.node1[i]] += y; cnt[net.node1[i]] += 1.0;
+        acc[net.node2[i]] += y; cnt[net.node2[i]] += 1.0;
+    }
+    for (int i = 0; i < nn; i++) {
+        if (net.nodeType[i] == OUTFALL || net.nodeType[i] == STORAGE) continue;
+        if (net.initDepth[i] > 0.0) continue;
+        if (cnt[i] > 0.0) s.newDepth[i] = acc[i] / cnt[i];
+    }
+    for (int i = 0; i < nl; i++) {                  // link_setOutfallDepth for all links
+        int k;
+        double zz;
+        if (net.nodeType[net.node2[i]] == OUTFALL) { k = net.node2[i]; zz = net.offset2[i]; }
+        else if (net.nodeType[net.node1[i]] == OUTFALL) { k = net.node1[i]; zz = net.offset1[i]; }
+        else continue;
+        Geom g = geom(i);
+        double q = fabs(s.lNewFlow[i] / net.barrels[i]);
+        double yNorm = linkYnorm(g, q, net.qMax[i], net.beta[i], ct);
+        double yCrit = getYcrit(g, q, ct);
+        // outfall_setOutletDepth (node.c:1413-1492), FREE/NORMAL/FIXED/TSERIES
+        double stage, yNew;
+        int ot = net.outfallType[k];
+        if (ot == O_FREE) { s.newDepth[k] = (zz > 0.0) ? 0.0 : gmin(yNorm, yCrit); continue; }
+        if (ot == O_NORMAL) { s.newDepth[k] = (zz > 0.0) ? 0.0 : yNorm; continue; }
+        if (ot == O_FIXED) stage = net.fixedStage[k];
+        else stage = tseriesLookup(net.outfallSeries[k], opt.startDateTime + 0.0 / kMsecPerDay, true) / ucfLength();
+        yCrit = gmin(yCrit, yNorm);
+        if (yCrit + zz + net.invertElev[k] < stage) yNew = stage - net.invertElev[k];
+        else if (zz > 0.0) {
+            if (stage < net.invertElev[k] + zz) yNew = gmax(0.0, (stage - net.invertElev[k]));
+            else yNew = zz + yCrit;
+        } else yNew = yCrit;
+        s.newDepth[k] = yNew;
+    }
+    // initLinkDepths (flowrout.c:389-421)
+    for (int i = 0; i < nl; i++) {
+        if (net.q0[i] != 0.0) continue;
+        double y1 = s.newDepth[net.node1[i]] - net.offset1[i];
+        y1 = gmax(y1, 0.0);
+        y1 = gmin(y1, net.xsect[i].yFull);
+        double y2 = s.newDepth[net.node2[i]] - net.offset2[i];
+        y2 = gmax(y2, 0.0);
+        y2 = gmin(y2, net.xsect[i].yFull);
+        double y = 0.5 * (y1 + y2);
+        y = gmax(y, kFudge);
+        s.lNewDepth[i] = y;
+    }
+    // initNodes (flowrout.c:425-468)
+    for (int i = 0; i < nn; i++) {
+        s.inflow[i] = s.newLatFlow[i];
+        s.outflow[i] = 0.0;
+        if (opt.allowPonding && net.pondedArea[i] > 0.0 && s.newDepth[i] > net.fullDepth[i])
+            s.newVolume[i] = net.fullVolume[i] + (s.newDepth[i] - net.fullDepth[i]) * net.pondedArea[i];
+        else
+            s.newVolume[i] = (net.fullDepth[i] > 0.0) ? net.fullVolume[i] * (s.newDepth[i] / net.fullDepth[i]) : 0.0;
+    }
+    for (int i = 0; i < nl; i++) {
+        if (s.lNewFlow[i] >= 0.0) {
+            s.outflow[net.node1[i]] += s.lNewFlow[i];
+            s.inflow[net.node2[i]] += s.lNewFlow[i];
+        } else {
+            s.inflow[net.node1[i]] -= s.lNewFlow[i];
+            s.outflow[net.node2[i]] -= s.lNewFlow[i];
+        }
+    }
+    // initLinks (flowrout.c:472-507)
+    for (int i = 0; i < nl; i++) {
+        s.q1[i] = s.lNewFlow[i] / net.barrels[i];
+        s.q2[i] = s.q1[i];
+        s.a1[i] = getAofY(geom(i), s.lNewDepth[i], ct);
+        s.a2[i] = s.a1[i];
+        s.lNewVolume[i] = s.a1[i] * net.length[i] * net.barrels[i];
+        s.lOldVolume[i] = s.lNewVolume[i];
+    }
+    // qualrout_init (qualrout.c:63-96)
+    for (int p = 0; p < P; p++) {
+        double c0 = net.pollut[p].cInit;
+        for (int i = 0; i < nn; i++) {
+            double c = (s.newDepth[i] > 0.003281) ? c0 : 0.0;
+            s.nOldQual[p * nn + i] = c;
+            s.nNewQual[p * nn + i] = c;
+        }
+        for (int i = 0; i < nl; i++) {
+            double c = (s.lNewDepth[i] > 0.003281) ? c0 : 0.0;
+            s.lOldQual[p * nl + i] = c;
+            s.lNewQual[p * nl + i] = c;
+        }
+    }
+}
+
+// ================================================================= inflows
+double Project::getDateTime(double elapsedMsec) const
+{
+    return addSeconds(opt.startDateTime, (elapsedMsec + 1) / 1000.0);
+}
+
+double Project::patternFactor(int p, int month, int day, int hour) const  // inflow.c:456-484
+{
+    const Pattern& pt = net.patterns[p];
+    switch (pt.type) {
+    case PAT_MONTHLY: if (month >= 0 && month < 12) return pt.factor[month]; break;
+    case PAT_DAILY: if (day >= 0 && day < 7) return pt.factor[day]; break;
+    case PAT_HOURLY: if (hour >= 0 && hour < 24) return pt.factor[hour]; break;
+    case PAT_WEEKEND:
+        if (day == 0 || day == 6)
+            if (hour >= 0 && hour < 24) return pt.factor[hour];
+        break;
+    }
+    return 1.0;
+}
+
+// table.c:745-806 (in-memory series)
+double Project::tseriesLookup(int k, double x, bool extend)
+{
+    Tseries& t = net.tseries[k];
+    auto interp = [](double xx, double x1, double y1, double x2, double y2) {
+        double dx = x2 - x1;
+        if (fabs(dx) < 1.0e-20) return (y1 + y2) / 2.;
+        return y1 + (xx - x1) * (y2 - y1) / dx;
+    };
+    if (t.x1 <= x && t.x2 >= x && t.x1 != t.x2) return interp(x, t.x1, t.y1, t.x2, t.y2);
+    if (t.x1 == t.x2 || x < t.x1) {
+        t.cur = 0;
+        t.x1 = t.x.empty() ? 0.0 : t.x[0];
+        t.y1 = t.y.empty() ? 0.0 : t.y[0];
+        if (x < t.x1) return extend ? t.y1 : 0.0;
+    }
+    t.x1 = t.x2;
+    t.y1 = t.y2;
+    while (t.cur + 1 < t.x.size()) {
+        t.cur++;
+        t.x2 = t.x[t.cur];
+        t.y2 = t.y[t.cur];
+        if (x <= t.x2) return interp(x, t.x1, t.y1, t.x2, t.y2);
+        t.x1 = t.x2;
+        t.y1 = t.y2;
+    }
+    return extend ? t.y1 : 0.0;
+}
+
+bool Project::inflowsAreConstant() const
+{
+    if (!net.extInflows.empty()) return false;
+    for (auto& d : net.dwfInflows)
+        for (int i = 0; i < 4; i++)
+            if (d.patterns[i] >= 0) return false;
+    return true;
+}
+
+void Project::evalInflows(double currentDate, std::vector<double>& lat,
+                          std::vector<double>* qual, double* dwfTotal, double* extTotal,
+                          double* extOut)
+{
+    int nn = net.nNodes(), P = net.nPollut();
+    lat.assign(nn, 0.0);
+    if (qual) qual->assign((size_t)nn * P, 0.0);
+    double dwf = 0.0, ext = 0.0, eout = 0.0;
+    // addExternalInflows (routing.c:435-494): per node, FLOW first then pollutants
+    std::vector<int> extFirst(nn, -1);
+    std::vector<int> order(net.extInflows.size());
+    // the reference keeps each node's inflows in a prepended list: last read first
+    std::vector<std::vector<int>> byNode(nn);
+    for (int i = 0; i < (int)net.extInflows.size(); i++) byNode[net.extInflows[i].node].push_back(i);
+    int month = -1, day = -1, hour = -1;
+    auto extValue = [&](const ExtInflow& in) {   // inflow.c:207-230
+        double blv = in.baseline, tsv = 0.0;
+        if (in.basePat >= 0) {
+            if (month < 0) { month = monthOfYear(currentDate) - 1; day = dayOfWeek(currentDate) - 1; hour = hourOfDay(currentDate); }
+            blv *= patternFactor(in.basePat, month, day, hour);
+        }
+        if (in.tseries >= 0) tsv = tseriesLookup(in.tseries, currentDate, false) * in.sFactor;
+        return in.cFactor * (tsv + blv);
+    };
+    for (int j = 0; j < nn; j++) {
+        if (byNode[j].empty()) continue;
+        double q = 0.0;
+        for (int k = (int)byNode[j].size() - 1; k >= 0; k--) {
+            const ExtInflow& in = net.extInflows[byNode[j][k]];
+            if (in.type == EXT_FLOW) { q += extValue(in); break; }
+        }
+        if (fabs(q) < kFlowTol) q = 0.0;
+        lat[j] += q;
+        if (q >= 0.0) ext += q;
+        else { eout += -q; continue; }
+        if (net.nodeType[j] == OUTFALL && st.oldNetInflow[j] < 0.0) q = q - st.oldNetInflow[j];
+        if (qual)
+            for (int k = (int)byNode[j].size() - 1; k >= 0; k--) {
+                const ExtInflow& in = net.extInflows[byNode[j][k]];
+                if (in.type == EXT_FLOW) continue;
+                double w = extValue(in);
+                if (in.type == EXT_CONCEN) w *= q;
+                (*qual)[(size_t)in.param * nn + j] += w;
+            }
+    }
+    // addDryWeatherInflows (routing.c:498-575)
+    month = monthOfYear(currentDate) - 1;
+    day = dayOfWeek(currentDate) - 1;
+    hour = hourOfDay(currentDate);
+    std::vector<std::vector<int>> dwfByNode(nn);
+    for (int i = 0; i < (int)net.dwfInflows.size(); i++) dwfByNode[net.dwfInflows[i].node].push_back(i);
+    auto dwfValue = [&](const DwfInflow& in) {   // inflow.c:361-390
+        double f = 1.0;
+        int p1 = in.patterns[PAT_MONTHLY];
+        if (p1 >= 0) f *= patternFactor(p1, month, day, hour);
+        p1 = in.patterns[PAT_DAILY];
+        if (p1 >= 0) f *= patternFactor(p1, month, day, hour);
+        p1 = in.patterns[PAT_HOURLY];
+        int p2 = in.patterns[PAT_WEEKEND];
+        if (p2 >= 0) {
+            if (day == 0 || day == 6) f *= patternFactor(p2, month, day, hour);
+            else if (p1 >= 0) f *= patternFactor(p1, month, day, hour);
+        } else if (p1 >= 0) f *= patternFactor(p1, month, day, hour);
+        return f * in.avgValue;
+    };
+    for (int j = 0; j < nn; j++) {
+        if (dwfByNode[j].empty()) continue;
+        double q = 0.0;
+        for (int k = (int)dwfByNode[j].size() - 1; k >= 0; k--) {
+            const DwfInflow& in = net.dwfInflows[dwfByNode[j][k]];
+            if (in.param < 0) { q = dwfValue(in); break; }
+        }
+        if (fabs(q) < kFlowTol) q = 0.0;
+        lat[j] += q;
+        dwf += q;
+        if (q <= 0.0 || !qual) continue;
+        for (int p = 0; p < P; p++)
+            if (net.pollut[p].cDWF > 0.0) (*qual)[(size_t)p * nn + j] += q * net.pollut[p].cDWF;
+        for (int k = (int)dwfByNode[j].size() - 1; k >= 0; k--) {
+            const DwfInflow& in = net.dwfInflows[dwfByNode[j][k]];
+            if (in.param < 0) continue;
+            int p = in.param;
+            (*qual)[(size_t)p * nn + j] += q * dwfValue(in);
+            if (net.pollut[p].cDWF > 0.0) (*qual)[(size_t)p * nn + j] -= q * net.pollut[p].cDWF;
+        }
+    }
+    if (dwfTotal) *dwfTotal = dwf;
+    if (extTotal) *extTotal = ext;
+    if (extOut) *extOut = eout;
+}
+
+}  // namespace swx

@@ -1,0 +1,86 @@
+// project.h -- host side of the engine: .inp reader, validation, initial
+// state, lateral inflows and per-run accounting.  No GPU code lives here;
+// the device side is router.h / dw_kernels.hip.
+#pragma once
+
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "model.h"
+
+namespace swx {
+
+// --- date/time (restates src/solver/datetime.c; DateTime = days since 12/30/1899)
+double encodeDate(int year, int month, int day);
+double encodeTime(int hour, int minute, int second);
+bool strToDate(const char* s, double* d);
+bool strToTime(const char* s, double* t);
+void decodeDate(double date, int* year, int* month, int* day);
+void decodeTime(double time, int* h, int* m, int* s);
+double addSeconds(double date, double seconds);
+int monthOfYear(double date);
+int dayOfWeek(double date);
+int hourOfDay(double date);
+
+struct StepInflow {           // host-evaluated lateral inflow for one step
+    std::vector<int> node;    // nodes whose external/patterned inflow differs from base
+    std::vector<double> q;    // lateral flow (cfs) for those nodes
+};
+
+class Project {
+public:
+    Options opt;
+    ReportFlags rpt;
+    Network net;
+    State st;
+    std::vector<int> rptNodes, rptLinks;   // explicit [REPORT] lists
+    int errorCode = 0;
+    std::string errorMsg;
+    int warnings = 0;
+
+    int open(const char* inpPath);          // swmm_open: read + validate
+    void initState();                       // swmm_start: project_init + routing init
+    double ucfLength() const;
+    double ucfFlow() const;
+    double ucfVolume() const;
+    double ucfRainfall() const;
+    double ucfEvapRate() const;
+
+    // Lateral inflow q for every node at currentDate (routing.c:435-575):
+    // lat[j] = ext + dwf, with the reference's FLOW_TOL clamps.  Pollutant
+    // mass loads w[p*N+j] likewise.  Also returns the step's DWF and external
+    // inflow totals (massbal_addInflowFlow) for mass balance.
+    void evalInflows(double currentDate, std::vector<double>& lat, std::vector<double>* qualLoad,
+                     double* dwfTotal, double* extTotal, double* extOutTotal);
+    bool inflowsAreConstant() const;        // no time series / patterns
+    double getDateTime(double elapsedMsec) const;  // swmm5.c:1543
+
+    int setError(int code, const std::string& msg);
+
+private:
+    std::unordered_map<long long, int> extKey_, dwfKey_;   // (node, param) -> inflow index
+    int readFile(const char* path);
+    int parseLine(int sect, std::vector<char*>& tok, int pass);
+    int readOption(const char* k, const char* v);
+    int readJunction(std::vector<char*>& tok);
+    int readOutfall(std::vector<char*>& tok);
+    int readConduit(std::vector<char*>& tok);
+    int readXsect(std::vector<char*>& tok);
+    int readLoss(std::vector<char*>& tok);
+    int readPollutant(std::vector<char*>& tok);
+    int readInflow(std::vector<char*>& tok);
+    int readDwf(std::vector<char*>& tok);
+    int readPattern(std::vector<char*>& tok);
+    int readTimeseries(std::vector<char*>& tok);
+    int readReport(std::vector<char*>& tok);
+    int readEvap(std::vector<char*>& tok);
+    void validate();
+    void validateConduit(int j);
+    double patternFactor(int p, int month, int day, int hour) const;
+    double tseriesLookup(int k, double x, bool extend);
+};
+
+bool setXsectParams(Xsect& x, int type, double p[4], double ucf);
+
+}  // namespace swx

@@ -1,0 +1,68 @@
+// router.h -- the HBM-resident dynamic-wave router (device side of the engine).
+//
+// Owns every device array (structure-of-arrays link/node state, the node->link
+// CSR that reproduces the reference's serial summation order, the LDS-staged
+// geometry tables) and one HIP stream.  A routing step is one replay of a
+// captured HIP graph: MaxTrials x {link momentum, node update} kernel pairs with
+// on-device early exit after convergence (no host round trip inside the Picard
+// loop), then the step-end accounting kernels.  See DESIGN.md.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "project.h"
+
+namespace swx {
+
+struct RouterTotals {            // system flow totals kept on the device (massbal.c)
+    double dwInflow, exInflow, flooding, outflow, evapLoss, seepLoss;  // volumes (ft3)
+    double initStorage;
+};
+
+class Router {
+public:
+    Router();
+    ~Router();
+    // Allocate + upload static network and initial state; build graph.
+    int init(Project& prj, int device);
+    // Enqueue one routing step.  The step length and the simulation clock
+    // live on the device (k_finalize computes the next dt exactly as
+    // dynwave_getRoutingStep + execRouting's clamp do), so a fixed-step run
+    // never synchronises.  latFlow/qualLoad: this step's lateral flows / mass
+    // loads (nullptr = the constant arrays evaluated at init); totals =
+    // {dwInflow, exInflow, exOutflow} rates of those inflows.
+    int step(const double* latFlow, const double* qualLoad, const double totals[3]);
+    // Read the device clock after the last enqueued step (synchronises):
+    // routing time (msec) and the step length used by that step.
+    int readClock(double* newRoutingTime, double* lastDt, double* nextDt);
+    // Change the routing duration (msec) used for the end-of-run clamp.
+    int setDuration(double msec);
+    // Copy device state into the host mirror (prj.st); synchronises.
+    int download(Project& prj);
+    // Upload the host mirror's dynamic state (after swmm_setValue edits).
+    int upload(Project& prj);
+    int sync();
+    // counters: total iterations, non-converging steps, iterations of last step
+    void counters(long long* totalIters, long long* nonConv, int* lastSteps);
+    void flowTotals(double out[8]);
+    // system flow rates of the last completed step {dw, ex, flooding, outflow, evap, seep}
+    void stepTotals(double out[6]);
+    void setTiming(bool on);
+    int kernelTimes(double* out, int n);
+    int kernelBytes(double* out, int n);
+    std::string deviceName() const { return devName_; }
+    bool ok() const { return ok_; }
+    int lastError() const { return err_; }
+    std::string lastErrorMsg() const { return errMsg_; }
+
+    struct Impl;
+private:
+    Impl* d_;
+    bool ok_ = false;
+    int err_ = 0;
+    std::string errMsg_, devName_;
+};
+
+}  // namespace swx

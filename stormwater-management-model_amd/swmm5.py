@@ -1,0 +1,246 @@
+"""Python host mirror of the SWMM 5.2 engine API over libswmm5_mi355x.so.
+
+A thin ctypes binding with the reference's entry-point names, argument meaning
+and error convention (src/solver/include/swmm5.h:129-151; integer error codes
+from src/solver/error.h, sticky once set).  It is what a pyswmm-style caller
+would bind; the parity tests drive the engine through it exactly the way the
+reference's own harnesses drive libswmm5.
+
+The library is built in-tree (``make -C stormwater-management-model_amd/csrc``
+or ``__graft_entry__.build()``); there is no pure-Python or CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libswmm5_mi355x.so")
+
+# swmm5.h enums (values are the reference's)
+GAGE, SUBCATCH, NODE, LINK, SYSTEM = 0, 1, 2, 3, 100
+JUNCTION, OUTFALL, STORAGE, DIVIDER = 0, 1, 2, 3
+CONDUIT, PUMP, ORIFICE, WEIR, OUTLET = 0, 1, 2, 3, 4
+NODE_TYPE, NODE_ELEV, NODE_MAXDEPTH, NODE_DEPTH, NODE_HEAD = 300, 301, 302, 303, 304
+NODE_VOLUME, NODE_LATFLOW, NODE_INFLOW, NODE_OVERFLOW, NODE_RPTFLAG = 305, 306, 307, 308, 309
+LINK_TYPE, LINK_NODE1, LINK_NODE2, LINK_LENGTH, LINK_SLOPE = 400, 401, 402, 403, 404
+LINK_FULLDEPTH, LINK_FULLFLOW, LINK_SETTING, LINK_TIMEOPEN, LINK_TIMECLOSED = 405, 406, 407, 408, 409
+LINK_FLOW, LINK_DEPTH, LINK_VELOCITY, LINK_TOPWIDTH, LINK_RPTFLAG = 410, 411, 412, 413, 414
+STARTDATE, CURRENTDATE, ELAPSEDTIME, ROUTESTEP, MAXROUTESTEP = 0, 1, 2, 3, 4
+REPORTSTEP, TOTALSTEPS, NOREPORT, FLOWUNITS = 5, 6, 7, 8
+
+_lib = None
+
+
+class EngineMissing(RuntimeError):
+    pass
+
+
+def load_library(path: str | None = None):
+    """Load the engine; raises EngineMissing (never falls back) if absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise EngineMissing(
+            "libswmm5_mi355x.so not built at %s -- run __graft_entry__.build()" % p)
+    L = ctypes.CDLL(p)
+    c_int, c_dbl, c_char_p = ctypes.c_int, ctypes.c_double, ctypes.c_char_p
+    P = ctypes.POINTER
+    sig = {
+        "swmm_run": (c_int, [c_char_p, c_char_p, c_char_p]),
+        "swmm_open": (c_int, [c_char_p, c_char_p, c_char_p]),
+        "swmm_start": (c_int, [c_int]),
+        "swmm_step": (c_int, [P(c_dbl)]),
+        "swmm_stride": (c_int, [c_int, P(c_dbl)]),
+        "swmm_end": (c_int, []),
+        "swmm_report": (c_int, []),
+        "swmm_close": (c_int, []),
+        "swmm_getMassBalErr": (c_int, [P(ctypes.c_float)] * 3),
+        "swmm_getVersion": (c_int, []),
+        "swmm_getError": (c_int, [ctypes.c_char_p, c_int]),
+        "swmm_getWarnings": (c_int, []),
+        "swmm_getCount": (c_int, [c_int]),
+        "swmm_getName": (None, [c_int, c_int, ctypes.c_char_p, c_int]),
+        "swmm_getIndex": (c_int, [c_int, c_char_p]),
+        "swmm_getValue": (c_dbl, [c_int, c_int]),
+        "swmm_setValue": (None, [c_int, c_int, c_dbl]),
+        "swmm_getSavedValue": (c_dbl, [c_int, c_int, c_int]),
+        "swmm_writeLine": (None, [c_char_p]),
+        "swmm_decodeDate": (None, [c_dbl] + [P(c_int)] * 7),
+        "swmmx_startHost": (c_int, []),
+        "swmmx_exportState": (c_int, [c_char_p]),
+        "swmmx_getArray": (ctypes.c_long, [c_char_p, P(c_dbl), ctypes.c_long]),
+        "swmmx_setArray": (ctypes.c_long, [c_char_p, P(c_dbl), ctypes.c_long]),
+        "swmmx_runSteps": (c_int, [c_int, P(c_dbl)]),
+        "swmmx_getCounters": (c_int, [P(ctypes.c_longlong), c_int]),
+        "swmmx_setTiming": (c_int, [c_int]),
+        "swmmx_getKernelTimes": (c_int, [P(c_dbl), c_int]),
+        "swmmx_getKernelBytes": (c_int, [P(c_dbl), c_int]),
+        "swmmx_getBackend": (c_int, [ctypes.c_char_p, c_int]),
+        "swmmx_setDevice": (c_int, [c_int]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = L
+    return L
+
+
+def exported_symbols() -> list:
+    """Names the C ABI must export (include/swmm5.h + include/swmm5_mi355x.h)."""
+    names = []
+    root = os.path.dirname(PKG_DIR)
+    for h in ("swmm5.h", "swmm5_mi355x.h"):
+        with open(os.path.join(root, "include", h)) as f:
+            for line in f:
+                line = line.strip()
+                if "DLLEXPORT" in line and "(" in line and not line.startswith("#"):
+                    head = line.split("(")[0].split()
+                    names.append(head[-1].lstrip("*"))
+    return names
+
+
+class SWMM:
+    """One engine instance (the engine is single-project per process, as the
+    reference).  Methods return the reference's integer error codes."""
+
+    def __init__(self, lib_path: str | None = None):
+        self.L = load_library(lib_path)
+
+    @staticmethod
+    def _b(s):
+        return s.encode() if isinstance(s, str) else s
+
+    # --- lifecycle (swmm5.c:186-702)
+    def run(self, inp, rpt, out):
+        return self.L.swmm_run(self._b(inp), self._b(rpt), self._b(out))
+
+    def open(self, inp, rpt, out):
+        return self.L.swmm_open(self._b(inp), self._b(rpt), self._b(out))
+
+    def start(self, save_results: bool = True):
+        return self.L.swmm_start(1 if save_results else 0)
+
+    def step(self):
+        t = ctypes.c_double(0.0)
+        err = self.L.swmm_step(ctypes.byref(t))
+        return err, t.value
+
+    def stride(self, seconds: int):
+        t = ctypes.c_double(0.0)
+        err = self.L.swmm_stride(int(seconds), ctypes.byref(t))
+        return err, t.value
+
+    def end(self):
+        return self.L.swmm_end()
+
+    def report(self):
+        return self.L.swmm_report()
+
+    def close(self):
+        return self.L.swmm_close()
+
+    # --- diagnostics
+    def getMassBalErr(self):
+        a, b, c = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+        self.L.swmm_getMassBalErr(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return a.value, b.value, c.value
+
+    def getVersion(self):
+        return self.L.swmm_getVersion()
+
+    def getError(self):
+        buf = ctypes.create_string_buffer(512)
+        code = self.L.swmm_getError(buf, 512)
+        return code, buf.value.decode(errors="replace")
+
+    def getWarnings(self):
+        return self.L.swmm_getWarnings()
+
+    def getCount(self, obj):
+        return self.L.swmm_getCount(obj)
+
+    def getName(self, obj, idx):
+        buf = ctypes.create_string_buffer(256)
+        self.L.swmm_getName(obj, idx, buf, 256)
+        return buf.value.decode()
+
+    def getIndex(self, obj, name):
+        return self.L.swmm_getIndex(obj, self._b(name))
+
+    def getValue(self, prop, idx=0):
+        return self.L.swmm_getValue(prop, idx)
+
+    def setValue(self, prop, idx, value):
+        self.L.swmm_setValue(prop, idx, float(value))
+
+    def getSavedValue(self, prop, idx, period):
+        return self.L.swmm_getSavedValue(prop, idx, period)
+
+    def writeLine(self, line):
+        self.L.swmm_writeLine(self._b(line))
+
+    def decodeDate(self, date):
+        v = [ctypes.c_int() for _ in range(7)]
+        self.L.swmm_decodeDate(float(date), *[ctypes.byref(x) for x in v])
+        return tuple(x.value for x in v)
+
+    # --- extensions (include/swmm5_mi355x.h)
+    def start_host(self):
+        return self.L.swmmx_startHost()
+
+    def export_state(self, path):
+        return self.L.swmmx_exportState(self._b(path))
+
+    def get_array(self, name) -> np.ndarray:
+        n = self.L.swmmx_getArray(self._b(name), None, 0)
+        if n < 0:
+            raise KeyError(name)
+        a = np.empty(max(n, 1), dtype=np.float64)
+        self.L.swmmx_getArray(self._b(name), a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n)
+        return a[:n]
+
+    def set_array(self, name, values):
+        a = np.ascontiguousarray(values, dtype=np.float64)
+        return self.L.swmmx_setArray(self._b(name),
+                                     a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), a.size)
+
+    def run_steps(self, n):
+        t = ctypes.c_double(0.0)
+        err = self.L.swmmx_runSteps(int(n), ctypes.byref(t))
+        return err, t.value
+
+    def counters(self):
+        a = (ctypes.c_longlong * 6)()
+        self.L.swmmx_getCounters(a, 6)
+        keys = ["steps", "iterations", "nonconverged", "last_iterations", "conduits", "nodes"]
+        return dict(zip(keys, list(a)))
+
+    def set_timing(self, on: bool):
+        return self.L.swmmx_setTiming(1 if on else 0)
+
+    def kernel_times(self):
+        a = (ctypes.c_double * 8)()
+        n = self.L.swmmx_getKernelTimes(a, 8)
+        names = ["link_momentum", "node_update", "step_end", "quality"]
+        return {names[k]: (a[2 * k], a[2 * k + 1]) for k in range(n)}
+
+    def kernel_bytes(self):
+        a = (ctypes.c_double * 4)()
+        n = self.L.swmmx_getKernelBytes(a, 4)
+        names = ["link_momentum", "node_update", "step_end", "quality"]
+        return {names[k]: a[k] for k in range(n)}
+
+    def backend(self):
+        buf = ctypes.create_string_buffer(256)
+        self.L.swmmx_getBackend(buf, 256)
+        return buf.value.decode()
+
+    def set_device(self, ordinal: int):
+        return self.L.swmmx_setDevice(int(ordinal))

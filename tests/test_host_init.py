@@ -1,0 +1,128 @@
+"""CPU tests of the engine's host side (no GPU): the C ABI loads and exports
+every declared symbol, .inp reading + validation + initial state are
+bit-identical to the reference's, and errors fail loudly with the
+reference's codes."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import _golden
+import swmm5
+
+STATIC_SKIP = {"link.q2"}   # the engine keeps one per-barrel flow (q2 == q1 under DW)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return swmm5.load_library()
+
+
+def test_abi_exports_every_declared_symbol(lib):
+    names = swmm5.exported_symbols()
+    assert "swmm_open" in names and "swmm_getSavedValue" in names and "swmmx_startHost" in names
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_version(lib):
+    assert swmm5.SWMM().getVersion() == 52004
+
+
+def _engine_name(k):
+    xs = ("yFull", "wMax", "ywMax", "aFull", "rFull", "sFull", "sMax", "yBot", "aBot", "sBot",
+          "rBot", "culvertCode")
+    if k.startswith("link.") and k[5:] in xs:
+        return "link.x" + k[5:]
+    return k
+
+
+@pytest.mark.parametrize("name", _golden.CASES)
+def test_open_and_initial_state_bit_identical(name, tmp_path):
+    d = _golden.load(name)
+    s = swmm5.SWMM()
+    assert s.open(_golden.inp(name), str(tmp_path / "r.rpt"), str(tmp_path / "r.out")) == 0, s.getError()
+    assert s.start_host() == 0
+    try:
+        checked = 0
+        for k, v in d.items():
+            if not (k.startswith("node.") or k.startswith("link.")) or k in STATIC_SKIP:
+                continue
+            a = s.get_array(_engine_name(k))
+            np.testing.assert_array_equal(a, v.astype(np.float64), err_msg=k)
+            checked += 1
+        assert checked > 60
+        o = s.get_array("opt")
+        np.testing.assert_array_equal(o[:11], d["opt.d"][:11])
+        assert int(o[11]) == d["opt.i"][0] and int(o[12]) == d["opt.i"][1]
+        assert int(o[13]) == d["opt.i"][2] and int(o[14]) == d["opt.i"][3]
+        assert s.getCount(swmm5.NODE) == d["counts"][0]
+        assert s.getCount(swmm5.LINK) == d["counts"][1]
+    finally:
+        s.close()
+
+
+def test_object_access(tmp_path):
+    s = swmm5.SWMM()
+    assert s.open(_golden.inp("example"), str(tmp_path / "a.rpt"), str(tmp_path / "a.out")) == 0
+    j = s.getIndex(swmm5.NODE, "N7")
+    assert j >= 0 and s.getName(swmm5.NODE, j) == "N7"
+    assert s.getValue(swmm5.NODE_ELEV, j) == 114.0
+    k = s.getIndex(swmm5.LINK, "C8")
+    assert s.getValue(swmm5.LINK_FULLDEPTH, k) == 3.0
+    assert s.getIndex(swmm5.NODE, "nope") == -1
+    s.close()
+
+
+def test_identical_file_names_rejected(tmp_path):
+    s = swmm5.SWMM()
+    p = str(tmp_path / "x.inp")
+    assert s.open(p, p, str(tmp_path / "x.out")) == 301
+    s.close()
+
+
+def test_missing_input_file(tmp_path):
+    s = swmm5.SWMM()
+    assert s.open(str(tmp_path / "none.inp"), str(tmp_path / "a.rpt"), str(tmp_path / "a.out")) == 303
+    s.close()
+
+
+@pytest.mark.parametrize("section", ["[SUBCATCHMENTS]\nS1 RG1 N1 1 25 500 0.5 0\n",
+                                     "[STORAGE]\nST1 100 10 0 FUNCTIONAL 1000 0 0\n",
+                                     "[PUMPS]\nP1 N1 N2 * ON 0 0\n"])
+def test_unsupported_sections_fail_loudly(section, tmp_path):
+    src = open(_golden.inp("example")).read()
+    p = tmp_path / "u.inp"
+    p.write_text(src.replace("[JUNCTIONS]", section + "\n[JUNCTIONS]"))
+    s = swmm5.SWMM()
+    err = s.open(str(p), str(tmp_path / "u.rpt"), str(tmp_path / "u.out"))
+    assert err == 200
+    assert "not supported" in s.getError()[1]
+    s.close()
+
+
+def test_step_without_gpu_start_is_an_error(tmp_path):
+    s = swmm5.SWMM()
+    assert s.open(_golden.inp("grid12"), str(tmp_path / "a.rpt"), str(tmp_path / "a.out")) == 0
+    assert s.start_host() == 0
+    err, t = s.step()
+    assert err == 502 and t == 0.0
+    s.close()
+
+
+def test_xsect_tables_match_reference():
+    """The circular geometry tables (model data) equal the reference's."""
+    ref = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "oracle", "_ref", "libswmm5_ref.so")
+    if not os.path.exists(ref):
+        pytest.skip("reference build not present")
+    L = ctypes.CDLL(ref)
+    import re
+    hdr = open(os.path.join(swmm5.PKG_DIR, "csrc", "xsect_tables.h")).read()
+    body = hdr[hdr.index("= {") + 3:hdr.rindex("};")]
+    rows = re.findall(r"\{([^}]*)\}", body)
+    mine = [np.array([float(x) for x in r.replace("\n", " ").split(",") if x.strip()]) for r in rows]
+    for name, row in zip(["A_Circ", "R_Circ", "Y_Circ", "S_Circ", "W_Circ"], mine):
+        arr = (ctypes.c_double * 51).in_dll(L, name)
+        np.testing.assert_array_equal(row, np.array(arr[:]), err_msg=name)
