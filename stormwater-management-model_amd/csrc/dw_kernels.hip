@@ -48,7 +48,8 @@ namespace swx {
 
 constexpr int kBlock = 256;
 constexpr int kMaxTrialsCap = 32;
-constexpr int kNumPartials = 8;   // per-block partial sums written by k_step_end
+constexpr int kNumPartials = 8;
+constexpr int kLinkWavesDefault = 1;   // per-block partial sums written by k_step_end
 
 // ---- packed per-link flags -------------------------------------------------
 enum : uint32_t {
@@ -63,6 +64,7 @@ enum : uint32_t {
     LF_SEEP = 1u << 19,           // seepage > 0 or evaporation active
     LF_QLIMIT = 1u << 20,
     LF_DIRNEG = 1u << 21,
+    LF_COLD = 1u << 22,           // offset or outfall end: may need normal/critical depth
 };
 // ---- packed per-node flags -------------------------------------------------
 enum : uint32_t {
@@ -130,6 +132,8 @@ struct Params {
     const double* gTables;        // global copy of the 5x51 circular tables
     double* partials;             // [nBlocksEnd][kNumPartials]
     int nBlocksEnd;
+    int nCold;
+    const int* coldLinks;         // LF_COLD conduits, ascending
     StepCtl* ctl;
 };
 
@@ -222,26 +226,35 @@ __device__ double conduitLossRate(const Params& p, int j, const Geom& x, double 
     return totalLossRate;
 }
 
-// dwflow.c:297-413
-__device__ int flowClassOf(const Params& p, int j, const Geom& x, uint32_t f, int n1, int n2,
-                           double q, double h1, double h2, double y1, double y2, double* yC,
-                           double* yN, double* fasnh, const double* ct)
+// dwflow.c:297-413.  kCold = false is the specialisation for links with both
+// offsets zero and no outfall end (LF_COLD clear): z1 = z2 = 0, so the branches
+// that need normal / critical depth (root finders) are unreachable and are not
+// compiled into the streaming kernel.
+template <bool kCold>
+__device__ __forceinline__ int flowClassOf(const Params& p, int j, const Geom& x, uint32_t f,
+                                           int n1, int n2, double q, double h1, double h2,
+                                           double y1, double y2, double* yC, double* yN,
+                                           double* fasnh, const double* ct)
 {
-    double z1 = p.off1[j], z2 = p.off2[j];
-    if (f & LF_N1_OUTFALL) z1 = gmax(0.0, (z1 - p.nNewDepth[n1]));
-    if (f & LF_N2_OUTFALL) z2 = gmax(0.0, (z2 - p.nNewDepth[n2]));
+    double z1 = 0.0, z2 = 0.0;
+    if (kCold) {
+        z1 = p.off1[j];
+        z2 = p.off2[j];
+        if (f & LF_N1_OUTFALL) z1 = gmax(0.0, (z1 - p.nNewDepth[n1]));
+        if (f & LF_N2_OUTFALL) z2 = gmax(0.0, (z2 - p.nNewDepth[n2]));
+    }
     int fc = F_SUBCRIT;
     *fasnh = 1.0;
     if (y1 > 0.0001 && y2 > 0.0001) {
         if (q < 0.0) {
-            if (z1 > 0.0) {
+            if (kCold && z1 > 0.0) {
                 *yN = linkYnorm(x, fabs(q), p.qMax[j], p.beta[j], ct);
                 *yC = getYcrit(x, fabs(q), ct);
                 double ycMin = gmin(*yN, *yC);
                 if (y1 < ycMin) fc = F_UP_CRIT;
             }
         } else {
-            if (z2 > 0.0) {
+            if (kCold && z2 > 0.0) {
                 *yN = linkYnorm(x, fabs(q), p.qMax[j], p.beta[j], ct);
                 *yC = getYcrit(x, fabs(q), ct);
                 double ycMin = gmin(*yN, *yC);
@@ -256,15 +269,15 @@ __device__ int flowClassOf(const Params& p, int j, const Geom& x, uint32_t f, in
     } else if (y1 <= 0.0001 && y2 <= 0.0001) {
         fc = F_DRY;
     } else if (y2 > 0.0001) {
-        if (h2 < p.inv1[j] + p.off1[j]) fc = F_UP_DRY;
-        else if (z1 > 0.0) {
+        if (h2 < p.inv1[j] + (kCold ? p.off1[j] : 0.0)) fc = F_UP_DRY;
+        else if (kCold && z1 > 0.0) {
             *yN = linkYnorm(x, fabs(q), p.qMax[j], p.beta[j], ct);
             *yC = getYcrit(x, fabs(q), ct);
             fc = F_UP_CRIT;
         }
     } else {
-        if (h1 < p.inv2[j] + p.off2[j]) fc = F_DN_DRY;
-        else if (z2 > 0.0) {
+        if (h1 < p.inv2[j] + (kCold ? p.off2[j] : 0.0)) fc = F_DN_DRY;
+        else if (kCold && z2 > 0.0) {
             *yN = linkYnorm(x, fabs(q), p.qMax[j], p.beta[j], ct);
             *yC = getYcrit(x, fabs(q), ct);
             fc = F_DN_CRIT;
@@ -274,13 +287,14 @@ __device__ int flowClassOf(const Params& p, int j, const Geom& x, uint32_t f, in
 }
 
 // dwflow.c:57-293 -- one conduit, one Picard iteration.
-template <bool kFirst>
-__device__ void conduitFlow(const Params& p, int j, int steps, double dt, const double* ct)
+template <bool kFirst, bool kCold>
+__device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, int2 nn, int steps,
+                                            double dt, const double* ct)
 {
     const double omega = 0.5;
-    uint32_t f = p.lflags[j];
-    int2 nn = p.lnodes[j];
     int n1 = nn.x, n2 = nn.y;
+    const double off1 = kCold ? p.off1[j] : 0.0;     // hot links: both offsets are 0
+    const double off2 = kCold ? p.off2[j] : 0.0;
     Geom x = loadGeom(p, j, f);
     double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
 
@@ -304,8 +318,8 @@ __device__ void conduitFlow(const Params& p, int j, int steps, double dt, const 
     double evapRate = 0.0, seepRate = 0.0;
 
     double inv1 = p.inv1[j], inv2 = p.inv2[j];
-    double z1 = inv1 + p.off1[j];
-    double z2 = inv2 + p.off2[j];
+    double z1 = inv1 + off1;
+    double z2 = inv2 + off2;
     double h1 = p.nNewDepth[n1] + inv1;
     double h2 = p.nNewDepth[n2] + inv2;
     h1 = gmax(h1, z1);
@@ -330,63 +344,57 @@ __device__ void conduitFlow(const Params& p, int j, int steps, double dt, const 
         double yNorm = (d1 + d2) / 2.0;
         double yCrit = yNorm;
         if (d1 >= x.yFull && d2 >= x.yFull) fc = F_SUBCRIT;
-        else fc = flowClassOf(p, j, x, f, n1, n2, qLast, h1, h2, y1, y2, &yCrit, &yNorm, &fasnh, ct);
+        else fc = flowClassOf<kCold>(p, j, x, f, n1, n2, qLast, h1, h2, y1, y2, &yCrit, &yNorm, &fasnh, ct);
+        // Every wet class evaluates the top width at (d1, d2, dMid) after
+        // adjusting one end; the widths are computed once, outside the switch,
+        // so the geometry code is instantiated three times instead of fifteen.
+        // (Widths a class does not use are pure and discarded.)
         switch (fc) {
-        case F_SUBCRIT:
-            dMid = 0.5 * (d1 + d2);
-            if (dMid < 0.0001) dMid = 0.0001;
-            w1 = widthAt(p, x, d1, ct);
-            w2 = widthAt(p, x, d2, ct);
-            wMid = widthAt(p, x, dMid, ct);
-            sa1 = (w1 + wMid) * length / 4.;
-            sa2 = (wMid + w2) * length / 4. * fasnh;
-            break;
         case F_UP_CRIT:
             d1 = yCrit;
             if (yNorm < yCrit) d1 = yNorm;
             d1 = gmax(d1, 0.0001);
-            h1 = inv1 + p.off1[j] + d1;
-            dMid = 0.5 * (d1 + d2);
-            if (dMid < 0.0001) dMid = 0.0001;
-            w2 = widthAt(p, x, d2, ct);
-            wMid = widthAt(p, x, dMid, ct);
-            sa2 = (wMid + w2) * length * 0.5;
+            h1 = inv1 + off1 + d1;
             break;
         case F_DN_CRIT:
             d2 = yCrit;
             if (yNorm < yCrit) d2 = yNorm;
             d2 = gmax(d2, 0.0001);
-            h2 = inv2 + p.off2[j] + d2;
-            w1 = widthAt(p, x, d1, ct);
-            dMid = 0.5 * (d1 + d2);
-            if (dMid < 0.0001) dMid = 0.0001;
-            wMid = widthAt(p, x, dMid, ct);
-            sa1 = (w1 + wMid) * length * 0.5;
+            h2 = inv2 + off2 + d2;
             break;
-        case F_UP_DRY:
-            d1 = 0.0001;
-            dMid = 0.5 * (d1 + d2);
-            if (dMid < 0.0001) dMid = 0.0001;
-            w1 = widthAt(p, x, d1, ct);
-            w2 = widthAt(p, x, d2, ct);
-            wMid = widthAt(p, x, dMid, ct);
-            sa2 = (wMid + w2) * length / 4.;
-            if (p.off1[j] <= 0.0) sa1 = (w1 + wMid) * length / 4.;
-            break;
-        case F_DN_DRY:
-            d2 = 0.0001;
-            dMid = 0.5 * (d1 + d2);
-            if (dMid < 0.0001) dMid = 0.0001;
-            w1 = widthAt(p, x, d1, ct);
-            w2 = widthAt(p, x, d2, ct);
-            wMid = widthAt(p, x, dMid, ct);
-            sa1 = (wMid + w1) * length / 4.;
-            if (p.off2[j] <= 0.0) sa2 = (w2 + wMid) * length / 4.;
-            break;
-        default:  // F_DRY
+        case F_UP_DRY: d1 = 0.0001; break;
+        case F_DN_DRY: d2 = 0.0001; break;
+        default: break;
+        }
+        if (fc == F_DRY) {
             sa1 = 0.0001 * length / 2.0;
             sa2 = sa1;
-            break;
+        } else {
+            dMid = 0.5 * (d1 + d2);
+            if (dMid < 0.0001) dMid = 0.0001;
+            w1 = widthAt(p, x, d1, ct);
+            w2 = widthAt(p, x, d2, ct);
+            wMid = widthAt(p, x, dMid, ct);
+            switch (fc) {
+            case F_SUBCRIT:                                  // dwflow.c:460-472
+                sa1 = (w1 + wMid) * length / 4.;
+                sa2 = (wMid + w2) * length / 4. * fasnh;
+                break;
+            case F_UP_CRIT:                                  // dwflow.c:474-488
+                sa2 = (wMid + w2) * length * 0.5;
+                break;
+            case F_DN_CRIT:                                  // dwflow.c:490-504
+                sa1 = (w1 + wMid) * length * 0.5;
+                break;
+            case F_UP_DRY:                                   // dwflow.c:506-519
+                sa2 = (wMid + w2) * length / 4.;
+                if (off1 <= 0.0) sa1 = (w1 + wMid) * length / 4.;
+                break;
+            default:                                         // F_DN_DRY dwflow.c:521-534
+                sa1 = (wMid + w1) * length / 4.;
+                if (off2 <= 0.0) sa2 = (w2 + wMid) * length / 4.;
+                break;
+            }
         }
         y1 = d1;
         y2 = d2;
@@ -542,27 +550,31 @@ __device__ __forceinline__ void stageTables(double* ct, const double* g)
     __syncthreads();
 }
 
-template <bool kFirst>
-__global__ __launch_bounds__(kBlock) void k_link(Params p, int k)
+// Streaming kernel: every conduit with LF_COLD clear (zero offsets, no outfall
+// end), one thread per conduit.  No calls, no root finders.
+// kWaves: minimum waves per SIMD the register allocator must allow (1 = no
+// constraint); selected at start-up (SWMM5_LINK_WAVES, default kLinkWavesDefault)
+template <bool kFirst, int kWaves>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves)))
+void k_link(Params p, int k)
 {
     if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;     // converged: dynwave.c:249-251
     __shared__ double ct[5 * SWX_CIRC_N];
     stageTables(ct, p.gTables);
     double dt = p.ctl->dt;
     for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nL; j += gridDim.x * kBlock) {
-        if (k >= 2) {                                      // findBypassedLinks dynwave.c:335-345
-            int2 nn = p.lnodes[j];
-            if (p.conv[nn.x] && p.conv[nn.y]) continue;
-        }
-        conduitFlow<kFirst>(p, j, k, dt, ct);
+        uint32_t f = p.lflags[j];
+        if (f & LF_COLD) continue;
+        int2 nn = p.lnodes[j];
+        if (k >= 2 && p.conv[nn.x] && p.conv[nn.y]) continue;   // findBypassedLinks dynwave.c:335-345
+        conduitFlow<kFirst, false>(p, j, f, nn, k, dt, ct);
     }
 }
 
 // link_setOutfallDepth + outfall_setOutletDepth (link.c:728-766, node.c:1413-1492)
-__device__ double outfallDepth(const Params& p, int i, uint32_t nf, int j)
+__device__ __forceinline__ double outfallDepth(const Params& p, int i, uint32_t nf, int j,
+                                               uint32_t f, const double* ct)
 {
-    const double* ct = p.gTables;
-    uint32_t f = p.lflags[j];
     Geom x = loadGeom(p, j, f);
     double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
     int2 nn = p.lnodes[j];
@@ -583,6 +595,31 @@ __device__ double outfallDepth(const Params& p, int i, uint32_t nf, int j)
         else yNew = z + yCrit;
     } else yNew = yCrit;
     return yNew;
+}
+
+
+// The few conduits with an invert offset or an outfall end (compacted list):
+// full flow classification with normal / critical depth, then, for an outfall
+// end, link_setOutfallDepth (findNodeDepths, dynwave.c:605).  The outfall's
+// only reader in the next iteration is this same link, and the outfall is
+// never "converged", so the link is never bypassed (dynwave.c:281, 340).
+template <bool kFirst>
+__global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
+{
+    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
+    __shared__ double ct[5 * SWX_CIRC_N];
+    stageTables(ct, p.gTables);
+    double dt = p.ctl->dt;
+    for (int c = blockIdx.x * kBlock + threadIdx.x; c < p.nCold; c += gridDim.x * kBlock) {
+        int j = p.coldLinks[c];
+        uint32_t f = p.lflags[j];
+        int2 nn = p.lnodes[j];
+        if (!(k >= 2 && p.conv[nn.x] && p.conv[nn.y])) conduitFlow<kFirst, true>(p, j, f, nn, k, dt, ct);
+        if (f & (LF_N1_OUTFALL | LF_N2_OUTFALL)) {
+            int i = (f & LF_N2_OUTFALL) ? nn.y : nn.x;     // link.c:743-753 (node2 first)
+            p.nNewDepth[i] = outfallDepth(p, i, p.nflags[i], j, f, ct);
+        }
+    }
 }
 
 template <bool kFirst>
@@ -649,11 +686,7 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
         }
         p.inflow[i] = inflow;
         p.outflow[i] = outflow;
-        if (type == OUTFALL) {
-            int l = p.outfallLink[i];
-            if (l >= 0) p.nNewDepth[i] = outfallDepth(p, i, nf, l);
-            continue;
-        }
+        if (type == OUTFALL) continue;                     // depth set by k_link_cold
         // setNodeDepth (dynwave.c:636-762)
         bool isPonded = (canPond && yLast > fullDepth);
         double yCrown = p.yCrown[i];
@@ -981,7 +1014,8 @@ struct Router::Impl {
     hipGraphExec_t graph = nullptr;
     bool useGraph = true;
     bool timing = false;
-    int gridL = 1, gridN = 1, gridEnd = 1;
+    int gridL = 1, gridN = 1, gridEnd = 1, gridC = 1;
+    int linkWaves = kLinkWavesDefault;
     std::vector<void*> allocs;
     double* latBase = nullptr;       // constant lateral inflows
     double* qualBase = nullptr;
@@ -1008,12 +1042,12 @@ Router::Router() : d_(new Impl) {}
 Router::~Router()
 {
     if (d_) {
-        if (d_->graph) hipGraphExecDestroy(d_->graph);
-        for (auto e : d_->ev) hipEventDestroy(e);
-        for (void* a : d_->allocs) hipFree(a);
-        if (d_->hostPinned) hipHostFree(d_->hostPinned);
-        if (d_->hostCtl) hipHostFree(d_->hostCtl);
-        if (d_->stream) hipStreamDestroy(d_->stream);
+        if (d_->graph) (void)hipGraphExecDestroy(d_->graph);
+        for (auto e : d_->ev) (void)hipEventDestroy(e);
+        for (void* a : d_->allocs) (void)hipFree(a);
+        if (d_->hostPinned) (void)hipHostFree(d_->hostPinned);
+        if (d_->hostCtl) (void)hipHostFree(d_->hostCtl);
+        if (d_->stream) (void)hipStreamDestroy(d_->stream);
         delete d_;
     }
 }
@@ -1027,37 +1061,52 @@ static T* devAlloc(Router::Impl* d, size_t n, hipError_t* err)
     return (T*)ptr;
 }
 
+typedef void (*LinkKernelFn)(Params, int);
+static LinkKernelFn linkKernel(bool first, int waves)
+{
+    switch (waves) {
+    case 3: return first ? k_link<true, 3> : k_link<false, 3>;
+    case 4: return first ? k_link<true, 4> : k_link<false, 4>;
+    case 5: return first ? k_link<true, 5> : k_link<false, 5>;
+    default: return first ? k_link<true, 1> : k_link<false, 1>;
+    }
+}
+
 static void launchIteration(Router::Impl* d, int k)
 {
     Params& p = d->p;
     if (k == 0) {
-        hipLaunchKernelGGL(k_link<true>, dim3(d->gridL), dim3(kBlock), 0, d->stream, p, k);
+        hipLaunchKernelGGL(linkKernel(true, d->linkWaves), dim3(d->gridL), dim3(kBlock), 0, d->stream, p, k);
+        if (p.nCold)
+            hipLaunchKernelGGL(k_link_cold<true>, dim3(d->gridC), dim3(kBlock), 0, d->stream, p, k);
     } else {
-        hipLaunchKernelGGL(k_link<false>, dim3(d->gridL), dim3(kBlock), 0, d->stream, p, k);
+        hipLaunchKernelGGL(linkKernel(false, d->linkWaves), dim3(d->gridL), dim3(kBlock), 0, d->stream, p, k);
+        if (p.nCold)
+            hipLaunchKernelGGL(k_link_cold<false>, dim3(d->gridC), dim3(kBlock), 0, d->stream, p, k);
     }
-    if (d->timing) hipEventRecord(d->ev[2 * k + 1], d->stream);
+    if (d->timing) (void)hipEventRecord(d->ev[2 * k + 1], d->stream);
     if (k == 0) {
         hipLaunchKernelGGL(k_node<true>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
     } else {
         hipLaunchKernelGGL(k_node<false>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
     }
-    if (d->timing) hipEventRecord(d->ev[2 * k + 2], d->stream);
+    if (d->timing) (void)hipEventRecord(d->ev[2 * k + 2], d->stream);
 }
 
 static void launchStep(Router::Impl* d)
 {
     Params& p = d->p;
-    if (d->timing) hipEventRecord(d->ev[0], d->stream);
+    if (d->timing) (void)hipEventRecord(d->ev[0], d->stream);
     for (int k = 0; k < p.maxTrials; k++) launchIteration(d, k);
     int base = 2 * p.maxTrials + 1;
     if (p.P > 0) {
         hipLaunchKernelGGL(k_qual_node, dim3(d->gridN), dim3(kBlock), 0, d->stream, p);
         hipLaunchKernelGGL(k_qual_link, dim3(d->gridL), dim3(kBlock), 0, d->stream, p);
     }
-    if (d->timing) hipEventRecord(d->ev[base], d->stream);
+    if (d->timing) (void)hipEventRecord(d->ev[base], d->stream);
     hipLaunchKernelGGL(k_step_end, dim3(d->gridEnd), dim3(kBlock), 0, d->stream, p);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, d->stream, p);
-    if (d->timing) hipEventRecord(d->ev[base + 1], d->stream);
+    if (d->timing) (void)hipEventRecord(d->ev[base + 1], d->stream);
 }
 
 int Router::init(Project& prj, int device)
@@ -1111,7 +1160,7 @@ int Router::init(Project& prj, int device)
 
     // ---- link static ------------------------------------------------------
     std::vector<int> nodes2((size_t)nL * 2);
-    std::vector<int> lflags(nL);
+    std::vector<int> lflags(nL), coldLinks;
     std::vector<double> inv1(nL), inv2(nL), xd[11];
     for (auto& v : xd) v.resize(nL);
     for (int j = 0; j < nL; j++) {
@@ -1131,6 +1180,10 @@ int Router::init(Project& prj, int device)
         if (net.seepRate[j] > 0.0 || (prj.opt.evapRate > 0.0 && isOpen(x.type))) f |= LF_SEEP;
         if (net.qLimit[j] > 0.0) f |= LF_QLIMIT;
         if (net.direction[j] < 0) f |= LF_DIRNEG;
+        if (net.offset1[j] > 0.0 || net.offset2[j] > 0.0 || (f & (LF_N1_OUTFALL | LF_N2_OUTFALL))) {
+            f |= LF_COLD;
+            coldLinks.push_back(j);
+        }
         lflags[j] = (int)f;
         xd[0][j] = x.yFull; xd[1][j] = x.wMax; xd[2][j] = x.ywMax; xd[3][j] = x.aFull;
         xd[4][j] = x.rFull; xd[5][j] = x.sFull; xd[6][j] = x.sMax; xd[7][j] = x.yBot;
@@ -1143,6 +1196,10 @@ int Router::init(Project& prj, int device)
         int* fl;
         UPI(fl, lflags, nL);
         p.lflags = (const uint32_t*)fl;
+        int* cl;
+        UPI(cl, coldLinks, coldLinks.size());
+        p.coldLinks = cl;
+        p.nCold = (int)coldLinks.size();
     }
     double* tmp;
     UPD(tmp, inv1, nL); p.inv1 = tmp;
@@ -1292,9 +1349,11 @@ int Router::init(Project& prj, int device)
         std::vector<double> t(&SWX_CIRC_TABLES[0][0], &SWX_CIRC_TABLES[0][0] + 5 * SWX_CIRC_N);
         UPD(tmp, t, t.size()); p.gTables = tmp;
     }
+    if (const char* w = getenv("SWMM5_LINK_WAVES")) d->linkWaves = atoi(w);
     int maxBlocks = 8 * std::max(prop.multiProcessorCount, 1);
     d->gridL = std::max(1, std::min((nL + kBlock - 1) / kBlock, maxBlocks));
     d->gridN = std::max(1, std::min((nN + kBlock - 1) / kBlock, maxBlocks));
+    d->gridC = std::max(1, std::min((p.nCold + kBlock - 1) / kBlock, maxBlocks));
     d->gridEnd = std::max(1, std::min((std::max(nN, nL) + kBlock - 1) / kBlock, 2 * prop.multiProcessorCount));
     p.nBlocksEnd = d->gridEnd;
     p.partials = devAlloc<double>(d, (size_t)d->gridEnd * kNumPartials, &e);
@@ -1330,11 +1389,14 @@ int Router::init(Project& prj, int device)
     // algorithmic bytes per launch (DESIGN.md byte model; per kernel class)
     {
         double L = nL, N = nN, E = d->nE;
-        // link momentum: static 8 (nodes) + 4 (flags) + 4x8 (inv/off) + 7x8 (geom)
-        //   + 3x8 (lengths, roughFactor) ; dynamic reads newFlow/oldFlow, q1,
-        //   a1/a2, setting, lstate (8x5 + 4) ; 2 node depth gathers (16) ;
-        //   writes a1 q1 newDepth newVolume newFlow dqdh froude sa1 sa2 evap seep + lstate (11x8+4)
-        d->kbytes[0] = L * (8 + 4 + 32 + 56 + 24 + 44 + 16 + 92);
+        // link momentum, per conduit and Picard iteration >= 1:
+        //   static   nodes 8 + flags 4 + inv1/inv2 16 + geometry 7x8
+        //            + length/modLength/roughFactor/beta 32           = 116
+        //   dynamic  oldFlow, setting, q1, a2 4x8 + lstate 4          =  36
+        //   gathers  newDepth at both end nodes                       =  16
+        //   writes   a1 q1 newDepth newVolume newFlow dqdh froude
+        //            sa1 sa2 evap seep 11x8 + lstate 4                =  92
+        d->kbytes[0] = L * (116 + 36 + 16 + 92);
         // node update: per node static (flags, fullDepth, surDepth, yCrown,
         //   fullVolume, ponded: 4+5x8) + rowptr 4 + dynamic reads (newDepth,
         //   oldDepth, oldNetInflow, newLat, oldSurfArea: 40) + writes (inflow,
@@ -1352,7 +1414,7 @@ int Router::init(Project& prj, int device)
     launchStep(d);
     HIPCHECK(hipStreamEndCapture(d->stream, &g));
     HIPCHECK(hipGraphInstantiate(&d->graph, g, nullptr, nullptr, 0));
-    hipGraphDestroy(g);
+    (void)hipGraphDestroy(g);
     HIPCHECK(hipStreamSynchronize(d->stream));
     ok_ = true;
     return 0;
@@ -1394,15 +1456,15 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
         HIPCHECK(hipMemcpy(&ran, &d->ctl->lastSteps, sizeof(int), hipMemcpyDeviceToHost));
         for (int k = 0; k < ran; k++) {    // early-exited iterations are not counted
             float ms1 = 0, ms2 = 0;
-            hipEventElapsedTime(&ms1, d->ev[2 * k], d->ev[2 * k + 1]);
-            hipEventElapsedTime(&ms2, d->ev[2 * k + 1], d->ev[2 * k + 2]);
+            (void)hipEventElapsedTime(&ms1, d->ev[2 * k], d->ev[2 * k + 1]);
+            (void)hipEventElapsedTime(&ms2, d->ev[2 * k + 1], d->ev[2 * k + 2]);
             d->kms[0] += ms1; d->kcnt[0]++;
             d->kms[1] += ms2; d->kcnt[1]++;
         }
         int base = 2 * p.maxTrials + 1;
         float ms3 = 0, msq = 0;
-        hipEventElapsedTime(&ms3, d->ev[base], d->ev[base + 1]);
-        hipEventElapsedTime(&msq, d->ev[2 * p.maxTrials], d->ev[base]);
+        (void)hipEventElapsedTime(&ms3, d->ev[base], d->ev[base + 1]);
+        (void)hipEventElapsedTime(&msq, d->ev[2 * p.maxTrials], d->ev[base]);
         d->kms[2] += ms3; d->kcnt[2]++;
         if (p.P) { d->kms[3] += msq; d->kcnt[3]++; }
     } else {
@@ -1538,11 +1600,23 @@ int Router::upload(Project& prj)
     return 0;
 }
 
+// copy the device step clock/accounting block to its pinned host mirror;
+// a failure (e.g. a faulted kernel) is latched into the router's error state
+static void pullCtl(Router::Impl* d, int& err, std::string& msg)
+{
+    hipError_t e = hipMemcpyAsync(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost,
+                                  d->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
+    if (e != hipSuccess && !err) {
+        err = 500;
+        msg = std::string("ERROR 500: GPU router: ") + hipGetErrorString(e);
+    }
+}
+
 void Router::counters(long long* totalIters, long long* nonConv, int* lastSteps)
 {
     Impl* d = d_;
-    hipMemcpyAsync(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost, d->stream);
-    hipStreamSynchronize(d->stream);
+    pullCtl(d, err_, errMsg_);
     *totalIters = d->hostCtl->totalIters;
     *nonConv = d->hostCtl->nonConverge;
     *lastSteps = d->hostCtl->lastSteps;
@@ -1551,16 +1625,14 @@ void Router::counters(long long* totalIters, long long* nonConv, int* lastSteps)
 void Router::flowTotals(double out[8])
 {
     Impl* d = d_;
-    hipMemcpyAsync(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost, d->stream);
-    hipStreamSynchronize(d->stream);
+    pullCtl(d, err_, errMsg_);
     for (int q = 0; q < 8; q++) out[q] = d->hostCtl->flowTot[q];
 }
 
 void Router::stepTotals(double out[6])
 {
     Impl* d = d_;
-    hipMemcpyAsync(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost, d->stream);
-    hipStreamSynchronize(d->stream);
+    pullCtl(d, err_, errMsg_);
     for (int q = 0; q < 6; q++) out[q] = d->hostCtl->prevStepTot[q];
 }
 

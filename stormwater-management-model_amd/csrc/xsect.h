@@ -18,8 +18,12 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define SWX_HD __host__ __device__ __forceinline__
+// rarely taken iterative paths (root finders) stay out of line so they do not
+// inflate the register budget of the streaming kernels
+#define SWX_HD_COLD __host__ __device__ __attribute__((noinline)) inline
 #else
 #define SWX_HD inline
+#define SWX_HD_COLD inline
 #endif
 
 namespace swx {
@@ -106,13 +110,14 @@ SWX_HD double invLookup(double y, const double* t, int nItems)
 }
 
 // xsect.c:2573-2591 -- Newton solve of theta - sin(theta) = 2 pi alpha
-SWX_HD double thetaOfAlpha(double alpha)
+SWX_HD_COLD double thetaOfAlpha(double alpha)
 {
     double theta;
     if (alpha > 0.04) theta = 1.2 + 5.08 * (alpha - 0.04) / 0.96;
     else theta = 0.031715 - 12.79384 * alpha + 8.28479 * sqrt(alpha);
     double theta1 = theta;
     double ap = (2.0 * 3.141592654) * alpha;
+    #pragma unroll 1
     for (int k = 1; k <= 40; k++) {
         double d = -(ap - theta + sin(theta)) / (1.0 - cos(theta));
         if (d > 1.0) d = (d >= 0.0 ? fabs(1.0) : -fabs(1.0));
@@ -123,7 +128,7 @@ SWX_HD double thetaOfAlpha(double alpha)
 }
 
 // xsect.c:2593-2618
-SWX_HD double thetaOfPsi(double psi)
+SWX_HD_COLD double thetaOfPsi(double psi)
 {
     double theta;
     if (psi > 0.90) theta = 4.17 + 1.12 * (psi - 0.90) / 0.176;
@@ -132,6 +137,7 @@ SWX_HD double thetaOfPsi(double psi)
     else theta = 0.12103 - 55.5075 * psi + 15.62254 * sqrt(psi);
     double theta1 = theta;
     double ap = (2.0 * 3.141592654) * psi;
+    #pragma unroll 1
     for (int k = 1; k <= 40; k++) {
         theta = fabs(theta);
         double tt = theta - sin(theta);
@@ -230,7 +236,7 @@ SWX_HD double getWofY(const Geom& x, double y, const double* ct)
     }
 }
 
-SWX_HD double getSofA(const Geom& x, double a, const double* ct);
+SWX_HD_COLD double getSofA(const Geom& x, double a, const double* ct);
 
 // xsect.c:1100-1145
 SWX_HD double getRofA(const Geom& x, double a, const double* ct)
@@ -259,7 +265,15 @@ SWX_HD double getRofY(const Geom& x, double y, const double* ct)
         if (y == 0.0) return 0.0;
         return ((x.yBot + x.sBot * y) * y) / (x.yBot + y * x.rBot);
     case G_TRIANGULAR: return (y * x.sBot) / (2. * x.rBot);
-    default: return getRofA(x, getAofY(x, y, ct), ct);
+    // xsect.c:1091 default branch R(A(y)); written out for the two table-free
+    // shapes that reach it so the kernels' hydraulic-radius path has no call
+    case G_RECT_CLOSED: return rectClosedRofA(x, getAofY(x, y, ct));
+    case G_RECT_OPEN: {
+        double a = getAofY(x, y, ct);
+        if (a <= 0.0) return 0.0;
+        return a / (x.wMax + (2. - x.sBot) * a / x.wMax);
+    }
+    default: return 0.0;     // no other shape is accepted by the reader
     }
 }
 
@@ -280,7 +294,7 @@ SWX_HD double getYofA(const Geom& x, double a, const double* ct)
 }
 
 // xsect.c:714-769 (+1755-1768, 1810-1815, 2391-2401)
-SWX_HD double getSofA(const Geom& x, double a, const double* ct)
+SWX_HD_COLD double getSofA(const Geom& x, double a, const double* ct)
 {
     double alpha = a / x.aFull;
     switch (x.type) {
@@ -306,7 +320,7 @@ SWX_HD double getSofA(const Geom& x, double a, const double* ct)
 }
 
 // xsect.c:1453-1470
-SWX_HD double genericdSdA(const Geom& x, double a, const double* ct)
+SWX_HD_COLD double genericdSdA(const Geom& x, double a, const double* ct)
 {
     double alpha = a / x.aFull, alpha1 = alpha - 0.001, alpha2 = alpha + 0.001;
     if (alpha1 < 0.0) alpha1 = 0.0;
@@ -316,7 +330,7 @@ SWX_HD double genericdSdA(const Geom& x, double a, const double* ct)
 }
 
 // xsect.c:1194-1253 with the shape-specific derivatives
-SWX_HD double getdSdA(const Geom& x, double a, const double* ct)
+SWX_HD_COLD double getdSdA(const Geom& x, double a, const double* ct)
 {
     double alpha, r, dPdA;
     switch (x.type) {
@@ -363,7 +377,7 @@ SWX_HD double getdSdA(const Geom& x, double a, const double* ct)
 }
 
 // findroot.c:19-87 on f(a) = S(a) - s, used by generic_getAofS (xsect.c:1359-1400)
-SWX_HD double genericAofS(const Geom& x, double s, const double* ct)
+SWX_HD_COLD double genericAofS(const Geom& x, double s, const double* ct)
 {
     if (s <= 0.0) return 0.0;
     double x1, x2;
@@ -379,6 +393,7 @@ SWX_HD double genericAofS(const Geom& x, double s, const double* ct)
     double dxold = fabs(x2 - x1), dx = dxold;
     double f = getSofA(x, xx, ct) - s;
     double df = getdSdA(x, xx, ct);
+    #pragma unroll 1
     for (int j = 1; j <= 60; j++) {
         if ((((xx - xhi) * df - f) * ((xx - xlo) * df - f) >= 0.0 ||
              (fabs(2.0 * f) > fabs(dxold * df)))) {
@@ -428,13 +443,14 @@ SWX_HD double qCritical(const Geom& x, double yc, double qTarget, const double* 
 }
 
 // xsect.c:1634-1696
-SWX_HD double yCritEnum(const Geom& x, double q, double y0, const double* ct)
+SWX_HD_COLD double yCritEnum(const Geom& x, double q, double y0, const double* ct)
 {
     double dy = x.yFull / 25., yc, qc;
     int i1 = (int)(y0 / dy);
     double q0 = qCritical(x, i1 * dy, 0.0, ct);
     if (q0 < q) {
         yc = x.yFull;
+        #pragma unroll 1
         for (int i = i1 + 1; i <= 25; i++) {
             qc = qCritical(x, i * dy, 0.0, ct);
             if (qc >= q) {
@@ -445,6 +461,7 @@ SWX_HD double yCritEnum(const Geom& x, double q, double y0, const double* ct)
         }
     } else {
         yc = 0.0;
+        #pragma unroll 1
         for (int i = i1 - 1; i >= 0; i--) {
             qc = qCritical(x, i * dy, 0.0, ct);
             if (qc < q) {
@@ -458,7 +475,7 @@ SWX_HD double yCritEnum(const Geom& x, double q, double y0, const double* ct)
 }
 
 // xsect.c:1700-1748 with findroot_Ridder (findroot.c:90-138)
-SWX_HD double yCritRidder(const Geom& x, double q, double y0, const double* ct)
+SWX_HD_COLD double yCritRidder(const Geom& x, double q, double y0, const double* ct)
 {
     double y1 = 0.0, y2 = 0.99 * x.yFull;
     double q2 = qCritical(x, y2, 0.0, ct);
@@ -473,6 +490,7 @@ SWX_HD double yCritRidder(const Geom& x, double q, double y0, const double* ct)
     double ans = 0.5 * (y1 + y2);
     if ((flo > 0.0 && fhi < 0.0) || (flo < 0.0 && fhi > 0.0)) {
         double xlo = y1, xhi = y2;
+        #pragma unroll 1
         for (int j = 1; j <= 60; j++) {
             double xm = 0.5 * (xlo + xhi);
             double fm = qCritical(x, xm, q, ct);
@@ -494,7 +512,7 @@ SWX_HD double yCritRidder(const Geom& x, double q, double y0, const double* ct)
 }
 
 // xsect.c:1257-1319
-SWX_HD double getYcrit(const Geom& x, double q, const double* ct)
+SWX_HD_COLD double getYcrit(const Geom& x, double q, const double* ct)
 {
     double q2g = (q * q) / 32.2, y;
     if (q2g == 0.0) return 0.0;
@@ -519,7 +537,7 @@ SWX_HD double getYcrit(const Geom& x, double q, const double* ct)
 }
 
 // link.c:783-804 (conduits)
-SWX_HD double linkYnorm(const Geom& x, double q, double qMax, double beta, const double* ct)
+SWX_HD_COLD double linkYnorm(const Geom& x, double q, double qMax, double beta, const double* ct)
 {
     if (x.type == G_DUMMY) return 0.0;
     q = fabs(q);
