@@ -9,18 +9,25 @@ Inputs are resident in HBM before the timed region (swmm_start uploads them).
     value = sum over timed steps of (true conduits x Picard iterations)
             / wall time of the K timed steps        (max over ranks, all ranks)
 
-Default workload (N=1): 707 x 707 grid = 998,285 conduits / 499,850 nodes,
-DYNWAVE, 1 s fixed routing step (BASELINE.json configs[1] scaled to the 1M
-conduits the north_star target is quoted on; --grid 224 gives configs[1]).
+Workloads (--config; BASELINE.json configs):
+  1m_surcharge (default, configs[2]) 707 x 707 grid = 998,285 conduits /
+        499,850 nodes, DYNWAVE, VARIABLE_STEP 0.75, ROUTING_STEP 5 s, 1.0-ft
+        pipes, DWF 0.1 cfs per junction.  The run is first spun up for
+        --spinup steps (untimed, outside warmup) so that the timed window has
+        surcharged nodes (fraction reported in config.surcharged_pct).
+  1m_quality (configs[3]) the same plus 3 pollutants (advection + decay).
+  100k (configs[1]) 224 x 224 grid = 99,905 conduits, fixed 1 s step.
+  1m_fixed  707 x 707, fixed 1 s step, 1.5-ft pipes (no surcharge).
 
 Extra JSON objects:
   roofline      dominant kernel (link momentum) algorithmic bytes per launch
                 (byte model in DESIGN.md, from swmmx_getKernelBytes) divided
                 by its average HIP-event duration on the routing stream;
                 peak 8000 GB/s (MI355X HBM3E spec).  "traffic" = PMC bytes
-                from profiles/ when supplied with --traffic.
+                per launch from profiles/ when supplied with --traffic.
   cpu_baseline  the CPU restatement (oracle/, "port") timed on this host's
-                cores on a bounded sample of the same workload.
+                cores on a bounded sample of the same workload, continuing
+                from the spun-up state.
 """
 import argparse
 import json
@@ -34,6 +41,18 @@ sys.path.insert(0, PKG)
 
 METRIC = ("dynamic-wave link-updates/sec on synthetic grid net at 1/2/4/8 GPUs; HBM %peak")
 HBM_PEAK_GBS = 8000.0
+
+
+PRESETS = {
+    "1m_surcharge": dict(grid=707, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.1,
+                         pollutants=0, spinup=400),
+    "1m_quality": dict(grid=707, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.1,
+                       pollutants=3, spinup=400),
+    "100k": dict(grid=224, route_step=1.0, variable_step=0.0, diameter=1.5, q=0.02,
+                 pollutants=0, spinup=0),
+    "1m_fixed": dict(grid=707, route_step=1.0, variable_step=0.0, diameter=1.5, q=0.02,
+                     pollutants=0, spinup=0),
+}
 
 
 def make_inp(nx, route_step, variable_step, pollutants, diameter, q):
@@ -52,33 +71,23 @@ def make_inp(nx, route_step, variable_step, pollutants, diameter, q):
     return path
 
 
-def cpu_baseline(inp, steps, q, route_step):
-    """Time the oracle (plain-C restatement, single thread) on the same grid."""
+def cpu_baseline(dump, steps, q, route_step, variable):
+    """Time the oracle (plain-C restatement, single thread) from a state dump."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import swmm5
     from _dumpio import read_dump
     from _oracle import oracle_from_dump
-    s = swmm5.SWMM()
-    tmpd = "/tmp/swmm_bench"
-    os.makedirs(tmpd, exist_ok=True)
-    assert s.open(inp, os.path.join(tmpd, "cpu.rpt"), os.path.join(tmpd, "cpu.out")) == 0
-    assert s.start_host() == 0
-    dump = os.path.join(tmpd, "cpu_init_%d.bin" % os.getpid())
-    s.export_state(dump)
-    nL = s.getCount(swmm5.LINK)
-    s.close()
     o = oracle_from_dump(read_dump(dump))
-    os.remove(dump)
     lat = np.full(o.nN, q)
     lat[-1] = 0.0                       # the outfall has no DWF
     o.d("node.latIn")[:] = lat
     t0 = time.perf_counter()
     iters = 0
     for _ in range(steps):
-        iters += o.step(route_step)
+        dt = o.routing_step(route_step) if variable else route_step
+        iters += o.step(dt)
     dt = time.perf_counter() - t0
-    return nL * iters / dt, iters / steps
+    return o.nL * iters / dt, iters / steps, dt
 
 
 def main():
@@ -86,18 +95,20 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--grid", type=int, default=707)
-    ap.add_argument("--route-step", type=float, default=1.0)
-    ap.add_argument("--variable-step", type=float, default=0.0)
-    ap.add_argument("--pollutants", type=int, default=0)
-    ap.add_argument("--diameter", type=float, default=1.5)
-    ap.add_argument("--q", type=float, default=0.02)
-    ap.add_argument("--cpu-steps", type=int, default=40)
+    ap.add_argument("--config", choices=sorted(PRESETS), default="1m_surcharge")
+    ap.add_argument("--grid", type=int, default=None)
+    ap.add_argument("--spinup", type=int, default=None)
+    ap.add_argument("--cpu-steps", type=int, default=12)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--timing-steps", type=int, default=10)
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per link-momentum launch from rocprofv3 PMC (profiles/)")
     args = ap.parse_args()
+    cfg = dict(PRESETS[args.config])
+    if args.grid is not None:
+        cfg["grid"] = args.grid
+    if args.spinup is not None:
+        cfg["spinup"] = args.spinup
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -108,8 +119,8 @@ def main():
         dist.init_process_group("gloo")
 
     import swmm5
-    inp = make_inp(args.grid, args.route_step, args.variable_step, args.pollutants,
-                   args.diameter, args.q)
+    inp = make_inp(cfg["grid"], cfg["route_step"], cfg["variable_step"], cfg["pollutants"],
+                   cfg["diameter"], cfg["q"])
     s = swmm5.SWMM()
     s.set_device(local)
     tmpd = "/tmp/swmm_bench"
@@ -125,13 +136,16 @@ def main():
     nL = s.getCount(swmm5.LINK)
     nN = s.getCount(swmm5.NODE)
 
+    if cfg["spinup"]:
+        err, _ = s.run_steps(cfg["spinup"])
+        assert err == 0, s.getError()
     err, _ = s.run_steps(args.warmup)
     assert err == 0, s.getError()
     c0 = s.counters()                       # synchronises the device
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    err, _ = s.run_steps(args.steps)
+    err, t_days = s.run_steps(args.steps)
     c1 = s.counters()                       # synchronises the device
     t1 = time.perf_counter()
     if dist:
@@ -139,6 +153,7 @@ def main():
     assert err == 0, s.getError()
     elapsed = t1 - t0
     iters = c1["iterations"] - c0["iterations"]
+    nonconv = c1["nonconverged"] - c0["nonconverged"]
     updates = float(nL) * float(iters)
     if dist:
         import torch
@@ -148,6 +163,13 @@ def main():
         tsum = t.clone()
         dist.all_reduce(tsum[1:], op=dist.ReduceOp.SUM)
         elapsed, updates = float(tmax[0]), float(tsum[1])
+    depth = s.get_array("node.newDepth")
+    surcharged = float((depth[:-1] > cfg["diameter"]).mean()) * 100.0
+
+    dump = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        dump = os.path.join(tmpd, "cpu_state_%d.bin" % os.getpid())
+        s.export_state(dump)
 
     # per-kernel timing (HIP events on the routing stream), eager launches
     s.set_timing(True)
@@ -175,12 +197,15 @@ def main():
     }
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        rate, ipc = cpu_baseline(inp, args.cpu_steps, args.q, args.route_step)
+    if dump:
+        rate, ipc, secs = cpu_baseline(dump, args.cpu_steps, cfg["q"], cfg["route_step"],
+                                       cfg["variable_step"] > 0)
+        os.remove(dump)
         cpu = {"value": round(rate, 1), "unit": "link-updates/s", "cores": 1, "kind": "port",
-               "sample": "%d routing steps of the same %dx%d grid from its initial state, "
-                         "oracle/dw_oracle.c single-threaded (%.2f iterations/step)"
-                         % (args.cpu_steps, args.grid, args.grid, ipc)}
+               "sample": "%d routing steps (%.1f s CPU, %.2f iterations/step) of the same %dx%d "
+                         "grid continuing from the GPU run's state after the timed window; "
+                         "oracle/dw_oracle.c single-threaded"
+                         % (args.cpu_steps, secs, ipc, cfg["grid"], cfg["grid"])}
 
     if rank == 0:
         value = updates / elapsed
@@ -190,12 +215,17 @@ def main():
             "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "manhattan_grid_%dx%d_DYNWAVE_%s" % (
-                           args.grid, args.grid,
-                           "fixed%gs" % args.route_step if args.variable_step == 0 else
-                           "variable%g" % args.variable_step),
-                       "conduits": nL, "nodes": nN, "pollutants": args.pollutants,
+            "config": {"workload": "%s: manhattan_grid_%dx%d_DYNWAVE_%s_D%gft_q%gcfs_P%d" % (
+                           args.config, cfg["grid"], cfg["grid"],
+                           "fixed%gs" % cfg["route_step"] if cfg["variable_step"] == 0 else
+                           "variable%g_max%gs" % (cfg["variable_step"], cfg["route_step"]),
+                           cfg["diameter"], cfg["q"], cfg["pollutants"]),
+                       "conduits": nL, "nodes": nN, "pollutants": cfg["pollutants"],
+                       "spinup_steps": cfg["spinup"],
                        "iterations_per_step": round(iters / args.steps, 3),
+                       "nonconverged_steps": nonconv,
+                       "surcharged_pct": round(surcharged, 2),
+                       "sim_time_at_end_s": round(t_days * 86400.0, 1),
                        "parallelism": "replicas" if world > 1 else "single",
                        "backend": backend},
             "roofline": roof,

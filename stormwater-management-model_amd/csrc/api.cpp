@@ -177,8 +177,9 @@ static int execRouting()   // swmm5.c:514-575 + routing.c:203-265 on the device
     }
     if (rc) return setErr(r.lastError(), r.lastErrorMsg());
     G->mirrorValid = false;
-    // clock: identical arithmetic to the device's k_finalize; fixed steps are
-    // mirrored on the host, variable steps are read back (one sync per step)
+    // clock: identical arithmetic to the device's k_finalize (routing.c:301);
+    // fixed steps are mirrored on the host, variable steps take the dt the
+    // device chose at the end of the previous step (Router::launchedDt)
     G->oldRoutingTime = G->newRoutingTime;
     if (prj.opt.courantFactor == 0.0 || prj.opt.routeStep < 0.001) {
         double dt = prj.opt.routeStep;
@@ -188,9 +189,9 @@ static int execRouting()   // swmm5.c:514-575 + routing.c:203-265 on the device
         }
         G->newRoutingTime = G->newRoutingTime + 1000.0 * dt;
     } else {
-        double t;
-        if (r.readClock(&t, nullptr, nullptr)) return setErr(r.lastError(), r.lastErrorMsg());
-        G->newRoutingTime = t;
+        double dt;
+        if (r.launchedDt(&dt)) return setErr(r.lastError(), r.lastErrorMsg());
+        G->newRoutingTime = G->newRoutingTime + 1000.0 * dt;
     }
     return 0;
 }

@@ -49,7 +49,7 @@ namespace swx {
 constexpr int kBlock = 256;
 constexpr int kMaxTrialsCap = 32;
 constexpr int kNumPartials = 8;
-constexpr int kLinkWavesDefault = 1;   // per-block partial sums written by k_step_end
+constexpr int kLinkWavesDefault = 3;   // measured best on MI355X   // per-block partial sums written by k_step_end
 
 // ---- packed per-link flags -------------------------------------------------
 enum : uint32_t {
@@ -617,6 +617,7 @@ __global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
         if (!(k >= 2 && p.conv[nn.x] && p.conv[nn.y])) conduitFlow<kFirst, true>(p, j, f, nn, k, dt, ct);
         if (f & (LF_N1_OUTFALL | LF_N2_OUTFALL)) {
             int i = (f & LF_N2_OUTFALL) ? nn.y : nn.x;     // link.c:743-753 (node2 first)
+            if (kFirst) p.nOldDepth[i] = p.nNewDepth[i];    // node_setOldHydState before the update
             p.nNewDepth[i] = outfallDepth(p, i, p.nflags[i], j, f, ct);
         }
     }
@@ -638,7 +639,7 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
             // routing.c:328-332, node.c:293-304, 325-341 -- step-begin rotation
             double inflowPrev = p.inflow[i], outflowPrev = p.outflow[i];
             yOld = yLast;
-            p.nOldDepth[i] = yOld;
+            if (type != OUTFALL) p.nOldDepth[i] = yOld;   // outfalls: rotated by k_link_cold
             p.nOldVolume[i] = p.nNewVolume[i];
             p.oldFlowInflow[i] = inflowPrev;
             p.oldNetInflow[i] = inflowPrev - outflowPrev;
@@ -952,15 +953,18 @@ __global__ void k_finalize(Params p)
         }
     for (int q = 0; q < kNumPartials; q++) sum[q][t] = acc[q];
     __syncthreads();
+    for (int h = kBlock / 2; h > 0; h >>= 1) {          // fixed-shape tree: deterministic
+        if (t < h) {
+            for (int q = 0; q < kNumPartials; q++) {
+                double a = sum[q][t], b = sum[q][t + h];
+                sum[q][t] = (q == 5 || q == 6) ? ((b < a) ? b : a) : a + b;
+            }
+        }
+        __syncthreads();
+    }
     if (t != 0) return;
     double tot[kNumPartials];
-    for (int q = 0; q < kNumPartials; q++) {
-        double v = sum[q][0];
-        for (int i = 1; i < kBlock; i++) {
-            if (q == 5 || q == 6) v = (sum[q][i] < v) ? sum[q][i] : v; else v += sum[q][i];
-        }
-        tot[q] = v;
-    }
+    for (int q = 0; q < kNumPartials; q++) tot[q] = sum[q][0];
     StepCtl* c = p.ctl;
     // Picard step count / convergence (dynwave.c:242-257)
     int steps;
@@ -1011,6 +1015,8 @@ __global__ void k_finalize(Params p)
 struct Router::Impl {
     Params p{};
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;      // fork/join branch for the cold conduits
+    hipEvent_t forkEv[kMaxTrialsCap] = {}, joinEv[kMaxTrialsCap] = {};
     hipGraphExec_t graph = nullptr;
     bool useGraph = true;
     bool timing = false;
@@ -1032,6 +1038,9 @@ struct Router::Impl {
     bool tableShapes = true;
     static constexpr int kRing = 4;
     hipEvent_t ringEv[kRing] = {};
+    hipEvent_t clockEv[kRing] = {};
+    double* clockPinned = nullptr;   // kRing slots: dt of each launched step
+    int clockNext = 0, clockLast = 0;
     int ringNext = 0;
     size_t slotDoubles = 0;
     double lastDtHost = 0.0;
@@ -1047,6 +1056,14 @@ Router::~Router()
         for (void* a : d_->allocs) (void)hipFree(a);
         if (d_->hostPinned) (void)hipHostFree(d_->hostPinned);
         if (d_->hostCtl) (void)hipHostFree(d_->hostCtl);
+        if (d_->clockPinned) (void)hipHostFree(d_->clockPinned);
+        for (auto e : d_->clockEv) if (e) (void)hipEventDestroy(e);
+        for (auto e : d_->ringEv) if (e) (void)hipEventDestroy(e);
+        for (int k = 0; k < kMaxTrialsCap; k++) {
+            if (d_->forkEv[k]) (void)hipEventDestroy(d_->forkEv[k]);
+            if (d_->joinEv[k]) (void)hipEventDestroy(d_->joinEv[k]);
+        }
+        if (d_->side) (void)hipStreamDestroy(d_->side);
         if (d_->stream) (void)hipStreamDestroy(d_->stream);
         delete d_;
     }
@@ -1075,15 +1092,19 @@ static LinkKernelFn linkKernel(bool first, int waves)
 static void launchIteration(Router::Impl* d, int k)
 {
     Params& p = d->p;
-    if (k == 0) {
-        hipLaunchKernelGGL(linkKernel(true, d->linkWaves), dim3(d->gridL), dim3(kBlock), 0, d->stream, p, k);
-        if (p.nCold)
-            hipLaunchKernelGGL(k_link_cold<true>, dim3(d->gridC), dim3(kBlock), 0, d->stream, p, k);
-    } else {
-        hipLaunchKernelGGL(linkKernel(false, d->linkWaves), dim3(d->gridL), dim3(kBlock), 0, d->stream, p, k);
-        if (p.nCold)
-            hipLaunchKernelGGL(k_link_cold<false>, dim3(d->gridC), dim3(kBlock), 0, d->stream, p, k);
+    // the cold conduits run on a side branch, concurrently with the streaming
+    // kernel (disjoint links; both only read node depths); joined before k_node
+    if (p.nCold) {
+        (void)hipEventRecord(d->forkEv[k], d->stream);
+        (void)hipStreamWaitEvent(d->side, d->forkEv[k], 0);
+        if (k == 0)
+            hipLaunchKernelGGL(k_link_cold<true>, dim3(d->gridC), dim3(kBlock), 0, d->side, p, k);
+        else
+            hipLaunchKernelGGL(k_link_cold<false>, dim3(d->gridC), dim3(kBlock), 0, d->side, p, k);
+        (void)hipEventRecord(d->joinEv[k], d->side);
     }
+    hipLaunchKernelGGL(linkKernel(k == 0, d->linkWaves), dim3(d->gridL), dim3(kBlock), 0, d->stream, p, k);
+    if (p.nCold) (void)hipStreamWaitEvent(d->stream, d->joinEv[k], 0);
     if (d->timing) (void)hipEventRecord(d->ev[2 * k + 1], d->stream);
     if (k == 0) {
         hipLaunchKernelGGL(k_node<true>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
@@ -1127,6 +1148,11 @@ int Router::init(Project& prj, int device)
     HIPCHECK(hipGetDeviceProperties(&prop, device));
     devName_ = std::string("hip:") + prop.gcnArchName + ":" + prop.name;
     HIPCHECK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    HIPCHECK(hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking));
+    for (int k = 0; k < kMaxTrialsCap; k++) {
+        HIPCHECK(hipEventCreateWithFlags(&d->forkEv[k], hipEventDisableTiming));
+        HIPCHECK(hipEventCreateWithFlags(&d->joinEv[k], hipEventDisableTiming));
+    }
 
     Params& p = d->p;
     p.nN = nN; p.nL = nL; p.P = P;
@@ -1351,8 +1377,18 @@ int Router::init(Project& prj, int device)
     }
     if (const char* w = getenv("SWMM5_LINK_WAVES")) d->linkWaves = atoi(w);
     int maxBlocks = 8 * std::max(prop.multiProcessorCount, 1);
-    d->gridL = std::max(1, std::min((nL + kBlock - 1) / kBlock, maxBlocks));
-    d->gridN = std::max(1, std::min((nN + kBlock - 1) / kBlock, maxBlocks));
+    // streaming kernels: one resident wave of workgroups (grid-stride loops),
+    // so early-exited Picard iterations dispatch few workgroups
+    auto resident = [&](const void* fn, int n) {
+        int per = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kBlock, 0) != hipSuccess || per < 1)
+            per = 2;
+        int cap = per * std::max(prop.multiProcessorCount, 1);
+        if (const char* g = getenv("SWMM5_GRID_FACTOR")) cap = (int)(cap * atof(g));
+        return std::max(1, std::min((n + kBlock - 1) / kBlock, std::max(cap, 1)));
+    };
+    d->gridL = resident((const void*)linkKernel(false, d->linkWaves), nL);
+    d->gridN = resident((const void*)k_node<false>, nN);
     d->gridC = std::max(1, std::min((p.nCold + kBlock - 1) / kBlock, maxBlocks));
     d->gridEnd = std::max(1, std::min((std::max(nN, nL) + kBlock - 1) / kBlock, 2 * prop.multiProcessorCount));
     p.nBlocksEnd = d->gridEnd;
@@ -1383,6 +1419,8 @@ int Router::init(Project& prj, int device)
     d->pinnedSize = d->slotDoubles * Impl::kRing;
     HIPCHECK(hipHostMalloc((void**)&d->hostPinned, d->pinnedSize * sizeof(double), hipHostMallocDefault));
     for (auto& ev : d->ringEv) { HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming)); HIPCHECK(hipEventRecord(ev, d->stream)); }
+    for (auto& ev : d->clockEv) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIPCHECK(hipHostMalloc((void**)&d->clockPinned, Impl::kRing * sizeof(double), hipHostMallocDefault));
     d->ev.resize(2 * kMaxTrialsCap + 4);
     for (auto& ev : d->ev) HIPCHECK(hipEventCreate(&ev));
 
@@ -1449,6 +1487,17 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
                                 hipMemcpyHostToDevice, d->stream));
         HIPCHECK(hipEventRecord(d->ringEv[s], d->stream));
     }
+    // step length this step will use (written by the previous step's
+    // k_finalize): copied behind the previous step so the host clock can be
+    // advanced without draining the queue (see Router::launchedDt)
+    {
+        int s = d->clockNext;
+        d->clockNext = (d->clockNext + 1) % Impl::kRing;
+        HIPCHECK(hipMemcpyAsync(d->clockPinned + s, &d->ctl->dt, sizeof(double),
+                                hipMemcpyDeviceToHost, d->stream));
+        HIPCHECK(hipEventRecord(d->clockEv[s], d->stream));
+        d->clockLast = s;
+    }
     if (d->timing) {
         launchStep(d);
         HIPCHECK(hipStreamSynchronize(d->stream));
@@ -1470,6 +1519,15 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
     } else {
         HIPCHECK(hipGraphLaunch(d->graph, d->stream));
     }
+    return 0;
+}
+
+int Router::launchedDt(double* dt)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    HIPCHECK(hipEventSynchronize(d->clockEv[d->clockLast]));
+    *dt = d->clockPinned[d->clockLast];
     return 0;
 }
 

@@ -36,6 +36,9 @@ public:
     int step(const double* latFlow, const double* qualLoad, const double totals[3]);
     // Read the device clock after the last enqueued step (synchronises):
     // routing time (msec) and the step length used by that step.
+    // dt (sec) of the step most recently passed to step(); waits only for the
+    // previous step to finish, so one step stays queued on the device
+    int launchedDt(double* dt);
     int readClock(double* newRoutingTime, double* lastDt, double* nextDt);
     // Change the routing duration (msec) used for the end-of-run clamp.
     int setDuration(double msec);

@@ -21,7 +21,8 @@ for s in $STEPS; do
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pytest) run pytest_gpu 900 python -m pytest tests -q -m gpu --maxfail=5 -p no:cacheprovider ;;
     bench)  run bench 600 python bench.py ;;
-    bench100k) run bench100k 600 python bench.py --grid 224 --steps 400 --no-cpu ;;
+    bench100k) run bench100k 600 python bench.py --config 100k --steps 400 --no-cpu ;;
+    benchall) for c in 100k 1m_fixed 1m_quality; do run bench_$c 600 python bench.py --config $c --no-cpu; done ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --no-cpu ;;
     sweep)  for w in 1 3 4 5; do SWMM5_LINK_WAVES=$w run sweep_w$w 300 python bench.py --steps 200 --no-cpu; done ;;
     pmc)    run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu \
