@@ -36,19 +36,26 @@ int    DLLEXPORT swmmx_runSteps(int n, double *elapsedTime);
 
 /* Counters: [0] total routing steps, [1] total Picard iterations,
  * [2] non-converging steps, [3] Picard iterations of the last step,
- * [4] true conduits, [5] nodes.  Synchronises with the device. */
+ * [4] true conduits, [5] nodes, [6] conduits updated (not bypassed) by the
+ * Picard iterations >= 1 timed since swmmx_setTiming(1), [7] conduits handled
+ * by the streaming link kernel.  Synchronises with the device. */
 int    DLLEXPORT swmmx_getCounters(long long *out, int n);
 
-/* Device kernel timing (HIP events on the routing stream).  mode=1 enables,
- * 0 disables; swmmx_getKernelTimes returns, per kernel class, the number of
- * timed launches and their total milliseconds:
- *   out[2*k] = launches, out[2*k+1] = ms;  k: 0 link momentum, 1 node update,
- *   2 step end, 3 quality.  Returns the number of classes written. */
+/* Device kernel timing (HIP events on the routing stream; steps run as eager
+ * launches while enabled).  mode=1 enables, 0 disables; swmmx_getKernelTimes
+ * returns, per kernel class, the number of timed launches and their total
+ * milliseconds:  out[2*k] = launches, out[2*k+1] = ms;
+ *   k: 0 link momentum, Picard iteration 0 (k_link<first>: every conduit),
+ *      1 node update, 2 step end, 3 quality,
+ *      4 link momentum, executed iterations >= 1 (bypassed conduits skipped).
+ * Returns the number of classes written. */
 int    DLLEXPORT swmmx_setTiming(int mode);
 int    DLLEXPORT swmmx_getKernelTimes(double *out, int n);
 
-/* Algorithmic bytes per launch of each kernel class for the current network
- * (the byte model of DESIGN.md), same class order as above. */
+/* Algorithmic bytes per launch of each kernel class (the byte model of
+ * DESIGN.md), same class order as above: the average over the launches timed
+ * since swmmx_setTiming(1) (class 4 counts the conduits actually updated),
+ * or the model value for a full launch when nothing has been timed. */
 int    DLLEXPORT swmmx_getKernelBytes(double *out, int n);
 
 /* Name of the compute backend ("hip:gfx950:<device name>" or "none"). */

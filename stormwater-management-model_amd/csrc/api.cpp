@@ -801,13 +801,17 @@ int DLLEXPORT swmmx_exportState(const char* path)
 int DLLEXPORT swmmx_getCounters(long long* out, int n)
 {
     if (!G || !out) return 0;
-    long long v[6] = {G->totalStepCount, 0, 0, 0, G->prj->net.nLinks(), G->prj->net.nNodes()};
+    long long v[8] = {G->totalStepCount, 0, 0, 0, G->prj->net.nLinks(), G->prj->net.nNodes(), 0, 0};
     if (G->router && G->router->ok()) {
         int last = 0;
         G->router->counters(&v[1], &v[2], &last);
         v[3] = last;
+        double upd = 0, hot = 0;
+        G->router->timedWork(&upd, &hot);
+        v[6] = (long long)upd;
+        v[7] = (long long)hot;
     }
-    int m = n < 6 ? n : 6;
+    int m = n < 8 ? n : 8;
     for (int i = 0; i < m; i++) out[i] = v[i];
     return m;
 }

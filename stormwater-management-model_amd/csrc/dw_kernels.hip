@@ -94,6 +94,7 @@ struct StepCtl {
     double newRoutingTime;            // msec (swmm5.c / routing.c clock mirror)
     double routingDuration;           // msec
     double routeStep;                 // fixed step (sec)
+    unsigned long long linkWork[kMaxTrialsCap];   // timing mode: conduits updated per iteration
 };
 
 struct Params {
@@ -132,8 +133,10 @@ struct Params {
     const double* gTables;        // global copy of the 5x51 circular tables
     double* partials;             // [nBlocksEnd][kNumPartials]
     int nBlocksEnd;
-    int nCold;
+    int countWork;                // timing mode: count updated conduits per iteration
+    int nCold, nOutLinks;
     const int* coldLinks;         // LF_COLD conduits, ascending
+    const int* outLinks;          // conduits with an outfall end, ascending
     StepCtl* ctl;
 };
 
@@ -562,12 +565,19 @@ void k_link(Params p, int k)
     __shared__ double ct[5 * SWX_CIRC_N];
     stageTables(ct, p.gTables);
     double dt = p.ctl->dt;
+    int work = 0;
     for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nL; j += gridDim.x * kBlock) {
         uint32_t f = p.lflags[j];
         if (f & LF_COLD) continue;
         int2 nn = p.lnodes[j];
         if (k >= 2 && p.conv[nn.x] && p.conv[nn.y]) continue;   // findBypassedLinks dynwave.c:335-345
         conduitFlow<kFirst, false>(p, j, f, nn, k, dt, ct);
+        work++;
+    }
+    if (p.countWork) {                                     // measurement only (eager launches)
+        for (int off = 32; off > 0; off >>= 1) work += __shfl_down(work, off, 64);
+        if ((threadIdx.x & 63) == 0 && work)
+            atomicAdd(&p.ctl->linkWork[k], (unsigned long long)work);
     }
 }
 
@@ -599,10 +609,7 @@ __device__ __forceinline__ double outfallDepth(const Params& p, int i, uint32_t 
 
 
 // The few conduits with an invert offset or an outfall end (compacted list):
-// full flow classification with normal / critical depth, then, for an outfall
-// end, link_setOutfallDepth (findNodeDepths, dynwave.c:605).  The outfall's
-// only reader in the next iteration is this same link, and the outfall is
-// never "converged", so the link is never bypassed (dynwave.c:281, 340).
+// full flow classification with normal / critical depth.
 template <bool kFirst>
 __global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
 {
@@ -614,12 +621,30 @@ __global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
         int j = p.coldLinks[c];
         uint32_t f = p.lflags[j];
         int2 nn = p.lnodes[j];
-        if (!(k >= 2 && p.conv[nn.x] && p.conv[nn.y])) conduitFlow<kFirst, true>(p, j, f, nn, k, dt, ct);
-        if (f & (LF_N1_OUTFALL | LF_N2_OUTFALL)) {
-            int i = (f & LF_N2_OUTFALL) ? nn.y : nn.x;     // link.c:743-753 (node2 first)
-            if (kFirst) p.nOldDepth[i] = p.nNewDepth[i];    // node_setOldHydState before the update
-            p.nNewDepth[i] = outfallDepth(p, i, p.nflags[i], j, f, ct);
-        }
+        if (k >= 2 && p.conv[nn.x] && p.conv[nn.y]) continue;
+        conduitFlow<kFirst, true>(p, j, f, nn, k, dt, ct);
+    }
+}
+
+// link_setOutfallDepth for every conduit with an outfall end (findNodeDepths,
+// dynwave.c:605): runs on the side branch after k_link_cold, concurrently with
+// k_node and the next iteration's streaming kernel.  That is safe because the
+// outfall's depth is read only by its single link (next iteration, in
+// k_link_cold, which waits for this kernel) and by the step-end kernels.  The
+// outfall is never "converged" (dynwave.c:281, 340), so its link is never
+// bypassed and the depth is always refreshed.
+template <bool kFirst>
+__global__ __launch_bounds__(kBlock) void k_outfall(Params p, int k)
+{
+    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
+    const double* ct = p.gTables;
+    for (int c = blockIdx.x * kBlock + threadIdx.x; c < p.nOutLinks; c += gridDim.x * kBlock) {
+        int j = p.outLinks[c];
+        uint32_t f = p.lflags[j];
+        int2 nn = p.lnodes[j];
+        int i = (f & LF_N2_OUTFALL) ? nn.y : nn.x;         // link.c:743-753 (node2 first)
+        if (kFirst) p.nOldDepth[i] = p.nNewDepth[i];        // node_setOldHydState before the update
+        p.nNewDepth[i] = outfallDepth(p, i, p.nflags[i], j, f, ct);
     }
 }
 
@@ -633,7 +658,9 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
         uint32_t nf = p.nflags[i];
         int type = (int)(nf & NF_TYPE);
-        double yLast = p.nNewDepth[i];
+        // an outfall's depth may be being written by k_outfall (side branch):
+        // it is not read here
+        double yLast = (type == OUTFALL) ? 0.0 : p.nNewDepth[i];
         double yOld, lat;
         if (kFirst) {
             // routing.c:328-332, node.c:293-304, 325-341 -- step-begin rotation
@@ -1016,11 +1043,11 @@ struct Router::Impl {
     Params p{};
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;      // fork/join branch for the cold conduits
-    hipEvent_t forkEv[kMaxTrialsCap] = {}, joinEv[kMaxTrialsCap] = {};
+    hipEvent_t forkEv[kMaxTrialsCap] = {}, joinEv[kMaxTrialsCap] = {}, tailEv = nullptr;
     hipGraphExec_t graph = nullptr;
     bool useGraph = true;
     bool timing = false;
-    int gridL = 1, gridN = 1, gridEnd = 1, gridC = 1;
+    int gridL = 1, gridN = 1, gridEnd = 1, gridC = 1, gridO = 1;
     int linkWaves = kLinkWavesDefault;
     std::vector<void*> allocs;
     double* latBase = nullptr;       // constant lateral inflows
@@ -1031,9 +1058,14 @@ struct Router::Impl {
     StepCtl* hostCtl = nullptr;      // pinned
     bool constantInflow = true;
     std::vector<hipEvent_t> ev;      // timing events
-    double kms[4] = {0, 0, 0, 0};
-    long long kcnt[4] = {0, 0, 0, 0};
-    double kbytes[4] = {0, 0, 0, 0};
+    static constexpr int kClasses = 5;
+    double kms[kClasses] = {};
+    long long kcnt[kClasses] = {};
+    double kbytes[kClasses] = {};     // byte model per launch (class 4: per updated conduit)
+    double kbytesSum[kClasses] = {};  // algorithmic bytes of the timed launches
+    hipEvent_t evHot[kMaxTrialsCap] = {};
+    double nHot = 0, nColdD = 0;
+    double workSum = 0;               // conduits updated in timed iterations >= 1
     int nE = 0;
     bool tableShapes = true;
     static constexpr int kRing = 4;
@@ -1053,6 +1085,7 @@ Router::~Router()
     if (d_) {
         if (d_->graph) (void)hipGraphExecDestroy(d_->graph);
         for (auto e : d_->ev) (void)hipEventDestroy(e);
+        for (auto e : d_->evHot) if (e) (void)hipEventDestroy(e);
         for (void* a : d_->allocs) (void)hipFree(a);
         if (d_->hostPinned) (void)hipHostFree(d_->hostPinned);
         if (d_->hostCtl) (void)hipHostFree(d_->hostCtl);
@@ -1063,6 +1096,7 @@ Router::~Router()
             if (d_->forkEv[k]) (void)hipEventDestroy(d_->forkEv[k]);
             if (d_->joinEv[k]) (void)hipEventDestroy(d_->joinEv[k]);
         }
+        if (d_->tailEv) (void)hipEventDestroy(d_->tailEv);
         if (d_->side) (void)hipStreamDestroy(d_->side);
         if (d_->stream) (void)hipStreamDestroy(d_->stream);
         delete d_;
@@ -1089,12 +1123,17 @@ static LinkKernelFn linkKernel(bool first, int waves)
     }
 }
 
+// Side branch per iteration k (stream d->side, joined into the graph):
+//   wait fork(k) -> k_link_cold(k) -> record join(k) -> k_outfall(k)
+// Main stream:
+//   record fork(k) -> k_link(k) -> wait join(k) -> k_node(k)
+// fork(k) is recorded after k_node(k-1), so k_link_cold(k) sees final node
+// depths, and (side stream order) after k_outfall(k-1).
 static void launchIteration(Router::Impl* d, int k)
 {
     Params& p = d->p;
-    // the cold conduits run on a side branch, concurrently with the streaming
-    // kernel (disjoint links; both only read node depths); joined before k_node
-    if (p.nCold) {
+    bool side = p.nCold > 0;
+    if (side) {
         (void)hipEventRecord(d->forkEv[k], d->stream);
         (void)hipStreamWaitEvent(d->side, d->forkEv[k], 0);
         if (k == 0)
@@ -1102,9 +1141,16 @@ static void launchIteration(Router::Impl* d, int k)
         else
             hipLaunchKernelGGL(k_link_cold<false>, dim3(d->gridC), dim3(kBlock), 0, d->side, p, k);
         (void)hipEventRecord(d->joinEv[k], d->side);
+        if (p.nOutLinks) {
+            if (k == 0)
+                hipLaunchKernelGGL(k_outfall<true>, dim3(d->gridO), dim3(kBlock), 0, d->side, p, k);
+            else
+                hipLaunchKernelGGL(k_outfall<false>, dim3(d->gridO), dim3(kBlock), 0, d->side, p, k);
+        }
     }
     hipLaunchKernelGGL(linkKernel(k == 0, d->linkWaves), dim3(d->gridL), dim3(kBlock), 0, d->stream, p, k);
-    if (p.nCold) (void)hipStreamWaitEvent(d->stream, d->joinEv[k], 0);
+    if (d->timing) (void)hipEventRecord(d->evHot[k], d->stream);
+    if (side) (void)hipStreamWaitEvent(d->stream, d->joinEv[k], 0);
     if (d->timing) (void)hipEventRecord(d->ev[2 * k + 1], d->stream);
     if (k == 0) {
         hipLaunchKernelGGL(k_node<true>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
@@ -1119,6 +1165,10 @@ static void launchStep(Router::Impl* d)
     Params& p = d->p;
     if (d->timing) (void)hipEventRecord(d->ev[0], d->stream);
     for (int k = 0; k < p.maxTrials; k++) launchIteration(d, k);
+    if (p.nCold) {                                  // outfall depths final before step end
+        (void)hipEventRecord(d->tailEv, d->side);
+        (void)hipStreamWaitEvent(d->stream, d->tailEv, 0);
+    }
     int base = 2 * p.maxTrials + 1;
     if (p.P > 0) {
         hipLaunchKernelGGL(k_qual_node, dim3(d->gridN), dim3(kBlock), 0, d->stream, p);
@@ -1149,6 +1199,7 @@ int Router::init(Project& prj, int device)
     devName_ = std::string("hip:") + prop.gcnArchName + ":" + prop.name;
     HIPCHECK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking));
+    HIPCHECK(hipEventCreateWithFlags(&d->tailEv, hipEventDisableTiming));
     for (int k = 0; k < kMaxTrialsCap; k++) {
         HIPCHECK(hipEventCreateWithFlags(&d->forkEv[k], hipEventDisableTiming));
         HIPCHECK(hipEventCreateWithFlags(&d->joinEv[k], hipEventDisableTiming));
@@ -1186,7 +1237,7 @@ int Router::init(Project& prj, int device)
 
     // ---- link static ------------------------------------------------------
     std::vector<int> nodes2((size_t)nL * 2);
-    std::vector<int> lflags(nL), coldLinks;
+    std::vector<int> lflags(nL), coldLinks, outLinks;
     std::vector<double> inv1(nL), inv2(nL), xd[11];
     for (auto& v : xd) v.resize(nL);
     for (int j = 0; j < nL; j++) {
@@ -1210,6 +1261,7 @@ int Router::init(Project& prj, int device)
             f |= LF_COLD;
             coldLinks.push_back(j);
         }
+        if (f & (LF_N1_OUTFALL | LF_N2_OUTFALL)) outLinks.push_back(j);
         lflags[j] = (int)f;
         xd[0][j] = x.yFull; xd[1][j] = x.wMax; xd[2][j] = x.ywMax; xd[3][j] = x.aFull;
         xd[4][j] = x.rFull; xd[5][j] = x.sFull; xd[6][j] = x.sMax; xd[7][j] = x.yBot;
@@ -1226,6 +1278,9 @@ int Router::init(Project& prj, int device)
         UPI(cl, coldLinks, coldLinks.size());
         p.coldLinks = cl;
         p.nCold = (int)coldLinks.size();
+        UPI(cl, outLinks, outLinks.size());
+        p.outLinks = cl;
+        p.nOutLinks = (int)outLinks.size();
     }
     double* tmp;
     UPD(tmp, inv1, nL); p.inv1 = tmp;
@@ -1390,6 +1445,7 @@ int Router::init(Project& prj, int device)
     d->gridL = resident((const void*)linkKernel(false, d->linkWaves), nL);
     d->gridN = resident((const void*)k_node<false>, nN);
     d->gridC = std::max(1, std::min((p.nCold + kBlock - 1) / kBlock, maxBlocks));
+    d->gridO = std::max(1, std::min((p.nOutLinks + kBlock - 1) / kBlock, maxBlocks));
     d->gridEnd = std::max(1, std::min((std::max(nN, nL) + kBlock - 1) / kBlock, 2 * prop.multiProcessorCount));
     p.nBlocksEnd = d->gridEnd;
     p.partials = devAlloc<double>(d, (size_t)d->gridEnd * kNumPartials, &e);
@@ -1423,18 +1479,27 @@ int Router::init(Project& prj, int device)
     HIPCHECK(hipHostMalloc((void**)&d->clockPinned, Impl::kRing * sizeof(double), hipHostMallocDefault));
     d->ev.resize(2 * kMaxTrialsCap + 4);
     for (auto& ev : d->ev) HIPCHECK(hipEventCreate(&ev));
+    for (auto& ev : d->evHot) HIPCHECK(hipEventCreate(&ev));
 
     // algorithmic bytes per launch (DESIGN.md byte model; per kernel class)
     {
         double L = nL, N = nN, E = d->nE;
-        // link momentum, per conduit and Picard iteration >= 1:
+        // link momentum, per streaming conduit:
         //   static   nodes 8 + flags 4 + inv1/inv2 16 + geometry 7x8
         //            + length/modLength/roughFactor/beta 32           = 116
-        //   dynamic  oldFlow, setting, q1, a2 4x8 + lstate 4          =  36
         //   gathers  newDepth at both end nodes                       =  16
         //   writes   a1 q1 newDepth newVolume newFlow dqdh froude
         //            sa1 sa2 evap seep 11x8 + lstate 4                =  92
-        d->kbytes[0] = L * (116 + 36 + 16 + 92);
+        //   iteration 0 (k_link<true>): reads newFlow newDepth newVolume a1
+        //            setting q1 6x8 + lstate 4, writes oldFlow oldDepth
+        //            oldVolume a2 4x8                                 =  84
+        //   iterations >= 1: reads oldFlow setting q1 a2 4x8 + lstate 4 = 36
+        //   a bypassed conduit costs flags 4 + nodes 8 + 2 conv flags 8 = 20,
+        //   a cold conduit skipped by the streaming kernel costs its flags 4
+        d->nHot = L - p.nCold;
+        d->nColdD = p.nCold;
+        d->kbytes[0] = d->nHot * (116 + 16 + 92 + 84) + d->nColdD * 4;
+        d->kbytes[4] = 116 + 16 + 92 + 36;
         // node update: per node static (flags, fullDepth, surDepth, yCrown,
         //   fullVolume, ponded: 4+5x8) + rowptr 4 + dynamic reads (newDepth,
         //   oldDepth, oldNetInflow, newLat, oldSurfArea: 40) + writes (inflow,
@@ -1503,19 +1568,31 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
         HIPCHECK(hipStreamSynchronize(d->stream));
         int ran = 0;
         HIPCHECK(hipMemcpy(&ran, &d->ctl->lastSteps, sizeof(int), hipMemcpyDeviceToHost));
+        unsigned long long work[kMaxTrialsCap];
+        HIPCHECK(hipMemcpy(work, d->ctl->linkWork, sizeof(work), hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemset(d->ctl->linkWork, 0, sizeof(work)));
         for (int k = 0; k < ran; k++) {    // early-exited iterations are not counted
             float ms1 = 0, ms2 = 0;
-            (void)hipEventElapsedTime(&ms1, d->ev[2 * k], d->ev[2 * k + 1]);
+            (void)hipEventElapsedTime(&ms1, d->ev[2 * k], d->evHot[k]);
             (void)hipEventElapsedTime(&ms2, d->ev[2 * k + 1], d->ev[2 * k + 2]);
-            d->kms[0] += ms1; d->kcnt[0]++;
+            int c = (k == 0) ? 0 : 4;
+            d->kms[c] += ms1; d->kcnt[c]++;
+            if (k == 0) d->kbytesSum[0] += d->kbytes[0];
+            else {
+                double w = (double)work[k];
+                d->workSum += w;
+                d->kbytesSum[4] += w * d->kbytes[4] + (d->nHot - w) * 20.0 + d->nColdD * 4.0;
+            }
             d->kms[1] += ms2; d->kcnt[1]++;
+            d->kbytesSum[1] += d->kbytes[1];
         }
         int base = 2 * p.maxTrials + 1;
         float ms3 = 0, msq = 0;
         (void)hipEventElapsedTime(&ms3, d->ev[base], d->ev[base + 1]);
         (void)hipEventElapsedTime(&msq, d->ev[2 * p.maxTrials], d->ev[base]);
         d->kms[2] += ms3; d->kcnt[2]++;
-        if (p.P) { d->kms[3] += msq; d->kcnt[3]++; }
+        d->kbytesSum[2] += d->kbytes[2];
+        if (p.P) { d->kms[3] += msq; d->kcnt[3]++; d->kbytesSum[3] += d->kbytes[3]; }
     } else {
         HIPCHECK(hipGraphLaunch(d->graph, d->stream));
     }
@@ -1697,12 +1774,20 @@ void Router::stepTotals(double out[6])
 void Router::setTiming(bool on)
 {
     d_->timing = on;
-    for (int k = 0; k < 4; k++) { d_->kms[k] = 0; d_->kcnt[k] = 0; }
+    d_->p.countWork = on ? 1 : 0;                  // eager launches only; the graph keeps 0
+    for (int k = 0; k < Impl::kClasses; k++) { d_->kms[k] = 0; d_->kcnt[k] = 0; d_->kbytesSum[k] = 0; }
+    d_->workSum = 0;
+}
+
+void Router::timedWork(double* updated, double* hot)
+{
+    *updated = d_->workSum;
+    *hot = d_->nHot;
 }
 
 int Router::kernelTimes(double* out, int n)
 {
-    int m = std::min(n / 2, 4);
+    int m = std::min(n / 2, (int)Impl::kClasses);
     for (int k = 0; k < m; k++) {
         out[2 * k] = (double)d_->kcnt[k];
         out[2 * k + 1] = d_->kms[k];
@@ -1712,8 +1797,12 @@ int Router::kernelTimes(double* out, int n)
 
 int Router::kernelBytes(double* out, int n)
 {
-    int m = std::min(n, 4);
-    for (int k = 0; k < m; k++) out[k] = d_->kbytes[k];
+    // average algorithmic bytes per timed launch (byte model when nothing was timed)
+    int m = std::min(n, (int)Impl::kClasses);
+    for (int k = 0; k < m; k++) {
+        double model = (k == 4) ? d_->kbytes[4] * d_->nHot : d_->kbytes[k];
+        out[k] = d_->kcnt[k] ? d_->kbytesSum[k] / (double)d_->kcnt[k] : model;
+    }
     return m;
 }
 

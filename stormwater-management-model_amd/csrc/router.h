@@ -38,6 +38,8 @@ public:
     // routing time (msec) and the step length used by that step.
     // dt (sec) of the step most recently passed to step(); waits only for the
     // previous step to finish, so one step stays queued on the device
+    // conduits updated by the timed iterations >= 1, and streaming conduits
+    void timedWork(double* updated, double* hot);
     int launchedDt(double* dt);
     int readClock(double* newRoutingTime, double* lastDt, double* nextDt);
     // Change the routing duration (msec) used for the end-of-run clamp.

@@ -38,6 +38,10 @@ class EngineMissing(RuntimeError):
     pass
 
 
+# kernel classes of swmmx_getKernelTimes / swmmx_getKernelBytes
+KERNEL_CLASSES = ["link_momentum_first", "node_update", "step_end", "quality", "link_momentum_iter"]
+
+
 def load_library(path: str | None = None):
     """Load the engine; raises EngineMissing (never falls back) if absent."""
     global _lib
@@ -217,24 +221,25 @@ class SWMM:
         return err, t.value
 
     def counters(self):
-        a = (ctypes.c_longlong * 6)()
-        self.L.swmmx_getCounters(a, 6)
-        keys = ["steps", "iterations", "nonconverged", "last_iterations", "conduits", "nodes"]
+        a = (ctypes.c_longlong * 8)()
+        self.L.swmmx_getCounters(a, 8)
+        keys = ["steps", "iterations", "nonconverged", "last_iterations", "conduits", "nodes",
+                "timed_updated", "streaming_conduits"]
         return dict(zip(keys, list(a)))
 
     def set_timing(self, on: bool):
         return self.L.swmmx_setTiming(1 if on else 0)
 
     def kernel_times(self):
-        a = (ctypes.c_double * 8)()
-        n = self.L.swmmx_getKernelTimes(a, 8)
-        names = ["link_momentum", "node_update", "step_end", "quality"]
+        a = (ctypes.c_double * 10)()
+        n = self.L.swmmx_getKernelTimes(a, 10)
+        names = KERNEL_CLASSES
         return {names[k]: (a[2 * k], a[2 * k + 1]) for k in range(n)}
 
     def kernel_bytes(self):
-        a = (ctypes.c_double * 4)()
-        n = self.L.swmmx_getKernelBytes(a, 4)
-        names = ["link_momentum", "node_update", "step_end", "quality"]
+        a = (ctypes.c_double * 5)()
+        n = self.L.swmmx_getKernelBytes(a, 5)
+        names = KERNEL_CLASSES
         return {names[k]: a[k] for k in range(n)}
 
     def backend(self):
