@@ -64,7 +64,7 @@ enum : uint32_t {
     LF_SEEP = 1u << 19,           // seepage > 0 or evaporation active
     LF_QLIMIT = 1u << 20,
     LF_DIRNEG = 1u << 21,
-    LF_COLD = 1u << 22,           // offset or outfall end: may need normal/critical depth
+    LF_COLD = 1u << 22,           // an invert offset: may need normal/critical depth
 };
 // ---- packed per-node flags -------------------------------------------------
 enum : uint32_t {
@@ -230,9 +230,10 @@ __device__ double conduitLossRate(const Params& p, int j, const Geom& x, double 
 }
 
 // dwflow.c:297-413.  kCold = false is the specialisation for links with both
-// offsets zero and no outfall end (LF_COLD clear): z1 = z2 = 0, so the branches
-// that need normal / critical depth (root finders) are unreachable and are not
-// compiled into the streaming kernel.
+// offsets zero (LF_COLD clear): z1 = z2 = 0 (at an outfall end too, since
+// max(0, 0 - depth) = 0), so the branches that need normal / critical depth
+// (root finders) are unreachable and are not compiled into the streaming
+// kernel.
 template <bool kCold>
 __device__ __forceinline__ int flowClassOf(const Params& p, int j, const Geom& x, uint32_t f,
                                            int n1, int n2, double q, double h1, double h2,
@@ -627,17 +628,17 @@ __global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
 }
 
 // link_setOutfallDepth for every conduit with an outfall end (findNodeDepths,
-// dynwave.c:605): runs on the side branch after k_link_cold, concurrently with
-// k_node and the next iteration's streaming kernel.  That is safe because the
-// outfall's depth is read only by its single link (next iteration, in
-// k_link_cold, which waits for this kernel) and by the step-end kernels.  The
-// outfall is never "converged" (dynwave.c:281, 340), so its link is never
-// bypassed and the depth is always refreshed.
+// dynwave.c:605): runs on the side branch once the iteration's link flows are
+// final, concurrently with k_node (which never reads an outfall's depth); the
+// next iteration's link kernels wait for it.  The outfall is never
+// "converged" (dynwave.c:281, 340), so its link is never bypassed and the
+// depth is refreshed every iteration, as in the reference.
 template <bool kFirst>
 __global__ __launch_bounds__(kBlock) void k_outfall(Params p, int k)
 {
     if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
-    const double* ct = p.gTables;
+    __shared__ double ct[5 * SWX_CIRC_N];
+    stageTables(ct, p.gTables);
     for (int c = blockIdx.x * kBlock + threadIdx.x; c < p.nOutLinks; c += gridDim.x * kBlock) {
         int j = p.outLinks[c];
         uint32_t f = p.lflags[j];
@@ -1043,7 +1044,8 @@ struct Router::Impl {
     Params p{};
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;      // fork/join branch for the cold conduits
-    hipEvent_t forkEv[kMaxTrialsCap] = {}, joinEv[kMaxTrialsCap] = {}, tailEv = nullptr;
+    hipEvent_t forkEv[kMaxTrialsCap] = {}, joinEv[kMaxTrialsCap] = {};
+    hipEvent_t hotEv[kMaxTrialsCap] = {}, outEv[kMaxTrialsCap] = {};
     hipGraphExec_t graph = nullptr;
     bool useGraph = true;
     bool timing = false;
@@ -1096,7 +1098,10 @@ Router::~Router()
             if (d_->forkEv[k]) (void)hipEventDestroy(d_->forkEv[k]);
             if (d_->joinEv[k]) (void)hipEventDestroy(d_->joinEv[k]);
         }
-        if (d_->tailEv) (void)hipEventDestroy(d_->tailEv);
+        for (int k = 0; k < kMaxTrialsCap; k++) {
+            if (d_->hotEv[k]) (void)hipEventDestroy(d_->hotEv[k]);
+            if (d_->outEv[k]) (void)hipEventDestroy(d_->outEv[k]);
+        }
         if (d_->side) (void)hipStreamDestroy(d_->side);
         if (d_->stream) (void)hipStreamDestroy(d_->stream);
         delete d_;
@@ -1123,17 +1128,17 @@ static LinkKernelFn linkKernel(bool first, int waves)
     }
 }
 
-// Side branch per iteration k (stream d->side, joined into the graph):
-//   wait fork(k) -> k_link_cold(k) -> record join(k) -> k_outfall(k)
-// Main stream:
-//   record fork(k) -> k_link(k) -> wait join(k) -> k_node(k)
-// fork(k) is recorded after k_node(k-1), so k_link_cold(k) sees final node
-// depths, and (side stream order) after k_outfall(k-1).
+// One Picard iteration k.  Main stream (d->stream) and side stream (d->side),
+// joined into one graph by events:
+//   main:  [fork k] k_link(k) [hot k] ─wait join k─ k_node(k) ─wait out k─►
+//   side:  wait fork k ─ k_link_cold(k) [join k] ─wait hot k─ k_outfall(k) [out k]
+// k_link_cold (offset conduits) overlaps the streaming kernel; k_outfall
+// overlaps k_node; iteration k+1 starts after both.
 static void launchIteration(Router::Impl* d, int k)
 {
     Params& p = d->p;
-    bool side = p.nCold > 0;
-    if (side) {
+    if (d->timing) (void)hipEventRecord(d->ev[4 * k], d->stream);
+    if (p.nCold) {
         (void)hipEventRecord(d->forkEv[k], d->stream);
         (void)hipStreamWaitEvent(d->side, d->forkEv[k], 0);
         if (k == 0)
@@ -1141,43 +1146,43 @@ static void launchIteration(Router::Impl* d, int k)
         else
             hipLaunchKernelGGL(k_link_cold<false>, dim3(d->gridC), dim3(kBlock), 0, d->side, p, k);
         (void)hipEventRecord(d->joinEv[k], d->side);
-        if (p.nOutLinks) {
-            if (k == 0)
-                hipLaunchKernelGGL(k_outfall<true>, dim3(d->gridO), dim3(kBlock), 0, d->side, p, k);
-            else
-                hipLaunchKernelGGL(k_outfall<false>, dim3(d->gridO), dim3(kBlock), 0, d->side, p, k);
-        }
     }
     hipLaunchKernelGGL(linkKernel(k == 0, d->linkWaves), dim3(d->gridL), dim3(kBlock), 0, d->stream, p, k);
     if (d->timing) (void)hipEventRecord(d->evHot[k], d->stream);
-    if (side) (void)hipStreamWaitEvent(d->stream, d->joinEv[k], 0);
-    if (d->timing) (void)hipEventRecord(d->ev[2 * k + 1], d->stream);
+    if (p.nOutLinks) {
+        (void)hipEventRecord(d->hotEv[k], d->stream);
+        (void)hipStreamWaitEvent(d->side, d->hotEv[k], 0);
+        if (k == 0)
+            hipLaunchKernelGGL(k_outfall<true>, dim3(d->gridO), dim3(kBlock), 0, d->side, p, k);
+        else
+            hipLaunchKernelGGL(k_outfall<false>, dim3(d->gridO), dim3(kBlock), 0, d->side, p, k);
+        (void)hipEventRecord(d->outEv[k], d->side);
+    }
+    if (p.nCold) (void)hipStreamWaitEvent(d->stream, d->joinEv[k], 0);
+    if (d->timing) (void)hipEventRecord(d->ev[4 * k + 1], d->stream);
     if (k == 0) {
         hipLaunchKernelGGL(k_node<true>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
     } else {
         hipLaunchKernelGGL(k_node<false>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
     }
-    if (d->timing) (void)hipEventRecord(d->ev[2 * k + 2], d->stream);
+    if (d->timing) (void)hipEventRecord(d->ev[4 * k + 2], d->stream);
+    if (p.nOutLinks) (void)hipStreamWaitEvent(d->stream, d->outEv[k], 0);
 }
 
 static void launchStep(Router::Impl* d)
 {
     Params& p = d->p;
-    if (d->timing) (void)hipEventRecord(d->ev[0], d->stream);
     for (int k = 0; k < p.maxTrials; k++) launchIteration(d, k);
-    if (p.nCold) {                                  // outfall depths final before step end
-        (void)hipEventRecord(d->tailEv, d->side);
-        (void)hipStreamWaitEvent(d->stream, d->tailEv, 0);
-    }
-    int base = 2 * p.maxTrials + 1;
+    int base = 4 * p.maxTrials;
+    if (d->timing) (void)hipEventRecord(d->ev[base], d->stream);
     if (p.P > 0) {
         hipLaunchKernelGGL(k_qual_node, dim3(d->gridN), dim3(kBlock), 0, d->stream, p);
         hipLaunchKernelGGL(k_qual_link, dim3(d->gridL), dim3(kBlock), 0, d->stream, p);
     }
-    if (d->timing) (void)hipEventRecord(d->ev[base], d->stream);
+    if (d->timing) (void)hipEventRecord(d->ev[base + 1], d->stream);
     hipLaunchKernelGGL(k_step_end, dim3(d->gridEnd), dim3(kBlock), 0, d->stream, p);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, d->stream, p);
-    if (d->timing) (void)hipEventRecord(d->ev[base + 1], d->stream);
+    if (d->timing) (void)hipEventRecord(d->ev[base + 2], d->stream);
 }
 
 int Router::init(Project& prj, int device)
@@ -1199,8 +1204,9 @@ int Router::init(Project& prj, int device)
     devName_ = std::string("hip:") + prop.gcnArchName + ":" + prop.name;
     HIPCHECK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking));
-    HIPCHECK(hipEventCreateWithFlags(&d->tailEv, hipEventDisableTiming));
     for (int k = 0; k < kMaxTrialsCap; k++) {
+        HIPCHECK(hipEventCreateWithFlags(&d->hotEv[k], hipEventDisableTiming));
+        HIPCHECK(hipEventCreateWithFlags(&d->outEv[k], hipEventDisableTiming));
         HIPCHECK(hipEventCreateWithFlags(&d->forkEv[k], hipEventDisableTiming));
         HIPCHECK(hipEventCreateWithFlags(&d->joinEv[k], hipEventDisableTiming));
     }
@@ -1257,7 +1263,7 @@ int Router::init(Project& prj, int device)
         if (net.seepRate[j] > 0.0 || (prj.opt.evapRate > 0.0 && isOpen(x.type))) f |= LF_SEEP;
         if (net.qLimit[j] > 0.0) f |= LF_QLIMIT;
         if (net.direction[j] < 0) f |= LF_DIRNEG;
-        if (net.offset1[j] > 0.0 || net.offset2[j] > 0.0 || (f & (LF_N1_OUTFALL | LF_N2_OUTFALL))) {
+        if (net.offset1[j] > 0.0 || net.offset2[j] > 0.0) {
             f |= LF_COLD;
             coldLinks.push_back(j);
         }
@@ -1477,7 +1483,7 @@ int Router::init(Project& prj, int device)
     for (auto& ev : d->ringEv) { HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming)); HIPCHECK(hipEventRecord(ev, d->stream)); }
     for (auto& ev : d->clockEv) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     HIPCHECK(hipHostMalloc((void**)&d->clockPinned, Impl::kRing * sizeof(double), hipHostMallocDefault));
-    d->ev.resize(2 * kMaxTrialsCap + 4);
+    d->ev.resize(4 * kMaxTrialsCap + 4);
     for (auto& ev : d->ev) HIPCHECK(hipEventCreate(&ev));
     for (auto& ev : d->evHot) HIPCHECK(hipEventCreate(&ev));
 
@@ -1573,8 +1579,8 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
         HIPCHECK(hipMemset(d->ctl->linkWork, 0, sizeof(work)));
         for (int k = 0; k < ran; k++) {    // early-exited iterations are not counted
             float ms1 = 0, ms2 = 0;
-            (void)hipEventElapsedTime(&ms1, d->ev[2 * k], d->evHot[k]);
-            (void)hipEventElapsedTime(&ms2, d->ev[2 * k + 1], d->ev[2 * k + 2]);
+            (void)hipEventElapsedTime(&ms1, d->ev[4 * k], d->evHot[k]);
+            (void)hipEventElapsedTime(&ms2, d->ev[4 * k + 1], d->ev[4 * k + 2]);
             int c = (k == 0) ? 0 : 4;
             d->kms[c] += ms1; d->kcnt[c]++;
             if (k == 0) d->kbytesSum[0] += d->kbytes[0];
@@ -1586,10 +1592,10 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
             d->kms[1] += ms2; d->kcnt[1]++;
             d->kbytesSum[1] += d->kbytes[1];
         }
-        int base = 2 * p.maxTrials + 1;
+        int base = 4 * p.maxTrials;
         float ms3 = 0, msq = 0;
-        (void)hipEventElapsedTime(&ms3, d->ev[base], d->ev[base + 1]);
-        (void)hipEventElapsedTime(&msq, d->ev[2 * p.maxTrials], d->ev[base]);
+        (void)hipEventElapsedTime(&ms3, d->ev[base + 1], d->ev[base + 2]);
+        (void)hipEventElapsedTime(&msq, d->ev[base], d->ev[base + 1]);
         d->kms[2] += ms3; d->kcnt[2]++;
         d->kbytesSum[2] += d->kbytes[2];
         if (p.P) { d->kms[3] += msq; d->kcnt[3]++; d->kbytesSum[3] += d->kbytes[3]; }
