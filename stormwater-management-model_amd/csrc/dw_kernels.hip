@@ -143,10 +143,13 @@ struct Params {
 // ===========================================================================
 //  device helpers
 // ===========================================================================
+// kFast: every streaming conduit is CIRCULAR and the surcharge method is not
+// SLOT (host-checked); the shape switches and the slot branch then fold away.
+template <bool kFast = false>
 __device__ __forceinline__ Geom loadGeom(const Params& p, int j, uint32_t f)
 {
     Geom g;
-    g.type = (int)(f & LF_XTYPE);
+    g.type = kFast ? (int)G_CIRCULAR : (int)(f & LF_XTYPE);
     g.yFull = p.yFull[j];
     g.wMax = p.wMax[j];
     g.aFull = p.aFull[j];
@@ -166,17 +169,20 @@ __device__ __forceinline__ Geom loadGeom(const Params& p, int j, uint32_t f)
 }
 
 // dwflow.c:575-588
+template <bool kFast = false>
 __device__ __forceinline__ double slotWidth(const Params& p, const Geom& x, double y)
 {
+    if (kFast) return 0.0;
     double yNorm = y / x.yFull;
     if (p.surchargeMethod != SUR_SLOT || isOpen(x.type) || yNorm < p.crownCutoff) return 0.0;
     if (yNorm > 1.78) return 0.01 * x.wMax;
     return x.wMax * 0.5423 * exp(-pow(yNorm, 2.4));
 }
 // dwflow.c:592-605
+template <bool kFast = false>
 __device__ __forceinline__ double widthAt(const Params& p, const Geom& x, double y, const double* ct)
 {
-    double wSlot = slotWidth(p, x, y);
+    double wSlot = slotWidth<kFast>(p, x, y);
     if (wSlot > 0.0) return wSlot;
     if (y / x.yFull >= p.crownCutoff && !isOpen(x.type)) y = p.crownCutoff * x.yFull;
     return getWofY(x, y, ct);
@@ -291,7 +297,7 @@ __device__ __forceinline__ int flowClassOf(const Params& p, int j, const Geom& x
 }
 
 // dwflow.c:57-293 -- one conduit, one Picard iteration.
-template <bool kFirst, bool kCold>
+template <bool kFirst, bool kCold, bool kFast = false>
 __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, int2 nn, int steps,
                                             double dt, const double* ct)
 {
@@ -299,7 +305,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     int n1 = nn.x, n2 = nn.y;
     const double off1 = kCold ? p.off1[j] : 0.0;     // hot links: both offsets are 0
     const double off2 = kCold ? p.off2[j] : 0.0;
-    Geom x = loadGeom(p, j, f);
+    Geom x = loadGeom<kFast>(p, j, f);
     double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
 
     // iteration 0: link_setOldHydState (link.c:564-583), a2 <- a1 (dynwave.c:292)
@@ -332,7 +338,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     double y2 = h2 - z2;
     y1 = gmax(y1, 0.0001);
     y2 = gmax(y2, 0.0001);
-    if (p.surchargeMethod != SUR_SLOT) {
+    if (kFast || p.surchargeMethod != SUR_SLOT) {
         y1 = gmin(y1, x.yFull);
         y2 = gmin(y2, x.yFull);
     }
@@ -376,9 +382,9 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         } else {
             dMid = 0.5 * (d1 + d2);
             if (dMid < 0.0001) dMid = 0.0001;
-            w1 = widthAt(p, x, d1, ct);
-            w2 = widthAt(p, x, d2, ct);
-            wMid = widthAt(p, x, dMid, ct);
+            w1 = widthAt<kFast>(p, x, d1, ct);
+            w2 = widthAt<kFast>(p, x, d2, ct);
+            wMid = widthAt<kFast>(p, x, dMid, ct);
             switch (fc) {
             case F_SUBCRIT:                                  // dwflow.c:460-472
                 sa1 = (w1 + wMid) * length / 4.;
@@ -406,13 +412,13 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     p.sa1[j] = sa1;
     p.sa2[j] = sa2;
 
-    double wSlot = slotWidth(p, x, y1);
+    double wSlot = slotWidth<kFast>(p, x, y1);
     double a1 = areaAt(x, y1, wSlot, ct);
     double r1 = hydRadAt(x, y1, ct);
-    wSlot = slotWidth(p, x, y2);
+    wSlot = slotWidth<kFast>(p, x, y2);
     double a2 = areaAt(x, y2, wSlot, ct);
     double yMid = 0.5 * (y1 + y2);
-    wSlot = slotWidth(p, x, yMid);
+    wSlot = slotWidth<kFast>(p, x, yMid);
     double aMid = areaAt(x, yMid, wSlot, ct);
     double rMid = hydRadAt(x, yMid, ct);
     bool isFull = (y1 >= x.yFull && y2 >= x.yFull);
@@ -558,7 +564,7 @@ __device__ __forceinline__ void stageTables(double* ct, const double* g)
 // end), one thread per conduit.  No calls, no root finders.
 // kWaves: minimum waves per SIMD the register allocator must allow (1 = no
 // constraint); selected at start-up (SWMM5_LINK_WAVES, default kLinkWavesDefault)
-template <bool kFirst, int kWaves>
+template <bool kFirst, int kWaves, bool kFast>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves)))
 void k_link(Params p, int k)
 {
@@ -572,7 +578,7 @@ void k_link(Params p, int k)
         if (f & LF_COLD) continue;
         int2 nn = p.lnodes[j];
         if (k >= 2 && p.conv[nn.x] && p.conv[nn.y]) continue;   // findBypassedLinks dynwave.c:335-345
-        conduitFlow<kFirst, false>(p, j, f, nn, k, dt, ct);
+        conduitFlow<kFirst, false, kFast>(p, j, f, nn, k, dt, ct);
         work++;
     }
     if (p.countWork) {                                     // measurement only (eager launches)
@@ -627,47 +633,43 @@ __global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
     }
 }
 
-// link_setOutfallDepth for every conduit with an outfall end (findNodeDepths,
-// dynwave.c:605): runs on the side branch once the iteration's link flows are
-// final, concurrently with k_node (which never reads an outfall's depth); the
-// next iteration's link kernels wait for it.  The outfall is never
-// "converged" (dynwave.c:281, 340), so its link is never bypassed and the
-// depth is refreshed every iteration, as in the reference.
-template <bool kFirst>
-__global__ __launch_bounds__(kBlock) void k_outfall(Params p, int k)
-{
-    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
-    __shared__ double ct[5 * SWX_CIRC_N];
-    stageTables(ct, p.gTables);
-    for (int c = blockIdx.x * kBlock + threadIdx.x; c < p.nOutLinks; c += gridDim.x * kBlock) {
-        int j = p.outLinks[c];
-        uint32_t f = p.lflags[j];
-        int2 nn = p.lnodes[j];
-        int i = (f & LF_N2_OUTFALL) ? nn.y : nn.x;         // link.c:743-753 (node2 first)
-        if (kFirst) p.nOldDepth[i] = p.nNewDepth[i];        // node_setOldHydState before the update
-        p.nNewDepth[i] = outfallDepth(p, i, p.nflags[i], j, f, ct);
-    }
-}
-
 template <bool kFirst>
 __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
 {
     if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
+    // prologue: outfall depths (link_setOutfallDepth, findNodeDepths
+    // dynwave.c:605) from this iteration's link flows.  Only the outfall's
+    // single link reads that depth (next iteration), and this kernel never
+    // reads an outfall's depth, so it can run alongside the node updates; it
+    // goes first because it is the long (iterative) part of the launch.  The
+    // outfall is never "converged" (dynwave.c:281, 340): its link is never
+    // bypassed and the depth is refreshed every iteration, as in the reference.
+    if (blockIdx.x * kBlock < p.nOutLinks) {
+        __shared__ double ct[5 * SWX_CIRC_N];
+        stageTables(ct, p.gTables);
+        for (int c = blockIdx.x * kBlock + threadIdx.x; c < p.nOutLinks; c += gridDim.x * kBlock) {
+            int j = p.outLinks[c];
+            uint32_t f = p.lflags[j];
+            int2 nn = p.lnodes[j];
+            int o = (f & LF_N2_OUTFALL) ? nn.y : nn.x;    // link.c:743-753 (node2 first)
+            if (kFirst) p.nOldDepth[o] = p.nNewDepth[o];   // node_setOldHydState before the update
+            p.nNewDepth[o] = outfallDepth(p, o, p.nflags[o], j, f, ct);
+        }
+    }
     const double dt = p.ctl->dt;
     const double omega = 0.5;
     bool anyUnconv = false;
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
         uint32_t nf = p.nflags[i];
         int type = (int)(nf & NF_TYPE);
-        // an outfall's depth may be being written by k_outfall (side branch):
-        // it is not read here
+        // an outfall's depth is written by the prologue above: not read here
         double yLast = (type == OUTFALL) ? 0.0 : p.nNewDepth[i];
         double yOld, lat;
         if (kFirst) {
             // routing.c:328-332, node.c:293-304, 325-341 -- step-begin rotation
             double inflowPrev = p.inflow[i], outflowPrev = p.outflow[i];
             yOld = yLast;
-            if (type != OUTFALL) p.nOldDepth[i] = yOld;   // outfalls: rotated by k_link_cold
+            if (type != OUTFALL) p.nOldDepth[i] = yOld;   // outfalls: rotated in the prologue
             p.nOldVolume[i] = p.nNewVolume[i];
             p.oldFlowInflow[i] = inflowPrev;
             p.oldNetInflow[i] = inflowPrev - outflowPrev;
@@ -715,7 +717,7 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
         }
         p.inflow[i] = inflow;
         p.outflow[i] = outflow;
-        if (type == OUTFALL) continue;                     // depth set by k_link_cold
+        if (type == OUTFALL) continue;                     // depth set by the prologue
         // setNodeDepth (dynwave.c:636-762)
         bool isPonded = (canPond && yLast > fullDepth);
         double yCrown = p.yCrown[i];
@@ -1045,12 +1047,12 @@ struct Router::Impl {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;      // fork/join branch for the cold conduits
     hipEvent_t forkEv[kMaxTrialsCap] = {}, joinEv[kMaxTrialsCap] = {};
-    hipEvent_t hotEv[kMaxTrialsCap] = {}, outEv[kMaxTrialsCap] = {};
     hipGraphExec_t graph = nullptr;
     bool useGraph = true;
     bool timing = false;
-    int gridL = 1, gridN = 1, gridEnd = 1, gridC = 1, gridO = 1;
+    int gridL = 1, gridN = 1, gridEnd = 1, gridC = 1;
     int linkWaves = kLinkWavesDefault;
+    bool fastLinks = false;          // all streaming conduits circular, no SLOT
     std::vector<void*> allocs;
     double* latBase = nullptr;       // constant lateral inflows
     double* qualBase = nullptr;
@@ -1059,13 +1061,19 @@ struct Router::Impl {
     StepCtl* ctl = nullptr;
     StepCtl* hostCtl = nullptr;      // pinned
     bool constantInflow = true;
-    std::vector<hipEvent_t> ev;      // timing events
+    struct TimingSlot {               // one timed step's events + readback
+        std::vector<hipEvent_t> ev, evHot;
+        unsigned long long* pinned = nullptr;   // [0] Picard iterations run, [1..] conduits updated
+    };
+    std::vector<TimingSlot> tslots;
+    int tUsed = 0;
+    hipEvent_t* curEv = nullptr;     // event set of the step being launched
+    hipEvent_t* curHot = nullptr;
     static constexpr int kClasses = 5;
     double kms[kClasses] = {};
     long long kcnt[kClasses] = {};
     double kbytes[kClasses] = {};     // byte model per launch (class 4: per updated conduit)
     double kbytesSum[kClasses] = {};  // algorithmic bytes of the timed launches
-    hipEvent_t evHot[kMaxTrialsCap] = {};
     double nHot = 0, nColdD = 0;
     double workSum = 0;               // conduits updated in timed iterations >= 1
     int nE = 0;
@@ -1086,8 +1094,11 @@ Router::~Router()
 {
     if (d_) {
         if (d_->graph) (void)hipGraphExecDestroy(d_->graph);
-        for (auto e : d_->ev) (void)hipEventDestroy(e);
-        for (auto e : d_->evHot) if (e) (void)hipEventDestroy(e);
+        for (auto& t : d_->tslots) {
+            for (auto e : t.ev) (void)hipEventDestroy(e);
+            for (auto e : t.evHot) (void)hipEventDestroy(e);
+            if (t.pinned) (void)hipHostFree(t.pinned);
+        }
         for (void* a : d_->allocs) (void)hipFree(a);
         if (d_->hostPinned) (void)hipHostFree(d_->hostPinned);
         if (d_->hostCtl) (void)hipHostFree(d_->hostCtl);
@@ -1097,10 +1108,6 @@ Router::~Router()
         for (int k = 0; k < kMaxTrialsCap; k++) {
             if (d_->forkEv[k]) (void)hipEventDestroy(d_->forkEv[k]);
             if (d_->joinEv[k]) (void)hipEventDestroy(d_->joinEv[k]);
-        }
-        for (int k = 0; k < kMaxTrialsCap; k++) {
-            if (d_->hotEv[k]) (void)hipEventDestroy(d_->hotEv[k]);
-            if (d_->outEv[k]) (void)hipEventDestroy(d_->outEv[k]);
         }
         if (d_->side) (void)hipStreamDestroy(d_->side);
         if (d_->stream) (void)hipStreamDestroy(d_->stream);
@@ -1118,26 +1125,31 @@ static T* devAlloc(Router::Impl* d, size_t n, hipError_t* err)
 }
 
 typedef void (*LinkKernelFn)(Params, int);
-static LinkKernelFn linkKernel(bool first, int waves)
+template <bool kFast>
+static LinkKernelFn linkKernelT(bool first, int waves)
 {
     switch (waves) {
-    case 3: return first ? k_link<true, 3> : k_link<false, 3>;
-    case 4: return first ? k_link<true, 4> : k_link<false, 4>;
-    case 5: return first ? k_link<true, 5> : k_link<false, 5>;
-    default: return first ? k_link<true, 1> : k_link<false, 1>;
+    case 3: return first ? k_link<true, 3, kFast> : k_link<false, 3, kFast>;
+    case 4: return first ? k_link<true, 4, kFast> : k_link<false, 4, kFast>;
+    default: return first ? k_link<true, 1, kFast> : k_link<false, 1, kFast>;
     }
 }
+static LinkKernelFn linkKernel(bool first, int waves, bool fast)
+{
+    return fast ? linkKernelT<true>(first, waves) : linkKernelT<false>(first, waves);
+}
 
-// One Picard iteration k.  Main stream (d->stream) and side stream (d->side),
-// joined into one graph by events:
-//   main:  [fork k] k_link(k) [hot k] ─wait join k─ k_node(k) ─wait out k─►
-//   side:  wait fork k ─ k_link_cold(k) [join k] ─wait hot k─ k_outfall(k) [out k]
-// k_link_cold (offset conduits) overlaps the streaming kernel; k_outfall
-// overlaps k_node; iteration k+1 starts after both.
+// One Picard iteration k.  Conduits with an invert offset (k_link_cold) run on
+// a side stream, concurrently with the streaming kernel, and are joined before
+// the node update; without such conduits the iteration is two kernels on one
+// stream (a cross-queue dependency costs ~5-10 us on MI355X, more than the
+// cold work it would hide):
+//   main:  [fork k] k_link(k) ─wait join k─ k_node(k)
+//   side:  wait fork k ─ k_link_cold(k) ─[join k]
 static void launchIteration(Router::Impl* d, int k)
 {
     Params& p = d->p;
-    if (d->timing) (void)hipEventRecord(d->ev[4 * k], d->stream);
+    if (d->timing) (void)hipEventRecord(d->curEv[4 * k], d->stream);
     if (p.nCold) {
         (void)hipEventRecord(d->forkEv[k], d->stream);
         (void)hipStreamWaitEvent(d->side, d->forkEv[k], 0);
@@ -1147,26 +1159,16 @@ static void launchIteration(Router::Impl* d, int k)
             hipLaunchKernelGGL(k_link_cold<false>, dim3(d->gridC), dim3(kBlock), 0, d->side, p, k);
         (void)hipEventRecord(d->joinEv[k], d->side);
     }
-    hipLaunchKernelGGL(linkKernel(k == 0, d->linkWaves), dim3(d->gridL), dim3(kBlock), 0, d->stream, p, k);
-    if (d->timing) (void)hipEventRecord(d->evHot[k], d->stream);
-    if (p.nOutLinks) {
-        (void)hipEventRecord(d->hotEv[k], d->stream);
-        (void)hipStreamWaitEvent(d->side, d->hotEv[k], 0);
-        if (k == 0)
-            hipLaunchKernelGGL(k_outfall<true>, dim3(d->gridO), dim3(kBlock), 0, d->side, p, k);
-        else
-            hipLaunchKernelGGL(k_outfall<false>, dim3(d->gridO), dim3(kBlock), 0, d->side, p, k);
-        (void)hipEventRecord(d->outEv[k], d->side);
-    }
+    hipLaunchKernelGGL(linkKernel(k == 0, d->linkWaves, d->fastLinks), dim3(d->gridL), dim3(kBlock), 0, d->stream, p, k);
+    if (d->timing) (void)hipEventRecord(d->curHot[k], d->stream);
     if (p.nCold) (void)hipStreamWaitEvent(d->stream, d->joinEv[k], 0);
-    if (d->timing) (void)hipEventRecord(d->ev[4 * k + 1], d->stream);
+    if (d->timing) (void)hipEventRecord(d->curEv[4 * k + 1], d->stream);
     if (k == 0) {
         hipLaunchKernelGGL(k_node<true>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
     } else {
         hipLaunchKernelGGL(k_node<false>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
     }
-    if (d->timing) (void)hipEventRecord(d->ev[4 * k + 2], d->stream);
-    if (p.nOutLinks) (void)hipStreamWaitEvent(d->stream, d->outEv[k], 0);
+    if (d->timing) (void)hipEventRecord(d->curEv[4 * k + 2], d->stream);
 }
 
 static void launchStep(Router::Impl* d)
@@ -1174,15 +1176,15 @@ static void launchStep(Router::Impl* d)
     Params& p = d->p;
     for (int k = 0; k < p.maxTrials; k++) launchIteration(d, k);
     int base = 4 * p.maxTrials;
-    if (d->timing) (void)hipEventRecord(d->ev[base], d->stream);
+    if (d->timing) (void)hipEventRecord(d->curEv[base], d->stream);
     if (p.P > 0) {
         hipLaunchKernelGGL(k_qual_node, dim3(d->gridN), dim3(kBlock), 0, d->stream, p);
         hipLaunchKernelGGL(k_qual_link, dim3(d->gridL), dim3(kBlock), 0, d->stream, p);
     }
-    if (d->timing) (void)hipEventRecord(d->ev[base + 1], d->stream);
+    if (d->timing) (void)hipEventRecord(d->curEv[base + 1], d->stream);
     hipLaunchKernelGGL(k_step_end, dim3(d->gridEnd), dim3(kBlock), 0, d->stream, p);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, d->stream, p);
-    if (d->timing) (void)hipEventRecord(d->ev[base + 2], d->stream);
+    if (d->timing) (void)hipEventRecord(d->curEv[base + 2], d->stream);
 }
 
 int Router::init(Project& prj, int device)
@@ -1205,8 +1207,6 @@ int Router::init(Project& prj, int device)
     HIPCHECK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking));
     for (int k = 0; k < kMaxTrialsCap; k++) {
-        HIPCHECK(hipEventCreateWithFlags(&d->hotEv[k], hipEventDisableTiming));
-        HIPCHECK(hipEventCreateWithFlags(&d->outEv[k], hipEventDisableTiming));
         HIPCHECK(hipEventCreateWithFlags(&d->forkEv[k], hipEventDisableTiming));
         HIPCHECK(hipEventCreateWithFlags(&d->joinEv[k], hipEventDisableTiming));
     }
@@ -1437,6 +1437,13 @@ int Router::init(Project& prj, int device)
         UPD(tmp, t, t.size()); p.gTables = tmp;
     }
     if (const char* w = getenv("SWMM5_LINK_WAVES")) d->linkWaves = atoi(w);
+    {
+        bool fast = prj.opt.surchargeMethod != SUR_SLOT;
+        for (int j = 0; j < nL && fast; j++)
+            if (!(lflags[j] & LF_COLD) && (lflags[j] & LF_XTYPE) != G_CIRCULAR) fast = false;
+        const char* g = getenv("SWMM5_GENERIC_LINKS");
+        d->fastLinks = fast && !(g && atoi(g));
+    }
     int maxBlocks = 8 * std::max(prop.multiProcessorCount, 1);
     // streaming kernels: one resident wave of workgroups (grid-stride loops),
     // so early-exited Picard iterations dispatch few workgroups
@@ -1448,10 +1455,9 @@ int Router::init(Project& prj, int device)
         if (const char* g = getenv("SWMM5_GRID_FACTOR")) cap = (int)(cap * atof(g));
         return std::max(1, std::min((n + kBlock - 1) / kBlock, std::max(cap, 1)));
     };
-    d->gridL = resident((const void*)linkKernel(false, d->linkWaves), nL);
+    d->gridL = resident((const void*)linkKernel(false, d->linkWaves, d->fastLinks), nL);
     d->gridN = resident((const void*)k_node<false>, nN);
     d->gridC = std::max(1, std::min((p.nCold + kBlock - 1) / kBlock, maxBlocks));
-    d->gridO = std::max(1, std::min((p.nOutLinks + kBlock - 1) / kBlock, maxBlocks));
     d->gridEnd = std::max(1, std::min((std::max(nN, nL) + kBlock - 1) / kBlock, 2 * prop.multiProcessorCount));
     p.nBlocksEnd = d->gridEnd;
     p.partials = devAlloc<double>(d, (size_t)d->gridEnd * kNumPartials, &e);
@@ -1483,9 +1489,6 @@ int Router::init(Project& prj, int device)
     for (auto& ev : d->ringEv) { HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming)); HIPCHECK(hipEventRecord(ev, d->stream)); }
     for (auto& ev : d->clockEv) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     HIPCHECK(hipHostMalloc((void**)&d->clockPinned, Impl::kRing * sizeof(double), hipHostMallocDefault));
-    d->ev.resize(4 * kMaxTrialsCap + 4);
-    for (auto& ev : d->ev) HIPCHECK(hipEventCreate(&ev));
-    for (auto& ev : d->evHot) HIPCHECK(hipEventCreate(&ev));
 
     // algorithmic bytes per launch (DESIGN.md byte model; per kernel class)
     {
@@ -1531,6 +1534,42 @@ int Router::init(Project& prj, int device)
 #undef UPI
 }
 
+// Accumulate the per-kernel-class times of all pending timed steps.
+static void flushTiming(Router::Impl* d)
+{
+    if (!d->tUsed) return;
+    (void)hipStreamSynchronize(d->stream);
+    const Params& p = d->p;
+    for (int s = 0; s < d->tUsed; s++) {
+        Router::Impl::TimingSlot& t = d->tslots[s];
+        int ran = (int)(t.pinned[0] & 0xFFFFFFFFull);
+        const unsigned long long* work = t.pinned + 1;
+        for (int k = 0; k < ran; k++) {    // early-exited iterations are not counted
+            float ms1 = 0, ms2 = 0;
+            (void)hipEventElapsedTime(&ms1, t.ev[4 * k], t.evHot[k]);
+            (void)hipEventElapsedTime(&ms2, t.ev[4 * k + 1], t.ev[4 * k + 2]);
+            int c = (k == 0) ? 0 : 4;
+            d->kms[c] += ms1; d->kcnt[c]++;
+            if (k == 0) d->kbytesSum[0] += d->kbytes[0];
+            else {
+                double w = (double)work[k];
+                d->workSum += w;
+                d->kbytesSum[4] += w * d->kbytes[4] + (d->nHot - w) * 20.0 + d->nColdD * 4.0;
+            }
+            d->kms[1] += ms2; d->kcnt[1]++;
+            d->kbytesSum[1] += d->kbytes[1];
+        }
+        int base = 4 * p.maxTrials;
+        float ms3 = 0, msq = 0;
+        (void)hipEventElapsedTime(&ms3, t.ev[base + 1], t.ev[base + 2]);
+        (void)hipEventElapsedTime(&msq, t.ev[base], t.ev[base + 1]);
+        d->kms[2] += ms3; d->kcnt[2]++;
+        d->kbytesSum[2] += d->kbytes[2];
+        if (p.P) { d->kms[3] += msq; d->kcnt[3]++; d->kbytesSum[3] += d->kbytes[3]; }
+    }
+    d->tUsed = 0;
+}
+
 int Router::step(const double* latFlow, const double* qualLoad, const double tot[3])
 {
     auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
@@ -1570,35 +1609,28 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
         d->clockLast = s;
     }
     if (d->timing) {
-        launchStep(d);
-        HIPCHECK(hipStreamSynchronize(d->stream));
-        int ran = 0;
-        HIPCHECK(hipMemcpy(&ran, &d->ctl->lastSteps, sizeof(int), hipMemcpyDeviceToHost));
-        unsigned long long work[kMaxTrialsCap];
-        HIPCHECK(hipMemcpy(work, d->ctl->linkWork, sizeof(work), hipMemcpyDeviceToHost));
-        HIPCHECK(hipMemset(d->ctl->linkWork, 0, sizeof(work)));
-        for (int k = 0; k < ran; k++) {    // early-exited iterations are not counted
-            float ms1 = 0, ms2 = 0;
-            (void)hipEventElapsedTime(&ms1, d->ev[4 * k], d->evHot[k]);
-            (void)hipEventElapsedTime(&ms2, d->ev[4 * k + 1], d->ev[4 * k + 2]);
-            int c = (k == 0) ? 0 : 4;
-            d->kms[c] += ms1; d->kcnt[c]++;
-            if (k == 0) d->kbytesSum[0] += d->kbytes[0];
-            else {
-                double w = (double)work[k];
-                d->workSum += w;
-                d->kbytesSum[4] += w * d->kbytes[4] + (d->nHot - w) * 20.0 + d->nColdD * 4.0;
-            }
-            d->kms[1] += ms2; d->kcnt[1]++;
-            d->kbytesSum[1] += d->kbytes[1];
+        // eager launches with a private event set per step; nothing synchronises
+        // until the results are read (flushTiming), so steps run back to back
+        if (d->tUsed == (int)d->tslots.size() && d->tslots.size() >= 256) flushTiming(d);
+        if (d->tUsed == (int)d->tslots.size()) {
+            d->tslots.emplace_back();
+            Impl::TimingSlot& t = d->tslots.back();
+            t.ev.resize(4 * kMaxTrialsCap + 4);
+            t.evHot.resize(kMaxTrialsCap);
+            for (auto& ev : t.ev) HIPCHECK(hipEventCreate(&ev));
+            for (auto& ev : t.evHot) HIPCHECK(hipEventCreate(&ev));
+            HIPCHECK(hipHostMalloc((void**)&t.pinned, (1 + kMaxTrialsCap) * sizeof(unsigned long long),
+                                   hipHostMallocDefault));
         }
-        int base = 4 * p.maxTrials;
-        float ms3 = 0, msq = 0;
-        (void)hipEventElapsedTime(&ms3, d->ev[base + 1], d->ev[base + 2]);
-        (void)hipEventElapsedTime(&msq, d->ev[base], d->ev[base + 1]);
-        d->kms[2] += ms3; d->kcnt[2]++;
-        d->kbytesSum[2] += d->kbytes[2];
-        if (p.P) { d->kms[3] += msq; d->kcnt[3]++; d->kbytesSum[3] += d->kbytes[3]; }
+        Impl::TimingSlot& t = d->tslots[d->tUsed++];
+        d->curEv = t.ev.data();
+        d->curHot = t.evHot.data();
+        launchStep(d);
+        HIPCHECK(hipMemcpyAsync(t.pinned, &d->ctl->lastSteps, sizeof(int), hipMemcpyDeviceToHost,
+                                d->stream));
+        HIPCHECK(hipMemcpyAsync(t.pinned + 1, d->ctl->linkWork, kMaxTrialsCap * sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost, d->stream));
+        HIPCHECK(hipMemsetAsync(d->ctl->linkWork, 0, kMaxTrialsCap * sizeof(unsigned long long), d->stream));
     } else {
         HIPCHECK(hipGraphLaunch(d->graph, d->stream));
     }
@@ -1779,6 +1811,7 @@ void Router::stepTotals(double out[6])
 
 void Router::setTiming(bool on)
 {
+    flushTiming(d_);
     d_->timing = on;
     d_->p.countWork = on ? 1 : 0;                  // eager launches only; the graph keeps 0
     for (int k = 0; k < Impl::kClasses; k++) { d_->kms[k] = 0; d_->kcnt[k] = 0; d_->kbytesSum[k] = 0; }
@@ -1787,12 +1820,14 @@ void Router::setTiming(bool on)
 
 void Router::timedWork(double* updated, double* hot)
 {
+    flushTiming(d_);
     *updated = d_->workSum;
     *hot = d_->nHot;
 }
 
 int Router::kernelTimes(double* out, int n)
 {
+    flushTiming(d_);
     int m = std::min(n / 2, (int)Impl::kClasses);
     for (int k = 0; k < m; k++) {
         out[2 * k] = (double)d_->kcnt[k];
@@ -1803,6 +1838,7 @@ int Router::kernelTimes(double* out, int n)
 
 int Router::kernelBytes(double* out, int n)
 {
+    flushTiming(d_);
     // average algorithmic bytes per timed launch (byte model when nothing was timed)
     int m = std::min(n, (int)Impl::kClasses);
     for (int k = 0; k < m; k++) {
