@@ -49,6 +49,7 @@ namespace swx {
 constexpr int kBlock = 256;
 constexpr int kMaxTrialsCap = 32;
 constexpr int kNumPartials = 8;
+constexpr int kDtRing = 4;          // host-mapped per-step dt ring (k_finalize -> host)
 constexpr int kLinkWavesDefault = 3;   // measured best on MI355X   // per-block partial sums written by k_step_end
 
 // ---- packed per-link flags -------------------------------------------------
@@ -134,6 +135,7 @@ struct Params {
     double* partials;             // [nBlocksEnd][kNumPartials]
     int nBlocksEnd;
     int countWork;                // timing mode: count updated conduits per iteration
+    double* hostDt;               // host-mapped ring of per-step dt (Router::launchedDt)
     int nCold, nOutLinks;
     const int* coldLinks;         // LF_COLD conduits, ascending
     const int* outLinks;          // conduits with an outfall end, ascending
@@ -1037,6 +1039,10 @@ __global__ void k_finalize(Params p)
         dtn = (dtn >= 1. / 1000.0) ? dtn : 1. / 1000.0;
     }
     c->dt = dtn;
+    // next step's dt straight into host memory: the host clock advances
+    // without a copy command in the step (totalSteps = index of that step)
+    p.hostDt[c->totalSteps % kDtRing] = dtn;
+    __threadfence_system();
 }
 
 // ===========================================================================
@@ -1078,11 +1084,11 @@ struct Router::Impl {
     double workSum = 0;               // conduits updated in timed iterations >= 1
     int nE = 0;
     bool tableShapes = true;
-    static constexpr int kRing = 4;
+    static constexpr int kRing = kDtRing;
     hipEvent_t ringEv[kRing] = {};
-    hipEvent_t clockEv[kRing] = {};
-    double* clockPinned = nullptr;   // kRing slots: dt of each launched step
-    int clockNext = 0, clockLast = 0;
+    hipEvent_t clockEv[kRing] = {};  // completion of step n -> clockEv[n % kRing]
+    double* hostDt = nullptr;        // host-mapped ring: dt of step n in slot n % kRing
+    long long launched = 0;          // steps passed to step()
     int ringNext = 0;
     size_t slotDoubles = 0;
     double lastDtHost = 0.0;
@@ -1102,7 +1108,7 @@ Router::~Router()
         for (void* a : d_->allocs) (void)hipFree(a);
         if (d_->hostPinned) (void)hipHostFree(d_->hostPinned);
         if (d_->hostCtl) (void)hipHostFree(d_->hostCtl);
-        if (d_->clockPinned) (void)hipHostFree(d_->clockPinned);
+        if (d_->hostDt) (void)hipHostFree(d_->hostDt);
         for (auto e : d_->clockEv) if (e) (void)hipEventDestroy(e);
         for (auto e : d_->ringEv) if (e) (void)hipEventDestroy(e);
         for (int k = 0; k < kMaxTrialsCap; k++) {
@@ -1488,7 +1494,14 @@ int Router::init(Project& prj, int device)
     HIPCHECK(hipHostMalloc((void**)&d->hostPinned, d->pinnedSize * sizeof(double), hipHostMallocDefault));
     for (auto& ev : d->ringEv) { HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming)); HIPCHECK(hipEventRecord(ev, d->stream)); }
     for (auto& ev : d->clockEv) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    HIPCHECK(hipHostMalloc((void**)&d->clockPinned, Impl::kRing * sizeof(double), hipHostMallocDefault));
+    HIPCHECK(hipHostMalloc((void**)&d->hostDt, Impl::kRing * sizeof(double),
+                           hipHostMallocMapped | hipHostMallocCoherent));
+    {
+        void* dp = nullptr;
+        HIPCHECK(hipHostGetDevicePointer(&dp, d->hostDt, 0));
+        p.hostDt = (double*)dp;
+        for (int r = 0; r < Impl::kRing; r++) d->hostDt[r] = d->hostCtl->dt;
+    }
 
     // algorithmic bytes per launch (DESIGN.md byte model; per kernel class)
     {
@@ -1597,17 +1610,6 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
                                 hipMemcpyHostToDevice, d->stream));
         HIPCHECK(hipEventRecord(d->ringEv[s], d->stream));
     }
-    // step length this step will use (written by the previous step's
-    // k_finalize): copied behind the previous step so the host clock can be
-    // advanced without draining the queue (see Router::launchedDt)
-    {
-        int s = d->clockNext;
-        d->clockNext = (d->clockNext + 1) % Impl::kRing;
-        HIPCHECK(hipMemcpyAsync(d->clockPinned + s, &d->ctl->dt, sizeof(double),
-                                hipMemcpyDeviceToHost, d->stream));
-        HIPCHECK(hipEventRecord(d->clockEv[s], d->stream));
-        d->clockLast = s;
-    }
     if (d->timing) {
         // eager launches with a private event set per step; nothing synchronises
         // until the results are read (flushTiming), so steps run back to back
@@ -1634,6 +1636,10 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
     } else {
         HIPCHECK(hipGraphLaunch(d->graph, d->stream));
     }
+    // completion marker of this step: k_finalize has by then written the next
+    // step's dt into the host-mapped ring (Router::launchedDt)
+    HIPCHECK(hipEventRecord(d->clockEv[d->launched % Impl::kRing], d->stream));
+    d->launched++;
     return 0;
 }
 
@@ -1641,8 +1647,11 @@ int Router::launchedDt(double* dt)
 {
     auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
     Impl* d = d_;
-    HIPCHECK(hipEventSynchronize(d->clockEv[d->clockLast]));
-    *dt = d->clockPinned[d->clockLast];
+    // the step just launched is L-1; its dt was written by step L-2's
+    // k_finalize into slot (L-1) % kRing (slot 0 holds the initial step)
+    long long L = d->launched;
+    if (L >= 2) HIPCHECK(hipEventSynchronize(d->clockEv[(L - 2) % Impl::kRing]));
+    *dt = d->hostDt[(L - 1) % Impl::kRing];
     return 0;
 }
 
@@ -1673,6 +1682,7 @@ int Router::setDuration(double msec)
     }
     d->hostCtl->dt = dtn;
     HIPCHECK(hipMemcpy(d->ctl, d->hostCtl, sizeof(StepCtl), hipMemcpyHostToDevice));
+    d->hostDt[d->launched % Impl::kRing] = dtn;      // the next step's slot
     return 0;
 }
 
