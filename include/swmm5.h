@@ -14,7 +14,7 @@
  *   swmm_step   swmm5.c:410   one routing step; *elapsedTime in days, 0 at end
  *   swmm_stride swmm5.c:466   advance strideStep seconds
  *   swmm_end    swmm5.c:618   final records, mass balance, statistics
- *   swmm_report swmm5.c:664   write report file
+ *   swmm_report swmm5.c:655   write report file
  *   swmm_close  swmm5.c:682   release everything
  * Error codes are the reference's (src/solver/error.h); a set error code is
  * sticky and returned by every later call, as in the reference.

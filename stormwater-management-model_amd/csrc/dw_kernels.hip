@@ -583,10 +583,18 @@ void k_link(Params p, int k)
         conduitFlow<kFirst, false, kFast>(p, j, f, nn, k, dt, ct);
         work++;
     }
-    if (p.countWork) {                                     // measurement only (eager launches)
+    // measurement only (eager timing launches, iterations >= 2 where links can
+    // be bypassed): one atomic per workgroup after an LDS reduction
+    if (k >= 2 && p.countWork) {
+        __shared__ int wsum[kBlock / 64];
         for (int off = 32; off > 0; off >>= 1) work += __shfl_down(work, off, 64);
-        if ((threadIdx.x & 63) == 0 && work)
-            atomicAdd(&p.ctl->linkWork[k], (unsigned long long)work);
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = work;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int t = 0;
+            for (int w = 0; w < kBlock / 64; w++) t += wsum[w];
+            if (t) atomicAdd(&p.ctl->linkWork[k], (unsigned long long)t);
+        }
     }
 }
 
@@ -1565,7 +1573,7 @@ static void flushTiming(Router::Impl* d)
             d->kms[c] += ms1; d->kcnt[c]++;
             if (k == 0) d->kbytesSum[0] += d->kbytes[0];
             else {
-                double w = (double)work[k];
+                double w = (k >= 2) ? (double)work[k] : d->nHot;   // no bypass before iteration 2
                 d->workSum += w;
                 d->kbytesSum[4] += w * d->kbytes[4] + (d->nHot - w) * 20.0 + d->nColdD * 4.0;
             }
