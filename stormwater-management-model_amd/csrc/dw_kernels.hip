@@ -139,8 +139,6 @@ struct Params {
     int nCold, nOutLinks;
     const int* coldLinks;         // LF_COLD conduits, ascending
     const int* outLinks;          // conduits with an outfall end, ascending
-    int nOutHot;
-    const int* outHot;            // ... of those, the ones without LF_COLD
     StepCtl* ctl;
 };
 
@@ -564,6 +562,42 @@ __device__ __forceinline__ void stageTables(double* ct, const double* g)
     __syncthreads();
 }
 
+// Streaming kernel: every conduit with LF_COLD clear (zero offsets, no outfall
+// end), one thread per conduit.  No calls, no root finders.
+// kWaves: minimum waves per SIMD the register allocator must allow (1 = no
+// constraint); selected at start-up (SWMM5_LINK_WAVES, default kLinkWavesDefault)
+template <bool kFirst, int kWaves, bool kFast>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves)))
+void k_link(Params p, int k)
+{
+    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;     // converged: dynwave.c:249-251
+    __shared__ double ct[5 * SWX_CIRC_N];
+    stageTables(ct, p.gTables);
+    double dt = p.ctl->dt;
+    int work = 0;
+    for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nL; j += gridDim.x * kBlock) {
+        uint32_t f = p.lflags[j];
+        if (f & LF_COLD) continue;
+        int2 nn = p.lnodes[j];
+        if (k >= 2 && p.conv[nn.x] && p.conv[nn.y]) continue;   // findBypassedLinks dynwave.c:335-345
+        conduitFlow<kFirst, false, kFast>(p, j, f, nn, k, dt, ct);
+        work++;
+    }
+    // measurement only (eager timing launches, iterations >= 2 where links can
+    // be bypassed): one atomic per workgroup after an LDS reduction
+    if (k >= 2 && p.countWork) {
+        __shared__ int wsum[kBlock / 64];
+        for (int off = 32; off > 0; off >>= 1) work += __shfl_down(work, off, 64);
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = work;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int t = 0;
+            for (int w = 0; w < kBlock / 64; w++) t += wsum[w];
+            if (t) atomicAdd(&p.ctl->linkWork[k], (unsigned long long)t);
+        }
+    }
+}
+
 // link_setOutfallDepth + outfall_setOutletDepth (link.c:728-766, node.c:1413-1492)
 __device__ __forceinline__ double outfallDepth(const Params& p, int i, uint32_t nf, int j,
                                                uint32_t f, const double* ct)
@@ -590,82 +624,6 @@ __device__ __forceinline__ double outfallDepth(const Params& p, int i, uint32_t 
     return yNew;
 }
 
-// Outfall node at link j's outfall end: at the first Picard iteration its old
-// depth is rotated (node_setOldHydState); later iterations refresh its depth
-// from the link's flow of the previous iteration (link_setOutfallDepth).
-template <bool kFirst>
-__device__ __forceinline__ void refreshOutfall(const Params& p, int j, uint32_t f, int2 nn,
-                                               const double* ct)
-{
-    int o = (f & LF_N2_OUTFALL) ? nn.y : nn.x;             // link.c:743-753 (node2 first)
-    if (kFirst) p.nOldDepth[o] = p.nNewDepth[o];
-    else p.nNewDepth[o] = outfallDepth(p, o, p.nflags[o], j, f, ct);
-}
-
-// After the Picard loop: outfall depths from the final link flows (the last
-// executed iteration's link_setOutfallDepth), before quality and step end.
-__global__ __launch_bounds__(kBlock) void k_outfall(Params p)
-{
-    __shared__ double ct[5 * SWX_CIRC_N];
-    stageTables(ct, p.gTables);
-    for (int c = blockIdx.x * kBlock + threadIdx.x; c < p.nOutLinks; c += gridDim.x * kBlock) {
-        int j = p.outLinks[c];
-        uint32_t f = p.lflags[j];
-        int2 nn = p.lnodes[j];
-        refreshOutfall<false>(p, j, f, nn, ct);
-    }
-}
-
-// Streaming kernel: every conduit with LF_COLD clear (zero offsets, no outfall
-// end), one thread per conduit.  No calls, no root finders.
-// kWaves: minimum waves per SIMD the register allocator must allow (1 = no
-// constraint); selected at start-up (SWMM5_LINK_WAVES, default kLinkWavesDefault)
-template <bool kFirst, int kWaves, bool kFast>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves)))
-void k_link(Params p, int k)
-{
-    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;     // converged: dynwave.c:249-251
-    __shared__ double ct[5 * SWX_CIRC_N];
-    stageTables(ct, p.gTables);
-    double dt = p.ctl->dt;
-    int work = 0;
-    // prologue: conduits with an outfall end.  link_setOutfallDepth of the
-    // previous iteration (findNodeDepths, dynwave.c:605) is evaluated here, on
-    // the thread that then updates the conduit -- the outfall's only reader --
-    // so it overlaps this launch instead of lengthening k_node.  Iteration 0
-    // uses the depth set at the end of the previous step (k_outfall).
-    for (int c = blockIdx.x * kBlock + threadIdx.x; c < p.nOutHot; c += gridDim.x * kBlock) {
-        int j = p.outHot[c];
-        uint32_t f = p.lflags[j];
-        int2 nn = p.lnodes[j];
-        refreshOutfall<kFirst>(p, j, f, nn, ct);
-        conduitFlow<kFirst, false, kFast>(p, j, f, nn, k, dt, ct);   // never bypassed
-        work++;
-    }
-    for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nL; j += gridDim.x * kBlock) {
-        uint32_t f = p.lflags[j];
-        if (f & (LF_COLD | LF_N1_OUTFALL | LF_N2_OUTFALL)) continue;
-        int2 nn = p.lnodes[j];
-        if (k >= 2 && p.conv[nn.x] && p.conv[nn.y]) continue;   // findBypassedLinks dynwave.c:335-345
-        conduitFlow<kFirst, false, kFast>(p, j, f, nn, k, dt, ct);
-        work++;
-    }
-    // measurement only (eager timing launches, iterations >= 2 where links can
-    // be bypassed): one atomic per workgroup after an LDS reduction
-    if (k >= 2 && p.countWork) {
-        __shared__ int wsum[kBlock / 64];
-        for (int off = 32; off > 0; off >>= 1) work += __shfl_down(work, off, 64);
-        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = work;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int t = 0;
-            for (int w = 0; w < kBlock / 64; w++) t += wsum[w];
-            if (t) atomicAdd(&p.ctl->linkWork[k], (unsigned long long)t);
-        }
-    }
-}
-
-
 
 // The few conduits with an invert offset or an outfall end (compacted list):
 // full flow classification with normal / critical depth.
@@ -680,8 +638,7 @@ __global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
         int j = p.coldLinks[c];
         uint32_t f = p.lflags[j];
         int2 nn = p.lnodes[j];
-        if (f & (LF_N1_OUTFALL | LF_N2_OUTFALL)) refreshOutfall<kFirst>(p, j, f, nn, ct);
-        else if (k >= 2 && p.conv[nn.x] && p.conv[nn.y]) continue;
+        if (k >= 2 && p.conv[nn.x] && p.conv[nn.y]) continue;
         conduitFlow<kFirst, true>(p, j, f, nn, k, dt, ct);
     }
 }
@@ -690,20 +647,39 @@ template <bool kFirst>
 __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
 {
     if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
+    // prologue: outfall depths (link_setOutfallDepth, findNodeDepths
+    // dynwave.c:605) from this iteration's link flows.  Only the outfall's
+    // single link reads that depth (next iteration), and this kernel never
+    // reads an outfall's depth, so it can run alongside the node updates; it
+    // goes first because it is the long (iterative) part of the launch.  The
+    // outfall is never "converged" (dynwave.c:281, 340): its link is never
+    // bypassed and the depth is refreshed every iteration, as in the reference.
+    if (blockIdx.x * kBlock < p.nOutLinks) {
+        __shared__ double ct[5 * SWX_CIRC_N];
+        stageTables(ct, p.gTables);
+        for (int c = blockIdx.x * kBlock + threadIdx.x; c < p.nOutLinks; c += gridDim.x * kBlock) {
+            int j = p.outLinks[c];
+            uint32_t f = p.lflags[j];
+            int2 nn = p.lnodes[j];
+            int o = (f & LF_N2_OUTFALL) ? nn.y : nn.x;    // link.c:743-753 (node2 first)
+            if (kFirst) p.nOldDepth[o] = p.nNewDepth[o];   // node_setOldHydState before the update
+            p.nNewDepth[o] = outfallDepth(p, o, p.nflags[o], j, f, ct);
+        }
+    }
     const double dt = p.ctl->dt;
     const double omega = 0.5;
     bool anyUnconv = false;
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
         uint32_t nf = p.nflags[i];
         int type = (int)(nf & NF_TYPE);
-        // an outfall's depth belongs to its link's kernel: not read here
+        // an outfall's depth is written by the prologue above: not read here
         double yLast = (type == OUTFALL) ? 0.0 : p.nNewDepth[i];
         double yOld, lat;
         if (kFirst) {
             // routing.c:328-332, node.c:293-304, 325-341 -- step-begin rotation
             double inflowPrev = p.inflow[i], outflowPrev = p.outflow[i];
             yOld = yLast;
-            if (type != OUTFALL) p.nOldDepth[i] = yOld;   // outfalls: refreshOutfall<true>
+            if (type != OUTFALL) p.nOldDepth[i] = yOld;   // outfalls: rotated in the prologue
             p.nOldVolume[i] = p.nNewVolume[i];
             p.oldFlowInflow[i] = inflowPrev;
             p.oldNetInflow[i] = inflowPrev - outflowPrev;
@@ -751,7 +727,7 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
         }
         p.inflow[i] = inflow;
         p.outflow[i] = outflow;
-        if (type == OUTFALL) continue;                     // depth: refreshOutfall / k_outfall
+        if (type == OUTFALL) continue;                     // depth set by the prologue
         // setNodeDepth (dynwave.c:636-762)
         bool isPonded = (canPond && yLast > fullDepth);
         double yCrown = p.yCrown[i];
@@ -1213,8 +1189,6 @@ static void launchStep(Router::Impl* d)
 {
     Params& p = d->p;
     for (int k = 0; k < p.maxTrials; k++) launchIteration(d, k);
-    if (p.nOutLinks)
-        hipLaunchKernelGGL(k_outfall, dim3(1), dim3(kBlock), 0, d->stream, p);
     int base = 4 * p.maxTrials;
     if (d->timing) (void)hipEventRecord(d->curEv[base], d->stream);
     if (p.P > 0) {
@@ -1283,7 +1257,7 @@ int Router::init(Project& prj, int device)
 
     // ---- link static ------------------------------------------------------
     std::vector<int> nodes2((size_t)nL * 2);
-    std::vector<int> lflags(nL), coldLinks, outLinks, outHot;
+    std::vector<int> lflags(nL), coldLinks, outLinks;
     std::vector<double> inv1(nL), inv2(nL), xd[11];
     for (auto& v : xd) v.resize(nL);
     for (int j = 0; j < nL; j++) {
@@ -1307,10 +1281,7 @@ int Router::init(Project& prj, int device)
             f |= LF_COLD;
             coldLinks.push_back(j);
         }
-        if (f & (LF_N1_OUTFALL | LF_N2_OUTFALL)) {
-            outLinks.push_back(j);
-            if (!(f & LF_COLD)) outHot.push_back(j);
-        }
+        if (f & (LF_N1_OUTFALL | LF_N2_OUTFALL)) outLinks.push_back(j);
         lflags[j] = (int)f;
         xd[0][j] = x.yFull; xd[1][j] = x.wMax; xd[2][j] = x.ywMax; xd[3][j] = x.aFull;
         xd[4][j] = x.rFull; xd[5][j] = x.sFull; xd[6][j] = x.sMax; xd[7][j] = x.yBot;
@@ -1330,9 +1301,6 @@ int Router::init(Project& prj, int device)
         UPI(cl, outLinks, outLinks.size());
         p.outLinks = cl;
         p.nOutLinks = (int)outLinks.size();
-        UPI(cl, outHot, outHot.size());
-        p.outHot = cl;
-        p.nOutHot = (int)outHot.size();
     }
     double* tmp;
     UPD(tmp, inv1, nL); p.inv1 = tmp;
