@@ -64,6 +64,26 @@ int    DLLEXPORT swmmx_getBackend(char *buf, int size);
 /* Select the HIP device ordinal used by swmm_start (default 0 / LOCAL_RANK). */
 int    DLLEXPORT swmmx_setDevice(int ordinal);
 
+/* ---- multi-GPU (one process per GPU) ----------------
+ * The network is split by node blocks (a conduit follows its node1, an
+ * outfall its conduit); every Picard iteration all-reduces the partial
+ * {inflow, outflow, surface area, dq/dh} sums of the nodes shared between
+ * ranks over RCCL.  Call before swmm_start, on every rank:
+ *   rank 0: swmmx_ncclUniqueId(id, 128) and broadcast the id to the others;
+ *   all:    swmmx_setPartition(rank, nranks, id, 128).
+ * Water quality and the binary results file are single-GPU only for now. */
+int    DLLEXPORT swmmx_ncclUniqueId(void *out, int bytes);     /* returns bytes written */
+int    DLLEXPORT swmmx_setPartition(int rank, int nranks, const void *ncclId, int idBytes);
+
+/* Test transport: replace RCCL by a host callback that reduces n doubles in
+ * place over the ranks (op 0 = sum, 1 = min) and returns 0 on success; steps
+ * then run as eager launches.  fn = NULL restores RCCL. */
+int    DLLEXPORT swmmx_setExchange(int (*fn)(double *buf, long n, int op, void *user), void *user);
+
+/* Owning rank of every node (objType swmm_NODE) or link (swmm_LINK) under the
+ * current partition; returns the object count. */
+int    DLLEXPORT swmmx_getOwner(int objType, int *out, int n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -15,6 +15,8 @@
 #include <memory>
 #include <string>
 
+#include <rccl/rccl.h>
+
 #include "../../include/swmm5_mi355x.h"
 #include "output.h"
 #include "project.h"
@@ -50,6 +52,7 @@ struct Engine {
 
 Engine* G = nullptr;
 int gDevice = -1;                    // swmmx_setDevice (survives swmm_open)
+Partition gPart;                     // swmmx_setPartition / swmmx_setExchange (survive swmm_open)
 
 int setErr(int code, const std::string& msg)
 {
@@ -145,7 +148,11 @@ int DLLEXPORT swmm_start(int saveFlag)
     G->initStorage = s;
     G->router.reset(new Router());
     int dev = (gDevice >= 0) ? gDevice : defaultDevice();
-    if (G->router->init(prj, dev)) return setErr(G->router->lastError(), G->router->lastErrorMsg());
+    if (gPart.active() && G->saveFlag)
+        return setErr(500, "ERROR 500: the results file is not yet supported with more than one GPU "
+                           "(swmm_start(0))");
+    if (G->router->init(prj, dev, gPart.active() ? &gPart : nullptr))
+        return setErr(G->router->lastError(), G->router->lastErrorMsg());
     G->isStarted = true;
     G->mirrorValid = true;
     return G->errorCode;
@@ -278,8 +285,17 @@ static double computeFlowError()   // massbal.c:858-902
 {
     Project& prj = *G->prj;
     double fs = 0.0;
-    for (int j = 0; j < prj.net.nNodes(); j++) fs += prj.st.newVolume[j];
-    for (int j = 0; j < prj.net.nLinks(); j++) fs += prj.st.lNewVolume[j];
+    const Partition& part = G->router->partition();
+    if (!part.active()) {
+        for (int j = 0; j < prj.net.nNodes(); j++) fs += prj.st.newVolume[j];
+        for (int j = 0; j < prj.net.nLinks(); j++) fs += prj.st.lNewVolume[j];
+    } else {                         // each rank sums what it owns, then over the ranks
+        for (int j = 0; j < prj.net.nNodes(); j++)
+            if (part.nodeOwner[j] == part.rank) fs += prj.st.newVolume[j];
+        for (int j = 0; j < prj.net.nLinks(); j++)
+            if (part.linkOwner[j] == part.rank) fs += prj.st.lNewVolume[j];
+        G->router->allreduceHost(&fs, 1, 0);
+    }
     G->finalStorage = fs;
     double* T = G->flowTot;   // dw, ex, flooding, outflow, evap, seep
     double totalInflow = G->initStorage + 0.0 + 0.0;
@@ -342,6 +358,7 @@ int DLLEXPORT swmm_end(void)   // swmm5.c:618-660
         if (!G->hostOnly) {
             syncMirror();
             G->router->flowTotals(G->flowTot);
+            G->router->allreduceHost(G->flowTot, 6, 0);   // per-rank totals (multi-GPU)
             G->flowError = computeFlowError();
             G->out.end(G->errorCode);
             if (!G->errorCode) writeReportSummary();
@@ -840,6 +857,52 @@ int DLLEXPORT swmmx_getBackend(char* buf, int size)
     std::string s = (G && G->router && G->router->ok()) ? G->router->deviceName() : std::string("none");
     if (buf && size > 0) snprintf(buf, (size_t)size, "%s", s.c_str());
     return 0;
+}
+
+int DLLEXPORT swmmx_ncclUniqueId(void* out, int bytes)
+{
+    if (!out || bytes < (int)sizeof(ncclUniqueId)) return -1;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return -2;
+    memcpy(out, &id, sizeof id);
+    return (int)sizeof id;
+}
+
+int DLLEXPORT swmmx_setPartition(int rank, int nranks, const void* ncclId, int idBytes)
+{
+    if (nranks < 1 || rank < 0 || rank >= nranks) return 500;
+    gPart = Partition();
+    gPart.rank = rank;
+    gPart.nranks = nranks;
+    gPart.transport = XCHG_RCCL;
+    if (ncclId && idBytes > 0) {
+        const unsigned char* b = (const unsigned char*)ncclId;
+        gPart.ncclId.assign(b, b + idBytes);
+        gPart.forced = (nranks == 1);     // one rank through the RCCL path: tests
+    }
+    return 0;
+}
+
+int DLLEXPORT swmmx_setExchange(int (*fn)(double*, long, int, void*), void* user)
+{
+    gPart.transport = fn ? XCHG_HOST : XCHG_RCCL;
+    gPart.xchg = fn;
+    gPart.xuser = user;
+    return 0;
+}
+
+int DLLEXPORT swmmx_getOwner(int objType, int* out, int n)
+{
+    if (!G || !G->prj) return -1;
+    Partition p;
+    p.rank = gPart.rank;
+    p.nranks = gPart.nranks;
+    std::string m;
+    if (buildPartition(G->prj->net, p, &m)) return -1;
+    const std::vector<int>& v = (objType == swmm_NODE) ? p.nodeOwner : p.linkOwner;
+    int k = std::min(n, (int)v.size());
+    for (int i = 0; i < k; i++) out[i] = v[i];
+    return (int)v.size();
 }
 
 int DLLEXPORT swmmx_setDevice(int ordinal)

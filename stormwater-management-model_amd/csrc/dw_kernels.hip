@@ -32,6 +32,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "router.h"
 #include "xsect.h"
 
@@ -73,6 +75,8 @@ enum : uint32_t {
     NF_OTYPE_SHIFT = 2,           // outfall type, 3 bits
     NF_DEGNEG = 1u << 5,          // degree < 0 (upstream terminal)
     NF_CANPOND = 1u << 6,
+    NF_SHARED = 1u << 7,          // multi-GPU: touched by conduits of several ranks
+    NF_REPLICA = 1u << 8,         // multi-GPU: replica of a node another rank owns
 };
 // ---- packed link state word ------------------------------------------------
 // bits 0-3 flowClass, 4-7 fullState code (0 / 8 / 9 / 10), 8 normalFlow,
@@ -96,6 +100,7 @@ struct StepCtl {
     double routingDuration;           // msec
     double routeStep;                 // fixed step (sec)
     unsigned long long linkWork[kMaxTrialsCap];   // timing mode: conduits updated per iteration
+    double stepRed[kNumPartials];     // this step's reduced block partials (k_finalize)
 };
 
 struct Params {
@@ -135,6 +140,14 @@ struct Params {
     double* partials;             // [nBlocksEnd][kNumPartials]
     int nBlocksEnd;
     int countWork;                // timing mode: count updated conduits per iteration
+    // multi-GPU exchange (partition.h): per local node its global shared slot
+    // (-1 if interior); partial sums {inflow, outflow, surfArea, sumdqdh} of
+    // shared nodes go to xsend[4*slot..], the all-reduced sums come back in
+    // xrecv; xsend[xflag] = 1 when an interior node did not converge
+    const int* sharedSlot;
+    const int* sharedList;        // local indices of the shared nodes
+    int nShared, xflag;
+    double *xsend, *xrecv;
     double* hostDt;               // host-mapped ring of per-step dt (Router::launchedDt)
     int nCold, nOutLinks;
     const int* coldLinks;         // LF_COLD conduits, ascending
@@ -571,6 +584,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
 void k_link(Params p, int k)
 {
     if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;     // converged: dynwave.c:249-251
+    if (p.nShared && blockIdx.x == 0 && threadIdx.x == 0) p.xsend[p.xflag] = 0.0;   // k_node sets it
     __shared__ double ct[5 * SWX_CIRC_N];
     stageTables(ct, p.gTables);
     double dt = p.ctl->dt;
@@ -643,6 +657,74 @@ __global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
     }
 }
 
+// setNodeDepth (dynwave.c:636-762) for node i given its summed inflow,
+// outflow, surface area and dq/dh; returns 1 when converged (dynwave.c:615-621)
+__device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_t nf, double dt,
+                                          double yLast, double yOld, double inflow, double outflow,
+                                          double surf, double sumdqdh)
+{
+    const double omega = 0.5;
+    bool canPond = (nf & NF_CANPOND) != 0;
+    double fullDepth = p.fullDepth[i];
+    bool isPonded = (canPond && yLast > fullDepth);
+    double yCrown = p.yCrown[i];
+    double overflow = 0.0;
+    double surfArea = gmax(surf, p.minSurfArea);
+    double dQ = inflow - outflow;
+    double dV = 0.5 * (p.oldNetInflow[i] + dQ) * dt;
+    bool isSurcharged = false;
+    if (p.surchargeMethod == SUR_EXTRAN) {
+        if (isPonded) isSurcharged = false;
+        else isSurcharged = (yCrown > 0.0 && yLast > yCrown);
+    }
+    double yNew, dy;
+    if (!isSurcharged) {
+        dy = dV / surfArea;
+        yNew = yOld + dy;
+        if (!isPonded) p.oldSurfArea[i] = surfArea;
+        if (k > 0) yNew = (1.0 - omega) * yLast + omega * yNew;
+        if (isPonded && yNew < fullDepth) yNew = fullDepth - 0.0001;
+    } else {
+        double corr = (nf & NF_DEGNEG) ? 0.6 : 1.0;
+        double denom = sumdqdh;
+        if (yLast < 1.25 * yCrown) {
+            double fr = (yLast - yCrown) / yCrown;
+            denom += (p.oldSurfArea[i] / dt - sumdqdh) * exp(-15.0 * fr);
+        }
+        if (denom == 0.0) dy = 0.0;
+        else dy = corr * dQ / denom;
+        yNew = yLast + dy;
+        if (yNew < yCrown) yNew = yCrown - 0.0001;
+        if (canPond && yNew > fullDepth) yNew = fullDepth + 0.0001;
+    }
+    if (yNew < 0) yNew = 0.0;
+    double yMax = fullDepth;
+    if (!canPond) yMax += p.surDepth[i];
+    double fullVolume = p.fullVolume[i];
+    if (yNew > yMax) {                                 // getFloodedDepth dynwave.c:766-795
+        double newVolume;
+        if (!canPond) {
+            overflow = dV / dt;
+            newVolume = fullVolume;
+            yNew = yMax;
+        } else {
+            double oldVolume = p.nOldVolume[i];
+            newVolume = gmax((oldVolume + dV), fullVolume);
+            overflow = (newVolume - gmax(oldVolume, fullVolume)) / dt;
+        }
+        if (overflow < 0.0001) overflow = 0.0;
+        p.nNewVolume[i] = newVolume;
+    } else {
+        p.nNewVolume[i] = (fullDepth > 0.0) ? fullVolume * (yNew / fullDepth) : 0.0;
+    }
+    p.overflow[i] = overflow;
+    p.dYdT[i] = fabs(yNew - yOld) / dt;
+    p.nNewDepth[i] = yNew;
+    int c = (fabs(yLast - yNew) > p.headTol) ? 0 : 1;  // dynwave.c:615-621
+    p.conv[i] = c;
+    return c;
+}
+
 template <bool kFirst>
 __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
 {
@@ -667,7 +749,6 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
         }
     }
     const double dt = p.ctl->dt;
-    const double omega = 0.5;
     bool anyUnconv = false;
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
         uint32_t nf = p.nflags[i];
@@ -694,7 +775,7 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
         bool canPond = (nf & NF_CANPOND) != 0;
         double fullDepth = p.fullDepth[i];
         double surf = 0.0;
-        if (canPond && yLast > fullDepth) surf = p.pondedArea[i];
+        if (canPond && yLast > fullDepth && !(nf & NF_REPLICA)) surf = p.pondedArea[i];  // owner adds it
         double inflow = 0.0, outflow = 0.0;   // node losses are 0 for non-storage nodes
         if (lat >= 0.0) inflow += lat;
         else outflow -= lat;
@@ -728,67 +809,45 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
         p.inflow[i] = inflow;
         p.outflow[i] = outflow;
         if (type == OUTFALL) continue;                     // depth set by the prologue
-        // setNodeDepth (dynwave.c:636-762)
-        bool isPonded = (canPond && yLast > fullDepth);
-        double yCrown = p.yCrown[i];
-        double overflow = 0.0;
-        double surfArea = gmax(surf, p.minSurfArea);
-        double dQ = inflow - outflow;
-        double dV = 0.5 * (p.oldNetInflow[i] + dQ) * dt;
-        bool isSurcharged = false;
-        if (p.surchargeMethod == SUR_EXTRAN) {
-            if (isPonded) isSurcharged = false;
-            else isSurcharged = (yCrown > 0.0 && yLast > yCrown);
+        if (nf & NF_SHARED) {                              // multi-GPU: partial sums out
+            int s4 = 4 * p.sharedSlot[i];
+            p.xsend[s4] = inflow;
+            p.xsend[s4 + 1] = outflow;
+            p.xsend[s4 + 2] = surf;
+            p.xsend[s4 + 3] = sumdqdh;
+            continue;
         }
-        double yNew, dy;
-        if (!isSurcharged) {
-            dy = dV / surfArea;
-            yNew = yOld + dy;
-            if (!isPonded) p.oldSurfArea[i] = surfArea;
-            if (k > 0) yNew = (1.0 - omega) * yLast + omega * yNew;
-            if (isPonded && yNew < fullDepth) yNew = fullDepth - 0.0001;
-        } else {
-            double corr = (nf & NF_DEGNEG) ? 0.6 : 1.0;
-            double denom = sumdqdh;
-            if (yLast < 1.25 * yCrown) {
-                double fr = (yLast - yCrown) / yCrown;
-                denom += (p.oldSurfArea[i] / dt - sumdqdh) * exp(-15.0 * fr);
-            }
-            if (denom == 0.0) dy = 0.0;
-            else dy = corr * dQ / denom;
-            yNew = yLast + dy;
-            if (yNew < yCrown) yNew = yCrown - 0.0001;
-            if (canPond && yNew > fullDepth) yNew = fullDepth + 0.0001;
-        }
-        if (yNew < 0) yNew = 0.0;
-        double yMax = fullDepth;
-        if (!canPond) yMax += p.surDepth[i];
-        double fullVolume = p.fullVolume[i];
-        if (yNew > yMax) {                                 // getFloodedDepth dynwave.c:766-795
-            double newVolume;
-            if (!canPond) {
-                overflow = dV / dt;
-                newVolume = fullVolume;
-                yNew = yMax;
-            } else {
-                double oldVolume = p.nOldVolume[i];
-                newVolume = gmax((oldVolume + dV), fullVolume);
-                overflow = (newVolume - gmax(oldVolume, fullVolume)) / dt;
-            }
-            if (overflow < 0.0001) overflow = 0.0;
-            p.nNewVolume[i] = newVolume;
-        } else {
-            p.nNewVolume[i] = (fullDepth > 0.0) ? fullVolume * (yNew / fullDepth) : 0.0;
-        }
-        p.overflow[i] = overflow;
-        p.dYdT[i] = fabs(yNew - yOld) / dt;
-        p.nNewDepth[i] = yNew;
-        int c = (fabs(yLast - yNew) > p.headTol) ? 0 : 1;  // dynwave.c:615-621
-        p.conv[i] = c;
-        if (!c) anyUnconv = true;
+        if (!nodeUpdate(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh)) anyUnconv = true;
     }
     // one flag per iteration; any writer stores 1 (no atomics needed)
+    if (__any(anyUnconv) && (threadIdx.x & 63) == 0) {
+        p.ctl->unconv[k] = 1;
+        if (p.nShared) p.xsend[p.xflag] = 1.0;             // tell the other ranks
+    }
+}
+
+// Multi-GPU: shared nodes after the all-reduce of their partial sums.  Every
+// replica applies the same update to the same sums (identical results on all
+// ranks), and an unconverged interior node on any rank marks the iteration.
+__global__ __launch_bounds__(kBlock) void k_node_shared(Params p, int k)
+{
+    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
+    const double dt = p.ctl->dt;
+    bool anyUnconv = false;
+    for (int s = blockIdx.x * kBlock + threadIdx.x; s < p.nShared; s += gridDim.x * kBlock) {
+        int i = p.sharedList[s];
+        int s4 = 4 * p.sharedSlot[i];
+        uint32_t nf = p.nflags[i];
+        double inflow = p.xrecv[s4], outflow = p.xrecv[s4 + 1];
+        double surf = p.xrecv[s4 + 2], sumdqdh = p.xrecv[s4 + 3];
+        p.inflow[i] = inflow;
+        p.outflow[i] = outflow;
+        if ((int)(nf & NF_TYPE) == OUTFALL) continue;
+        double yLast = p.nNewDepth[i], yOld = p.nOldDepth[i];
+        if (!nodeUpdate(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh)) anyUnconv = true;
+    }
     if (__any(anyUnconv) && (threadIdx.x & 63) == 0) p.ctl->unconv[k] = 1;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && p.xrecv[p.xflag] > 0.0) p.ctl->unconv[k] = 1;
 }
 
 // qualrout.c:146-174, 498-518
@@ -922,6 +981,7 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
     }
     for (int i = tid; i < p.nN; i += n) {
         uint32_t nf = p.nflags[i];
+        if (nf & NF_REPLICA) continue;                     // counted by the owning rank
         int type = (int)(nf & NF_TYPE);
         double q = 0.0;
         bool flooded = false;
@@ -980,32 +1040,40 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
 }
 
 // single-block finalisation (fixed-order reductions -> deterministic)
+// kPhase 0: reduce + apply (one GPU).  Multi-GPU: phase 1 reduces this rank's
+// partials into ctl->stepRed, the host/RCCL takes the min of the two Courant
+// limits over the ranks, phase 2 applies.
+template <int kPhase>
 __global__ void k_finalize(Params p)
 {
     __shared__ double sum[kNumPartials][kBlock];
     int t = threadIdx.x;
-    double acc[kNumPartials];
-    for (int q = 0; q < kNumPartials; q++) acc[q] = (q == 5 || q == 6) ? 1.0e300 : 0.0;
-    for (int b = t; b < p.nBlocksEnd; b += kBlock)
-        for (int q = 0; q < kNumPartials; q++) {
-            double v = p.partials[(size_t)b * kNumPartials + q];
-            if (q == 5 || q == 6) acc[q] = (v < acc[q]) ? v : acc[q]; else acc[q] += v;
-        }
-    for (int q = 0; q < kNumPartials; q++) sum[q][t] = acc[q];
-    __syncthreads();
-    for (int h = kBlock / 2; h > 0; h >>= 1) {          // fixed-shape tree: deterministic
-        if (t < h) {
-            for (int q = 0; q < kNumPartials; q++) {
-                double a = sum[q][t], b = sum[q][t + h];
-                sum[q][t] = (q == 5 || q == 6) ? ((b < a) ? b : a) : a + b;
-            }
-        }
-        __syncthreads();
-    }
-    if (t != 0) return;
-    double tot[kNumPartials];
-    for (int q = 0; q < kNumPartials; q++) tot[q] = sum[q][0];
     StepCtl* c = p.ctl;
+    if (kPhase != 2) {
+        double acc[kNumPartials];
+        for (int q = 0; q < kNumPartials; q++) acc[q] = (q == 5 || q == 6) ? 1.0e300 : 0.0;
+        for (int b = t; b < p.nBlocksEnd; b += kBlock)
+            for (int q = 0; q < kNumPartials; q++) {
+                double v = p.partials[(size_t)b * kNumPartials + q];
+                if (q == 5 || q == 6) acc[q] = (v < acc[q]) ? v : acc[q]; else acc[q] += v;
+            }
+        for (int q = 0; q < kNumPartials; q++) sum[q][t] = acc[q];
+        __syncthreads();
+        for (int h = kBlock / 2; h > 0; h >>= 1) {      // fixed-shape tree: deterministic
+            if (t < h) {
+                for (int q = 0; q < kNumPartials; q++) {
+                    double a = sum[q][t], b = sum[q][t + h];
+                    sum[q][t] = (q == 5 || q == 6) ? ((b < a) ? b : a) : a + b;
+                }
+            }
+            __syncthreads();
+        }
+        if (t == 0)
+            for (int q = 0; q < kNumPartials; q++) c->stepRed[q] = sum[q][0];
+    }
+    if (t != 0 || kPhase == 1) return;
+    double tot[kNumPartials];
+    for (int q = 0; q < kNumPartials; q++) tot[q] = c->stepRed[q];
     // Picard step count / convergence (dynwave.c:242-257)
     int steps;
     bool converged;
@@ -1060,6 +1128,10 @@ struct Router::Impl {
     Params p{};
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;      // fork/join branch for the cold conduits
+    Partition part;                  // this rank's part of the network (whole net on one GPU)
+    ncclComm_t comm = nullptr;       // RCCL communicator (multi-GPU, RCCL transport)
+    int gridS = 1;                   // k_node_shared grid
+    double* hostX = nullptr;         // host staging for the test transport
     hipEvent_t forkEv[kMaxTrialsCap] = {}, joinEv[kMaxTrialsCap] = {};
     hipGraphExec_t graph = nullptr;
     bool useGraph = true;
@@ -1117,6 +1189,8 @@ Router::~Router()
         if (d_->hostPinned) (void)hipHostFree(d_->hostPinned);
         if (d_->hostCtl) (void)hipHostFree(d_->hostCtl);
         if (d_->hostDt) (void)hipHostFree(d_->hostDt);
+        if (d_->hostX) (void)hipHostFree(d_->hostX);
+        if (d_->comm) (void)ncclCommDestroy(d_->comm);
         for (auto e : d_->clockEv) if (e) (void)hipEventDestroy(e);
         for (auto e : d_->ringEv) if (e) (void)hipEventDestroy(e);
         for (int k = 0; k < kMaxTrialsCap; k++) {
@@ -1160,6 +1234,21 @@ static LinkKernelFn linkKernel(bool first, int waves, bool fast)
 // cold work it would hide):
 //   main:  [fork k] k_link(k) ─wait join k─ k_node(k)
 //   side:  wait fork k ─ k_link_cold(k) ─[join k]
+// In-place all-reduce of n doubles across the ranks (op 0 sum, 1 min):
+// ncclAllReduce on the routing stream (graph-capturable), or, for the test
+// transport, a synchronous round trip through the host callback.
+static void exchange(Router::Impl* d, const double* send, double* recv, size_t n, int op)
+{
+    if (d->part.transport == XCHG_RCCL) {
+        (void)ncclAllReduce(send, recv, n, ncclDouble, op ? ncclMin : ncclSum, d->comm, d->stream);
+        return;
+    }
+    (void)hipMemcpyAsync(d->hostX, send, n * sizeof(double), hipMemcpyDeviceToHost, d->stream);
+    (void)hipStreamSynchronize(d->stream);
+    if (d->part.xchg) d->part.xchg(d->hostX, (long)n, op, d->part.xuser);
+    (void)hipMemcpyAsync(recv, d->hostX, n * sizeof(double), hipMemcpyHostToDevice, d->stream);
+}
+
 static void launchIteration(Router::Impl* d, int k)
 {
     Params& p = d->p;
@@ -1182,6 +1271,10 @@ static void launchIteration(Router::Impl* d, int k)
     } else {
         hipLaunchKernelGGL(k_node<false>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
     }
+    if (d->part.active()) {                        // interface sums + convergence flag
+        exchange(d, p.xsend, p.xrecv, (size_t)p.xflag + 1, 0);
+        hipLaunchKernelGGL(k_node_shared, dim3(d->gridS), dim3(kBlock), 0, d->stream, p, k);
+    }
     if (d->timing) (void)hipEventRecord(d->curEv[4 * k + 2], d->stream);
 }
 
@@ -1197,17 +1290,58 @@ static void launchStep(Router::Impl* d)
     }
     if (d->timing) (void)hipEventRecord(d->curEv[base + 1], d->stream);
     hipLaunchKernelGGL(k_step_end, dim3(d->gridEnd), dim3(kBlock), 0, d->stream, p);
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, d->stream, p);
+    if (d->part.active() && p.varStep) {           // global Courant limits (min over ranks)
+        hipLaunchKernelGGL(k_finalize<1>, dim3(1), dim3(kBlock), 0, d->stream, p);
+        exchange(d, &p.ctl->stepRed[5], &p.ctl->stepRed[5], 2, 1);
+        hipLaunchKernelGGL(k_finalize<2>, dim3(1), dim3(kBlock), 0, d->stream, p);
+    } else {
+        hipLaunchKernelGGL(k_finalize<0>, dim3(1), dim3(kBlock), 0, d->stream, p);
+    }
     if (d->timing) (void)hipEventRecord(d->curEv[base + 2], d->stream);
 }
 
-int Router::init(Project& prj, int device)
+int Router::init(Project& prj, int device, const Partition* partIn)
 {
     auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
     Impl* d = d_;
     Network& net = prj.net;
     State& st = prj.st;
     int nN = net.nNodes(), nL = net.nLinks(), P = prj.opt.ignoreQuality ? 0 : net.nPollut();
+    // local view: the whole network on one GPU, or this rank's part of it
+    if (partIn) d->part = *partIn;
+    else d->part.nranks = 1;
+    {
+        std::string m;
+        if (buildPartition(net, d->part, &m)) { fail(m); return err_; }
+    }
+    const Partition& part = d->part;
+    const std::vector<int>& LL = part.llink;
+    const std::vector<int>& LN = part.lnode;
+    if (part.active() && P > 0) { fail("water quality is not yet supported with more than one GPU"); return err_; }
+    nN = (int)LN.size();
+    nL = (int)LL.size();
+    auto gl = [&](const std::vector<double>& v) {
+        std::vector<double> o(nL);
+        for (int j = 0; j < nL; j++) o[j] = v[LL[j]];
+        return o;
+    };
+    auto gn = [&](const std::vector<double>& v) {
+        std::vector<double> o(nN);
+        for (int i = 0; i < nN; i++) o[i] = v[LN[i]];
+        return o;
+    };
+    auto gni = [&](const std::vector<int>& v) {
+        std::vector<int> o(nN);
+        for (int i = 0; i < nN; i++) o[i] = v[LN[i]];
+        return o;
+    };
+    auto gq = [&](const std::vector<double>& v, int nObj, const std::vector<int>& map) {
+        std::vector<double> o((size_t)P * map.size());
+        for (int q = 0; q < P; q++)
+            for (size_t k = 0; k < map.size(); k++) o[(size_t)q * map.size() + k] = v[(size_t)q * nObj + map[k]];
+        return o;
+    };
+    const int gN = net.nNodes(), gL = net.nLinks();
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         fail("no HIP device available (the MI355X engine has no CPU fallback)");
@@ -1260,24 +1394,26 @@ int Router::init(Project& prj, int device)
     std::vector<int> lflags(nL), coldLinks, outLinks;
     std::vector<double> inv1(nL), inv2(nL), xd[11];
     for (auto& v : xd) v.resize(nL);
+    for (int jj = 0; jj < gL; jj++)
+        if (net.linkType[jj] != CONDUIT) { fail("only conduit links are supported"); return err_; }
     for (int j = 0; j < nL; j++) {
-        if (net.linkType[j] != CONDUIT) { fail("only conduit links are supported"); return err_; }
-        int n1 = net.node1[j], n2 = net.node2[j];
-        nodes2[2 * j] = n1;
-        nodes2[2 * j + 1] = n2;
+        const int g = LL[j];                        // global link index
+        int n1 = net.node1[g], n2 = net.node2[g];   // global node indices
+        nodes2[2 * j] = part.gnode[n1];
+        nodes2[2 * j + 1] = part.gnode[n2];
         inv1[j] = net.invertElev[n1];
         inv2[j] = net.invertElev[n2];
-        const Xsect& x = net.xsect[j];
+        const Xsect& x = net.xsect[g];
         uint32_t f = (uint32_t)x.type & LF_XTYPE;
-        f |= ((uint32_t)net.barrels[j] & 0xFFu) << LF_BARREL_SHIFT;
-        if (net.hasLosses[j]) f |= LF_LOSSES;
-        if (net.hasFlapGate[j]) f |= LF_FLAP;
+        f |= ((uint32_t)net.barrels[g] & 0xFFu) << LF_BARREL_SHIFT;
+        if (net.hasLosses[g]) f |= LF_LOSSES;
+        if (net.hasFlapGate[g]) f |= LF_FLAP;
         if (net.nodeType[n1] == OUTFALL) { f |= LF_N1_OUTFALL; if (net.outfallFlap[n1]) f |= LF_N1_OFLAP; }
         if (net.nodeType[n2] == OUTFALL) { f |= LF_N2_OUTFALL; if (net.outfallFlap[n2]) f |= LF_N2_OFLAP; }
-        if (net.seepRate[j] > 0.0 || (prj.opt.evapRate > 0.0 && isOpen(x.type))) f |= LF_SEEP;
-        if (net.qLimit[j] > 0.0) f |= LF_QLIMIT;
-        if (net.direction[j] < 0) f |= LF_DIRNEG;
-        if (net.offset1[j] > 0.0 || net.offset2[j] > 0.0) {
+        if (net.seepRate[g] > 0.0 || (prj.opt.evapRate > 0.0 && isOpen(x.type))) f |= LF_SEEP;
+        if (net.qLimit[g] > 0.0) f |= LF_QLIMIT;
+        if (net.direction[g] < 0) f |= LF_DIRNEG;
+        if (net.offset1[g] > 0.0 || net.offset2[g] > 0.0) {
             f |= LF_COLD;
             coldLinks.push_back(j);
         }
@@ -1305,8 +1441,8 @@ int Router::init(Project& prj, int device)
     double* tmp;
     UPD(tmp, inv1, nL); p.inv1 = tmp;
     UPD(tmp, inv2, nL); p.inv2 = tmp;
-    UPD(tmp, net.offset1, nL); p.off1 = tmp;
-    UPD(tmp, net.offset2, nL); p.off2 = tmp;
+    UPD(tmp, gl(net.offset1), nL); p.off1 = tmp;
+    UPD(tmp, gl(net.offset2), nL); p.off2 = tmp;
     UPD(tmp, xd[0], nL); p.yFull = tmp;
     UPD(tmp, xd[1], nL); p.wMax = tmp;
     UPD(tmp, xd[2], nL); p.ywMax = tmp;
@@ -1318,52 +1454,58 @@ int Router::init(Project& prj, int device)
     UPD(tmp, xd[8], nL); p.aBot = tmp;
     UPD(tmp, xd[9], nL); p.sBot = tmp;
     UPD(tmp, xd[10], nL); p.rBot = tmp;
-    UPD(tmp, net.length, nL); p.length = tmp;
-    UPD(tmp, net.modLength, nL); p.modLength = tmp;
-    UPD(tmp, net.roughFactor, nL); p.roughFactor = tmp;
-    UPD(tmp, net.beta, nL); p.beta = tmp;
-    UPD(tmp, net.qMax, nL); p.qMax = tmp;
-    UPD(tmp, net.qLimit, nL); p.qLimit = tmp;
-    UPD(tmp, net.slope, nL); p.slope = tmp;
-    UPD(tmp, net.cLossInlet, nL); p.cIn = tmp;
-    UPD(tmp, net.cLossOutlet, nL); p.cOut = tmp;
-    UPD(tmp, net.cLossAvg, nL); p.cAvg = tmp;
-    UPD(tmp, net.seepRate, nL); p.seepRate = tmp;
+    UPD(tmp, gl(net.length), nL); p.length = tmp;
+    UPD(tmp, gl(net.modLength), nL); p.modLength = tmp;
+    UPD(tmp, gl(net.roughFactor), nL); p.roughFactor = tmp;
+    UPD(tmp, gl(net.beta), nL); p.beta = tmp;
+    UPD(tmp, gl(net.qMax), nL); p.qMax = tmp;
+    UPD(tmp, gl(net.qLimit), nL); p.qLimit = tmp;
+    UPD(tmp, gl(net.slope), nL); p.slope = tmp;
+    UPD(tmp, gl(net.cLossInlet), nL); p.cIn = tmp;
+    UPD(tmp, gl(net.cLossOutlet), nL); p.cOut = tmp;
+    UPD(tmp, gl(net.cLossAvg), nL); p.cAvg = tmp;
+    UPD(tmp, gl(net.seepRate), nL); p.seepRate = tmp;
     // ---- link dynamic -----------------------------------------------------
-    UPD(p.lNewFlow, st.lNewFlow, nL);
-    UPD(p.lOldFlow, st.lOldFlow, nL);
-    UPD(p.lNewDepth, st.lNewDepth, nL);
-    UPD(p.lOldDepth, st.lOldDepth, nL);
-    UPD(p.lNewVolume, st.lNewVolume, nL);
-    UPD(p.lOldVolume, st.lOldVolume, nL);
-    UPD(p.a1, st.a1, nL);
-    UPD(p.a2, st.a2, nL);
-    UPD(p.q1, st.q1, nL);
-    UPD(p.dqdh, st.dqdh, nL);
-    UPD(p.froude, st.froude, nL);
-    UPD(p.sa1, st.surfArea1, nL);
-    UPD(p.sa2, st.surfArea2, nL);
-    UPD(p.evapLoss, st.evapLossRate, nL);
-    UPD(p.seepLoss, st.seepLossRate, nL);
-    UPD(p.setting, st.setting, nL);
+    UPD(p.lNewFlow, gl(st.lNewFlow), nL);
+    UPD(p.lOldFlow, gl(st.lOldFlow), nL);
+    UPD(p.lNewDepth, gl(st.lNewDepth), nL);
+    UPD(p.lOldDepth, gl(st.lOldDepth), nL);
+    UPD(p.lNewVolume, gl(st.lNewVolume), nL);
+    UPD(p.lOldVolume, gl(st.lOldVolume), nL);
+    UPD(p.a1, gl(st.a1), nL);
+    UPD(p.a2, gl(st.a2), nL);
+    UPD(p.q1, gl(st.q1), nL);
+    UPD(p.dqdh, gl(st.dqdh), nL);
+    UPD(p.froude, gl(st.froude), nL);
+    UPD(p.sa1, gl(st.surfArea1), nL);
+    UPD(p.sa2, gl(st.surfArea2), nL);
+    UPD(p.evapLoss, gl(st.evapLossRate), nL);
+    UPD(p.seepLoss, gl(st.seepLossRate), nL);
+    UPD(p.setting, gl(st.setting), nL);
     {
         std::vector<int> ls(nL);
-        for (int j = 0; j < nL; j++)
-            ls[j] = st.flowClass[j] | (st.fullState[j] << 4) | (st.normalFlow[j] << 8) |
-                    (st.capacityLimited[j] << 9);
+        for (int j = 0; j < nL; j++) {
+            const int g = LL[j];
+            ls[j] = st.flowClass[g] | (st.fullState[g] << 4) | (st.normalFlow[g] << 8) |
+                    (st.capacityLimited[g] << 9);
+        }
         UPI(p.lstate, ls, nL);
     }
     // ---- node static ------------------------------------------------------
     std::vector<int> nflags(nN), outLink(nN, -1);
     std::vector<double> yCrown(nN);
+    std::vector<int> sharedNodes;
     for (int i = 0; i < nN; i++) {
-        uint32_t f = (uint32_t)net.nodeType[i] & NF_TYPE;
-        if (net.nodeType[i] == OUTFALL) f |= ((uint32_t)net.outfallType[i] & 0x7u) << NF_OTYPE_SHIFT;
-        if (net.degree[i] < 0) f |= NF_DEGNEG;
-        if (prj.opt.allowPonding && net.pondedArea[i] > 0.0) f |= NF_CANPOND;
+        const int g = LN[i];                        // global node index
+        uint32_t f = (uint32_t)net.nodeType[g] & NF_TYPE;
+        if (net.nodeType[g] == OUTFALL) f |= ((uint32_t)net.outfallType[g] & 0x7u) << NF_OTYPE_SHIFT;
+        if (net.degree[g] < 0) f |= NF_DEGNEG;
+        if (prj.opt.allowPonding && net.pondedArea[g] > 0.0) f |= NF_CANPOND;
+        if (part.sharedSlot[i] >= 0) { f |= NF_SHARED; sharedNodes.push_back(i); }
+        if (!part.owned[i]) f |= NF_REPLICA;
         nflags[i] = (int)f;
-        yCrown[i] = net.crownElev[i] - net.invertElev[i];
-        if (net.nodeType[i] == OUTFALL && net.outfallType[i] > O_FIXED) {
+        yCrown[i] = net.crownElev[g] - net.invertElev[g];
+        if (net.nodeType[g] == OUTFALL && net.outfallType[g] > O_FIXED) {
             fail("TIMESERIES outfalls are not supported on the device yet");
             return err_;
         }
@@ -1371,18 +1513,19 @@ int Router::init(Project& prj, int device)
     // CSR: incident links per node, ascending link index (all links are true
     // conduits, so this is exactly the order of dynwave.c:398-401)
     std::vector<int> rowptr(nN + 1, 0), csr;
-    for (int j = 0; j < nL; j++) { rowptr[net.node1[j] + 1]++; rowptr[net.node2[j] + 1]++; }
+    for (int j = 0; j < nL; j++) { rowptr[nodes2[2 * j] + 1]++; rowptr[nodes2[2 * j + 1] + 1]++; }
     for (int i = 0; i < nN; i++) rowptr[i + 1] += rowptr[i];
     csr.resize(rowptr[nN]);
     {
         std::vector<int> fillp(rowptr.begin(), rowptr.end() - 1);
         for (int j = 0; j < nL; j++) {
-            csr[fillp[net.node1[j]]++] = j;
-            csr[fillp[net.node2[j]]++] = (int)((unsigned)j | 0x80000000u);
+            int a = nodes2[2 * j], b = nodes2[2 * j + 1];
+            csr[fillp[a]++] = j;
+            csr[fillp[b]++] = (int)((unsigned)j | 0x80000000u);
             // the reference's link_setOutfallDepth loop: last link touching an
             // outfall wins (validateGeneralLayout allows only one)
-            if (net.nodeType[net.node2[j]] == OUTFALL) outLink[net.node2[j]] = j;
-            else if (net.nodeType[net.node1[j]] == OUTFALL) outLink[net.node1[j]] = j;
+            if (net.nodeType[LN[b]] == OUTFALL) outLink[b] = j;
+            else if (net.nodeType[LN[a]] == OUTFALL) outLink[a] = j;
         }
     }
     d->nE = (int)csr.size();
@@ -1395,39 +1538,44 @@ int Router::init(Project& prj, int device)
         UPI(rp, csr, csr.size()); p.csr = rp;
         UPI(rp, outLink, nN); p.outfallLink = rp;
     }
-    UPD(tmp, net.invertElev, nN); p.invert = tmp;
-    UPD(tmp, net.fullDepth, nN); p.fullDepth = tmp;
-    UPD(tmp, net.surDepth, nN); p.surDepth = tmp;
-    UPD(tmp, net.pondedArea, nN); p.pondedArea = tmp;
+    UPD(tmp, gn(net.invertElev), nN); p.invert = tmp;
+    UPD(tmp, gn(net.fullDepth), nN); p.fullDepth = tmp;
+    UPD(tmp, gn(net.surDepth), nN); p.surDepth = tmp;
+    UPD(tmp, gn(net.pondedArea), nN); p.pondedArea = tmp;
     UPD(tmp, yCrown, nN); p.yCrown = tmp;
-    UPD(tmp, net.crownElev, nN); p.crownElev = tmp;
-    UPD(tmp, net.fullVolume, nN); p.fullVolume = tmp;
-    UPD(tmp, net.fixedStage, nN); p.fixedStage = tmp;
+    UPD(tmp, gn(net.crownElev), nN); p.crownElev = tmp;
+    UPD(tmp, gn(net.fullVolume), nN); p.fullVolume = tmp;
+    UPD(tmp, gn(net.fixedStage), nN); p.fixedStage = tmp;
     // ---- node dynamic -----------------------------------------------------
-    UPD(p.nNewDepth, st.newDepth, nN);
-    UPD(p.nOldDepth, st.oldDepth, nN);
-    UPD(p.nNewVolume, st.newVolume, nN);
-    UPD(p.nOldVolume, st.oldVolume, nN);
-    UPD(p.inflow, st.inflow, nN);
-    UPD(p.outflow, st.outflow, nN);
-    UPD(p.overflow, st.overflow, nN);
-    UPD(p.newLat, st.newLatFlow, nN);
-    UPD(p.oldLat, st.oldLatFlow, nN);
-    UPD(p.oldNetInflow, st.oldNetInflow, nN);
-    UPD(p.oldFlowInflow, st.oldFlowInflow, nN);
-    UPD(p.oldSurfArea, st.oldSurfArea, nN);
-    UPD(p.dYdT, st.dYdT, nN);
-    UPI(p.conv, st.converged, nN);
+    UPD(p.nNewDepth, gn(st.newDepth), nN);
+    UPD(p.nOldDepth, gn(st.oldDepth), nN);
+    UPD(p.nNewVolume, gn(st.newVolume), nN);
+    UPD(p.nOldVolume, gn(st.oldVolume), nN);
+    UPD(p.inflow, gn(st.inflow), nN);
+    UPD(p.outflow, gn(st.outflow), nN);
+    UPD(p.overflow, gn(st.overflow), nN);
+    UPD(p.newLat, gn(st.newLatFlow), nN);
+    UPD(p.oldLat, gn(st.oldLatFlow), nN);
+    UPD(p.oldNetInflow, gn(st.oldNetInflow), nN);
+    UPD(p.oldFlowInflow, gn(st.oldFlowInflow), nN);
+    UPD(p.oldSurfArea, gn(st.oldSurfArea), nN);
+    UPD(p.dYdT, gn(st.dYdT), nN);
+    UPI(p.conv, gni(st.converged), nN);
     // ---- inflows ----------------------------------------------------------
     d->constantInflow = prj.inflowsAreConstant();
     {
         std::vector<double> lat, qual;
         double tot[3];
         prj.evalInflows(prj.getDateTime(0.0), lat, P ? &qual : nullptr, &tot[0], &tot[1], &tot[2]);
+        // system inflow totals are counted once (rank 0); a node's own inflow
+        // is added by its owner only (replicas start their sums from 0)
+        if (part.rank != 0) tot[0] = tot[1] = tot[2] = 0.0;
         d->latTot0[0] = tot[0]; d->latTot0[1] = tot[1]; d->latTot0[2] = tot[2];
-        UPD(d->latBase, lat, nN);
+        std::vector<double> latL(nN);
+        for (int i = 0; i < nN; i++) latL[i] = part.owned[i] ? lat[LN[i]] : 0.0;
+        UPD(d->latBase, latL, nN);
         if (P) {
-            UPD(d->qualBase, qual, (size_t)P * nN);
+            UPD(d->qualBase, gq(qual, gN, LN), (size_t)P * nN);
         } else {
             d->qualBase = devAlloc<double>(d, 1, &e);
         }
@@ -1440,10 +1588,10 @@ int Router::init(Project& prj, int device)
         for (int q = 0; q < P; q++) kd[q] = net.pollut[q].kDecay;
         UPD(tmp, kd, kd.size()); p.kDecay = tmp;
         size_t nq = (size_t)std::max(P, 0);
-        UPD(p.nOldQual, st.nOldQual, nq * nN);
-        UPD(p.nNewQual, st.nNewQual, nq * nN);
-        UPD(p.lOldQual, st.lOldQual, nq * nL);
-        UPD(p.lNewQual, st.lNewQual, nq * nL);
+        UPD(p.nOldQual, gq(st.nOldQual, gN, LN), nq * nN);
+        UPD(p.nNewQual, gq(st.nNewQual, gN, LN), nq * nN);
+        UPD(p.lOldQual, gq(st.lOldQual, gL, LL), nq * nL);
+        UPD(p.lNewQual, gq(st.lNewQual, gL, LL), nq * nL);
     }
     // ---- tables, partials, control ---------------------------------------
     {
@@ -1474,6 +1622,31 @@ int Router::init(Project& prj, int device)
     d->gridC = std::max(1, std::min((p.nCold + kBlock - 1) / kBlock, maxBlocks));
     d->gridEnd = std::max(1, std::min((std::max(nN, nL) + kBlock - 1) / kBlock, 2 * prop.multiProcessorCount));
     p.nBlocksEnd = d->gridEnd;
+    // ---- multi-GPU exchange ----------------------------------------------------
+    p.nShared = (int)sharedNodes.size();
+    p.xflag = 4 * part.nSharedGlobal;
+    {
+        std::vector<int> slots(part.sharedSlot.begin(), part.sharedSlot.end());
+        int* ip;
+        UPI(ip, slots, nN); p.sharedSlot = ip;
+        UPI(ip, sharedNodes, sharedNodes.size()); p.sharedList = ip;
+        std::vector<double> z((size_t)p.xflag + 1, 0.0);
+        UPD(p.xsend, z, z.size());
+        UPD(p.xrecv, z, z.size());
+    }
+    d->gridS = std::max(1, std::min((p.nShared + kBlock - 1) / kBlock, maxBlocks));
+    if (part.active()) {
+        if (part.transport == XCHG_RCCL) {
+            if (part.ncclId.size() != sizeof(ncclUniqueId)) { fail("RCCL unique id missing"); return err_; }
+            ncclUniqueId id;
+            memcpy(&id, part.ncclId.data(), sizeof id);
+            ncclResult_t r = ncclCommInitRank(&d->comm, part.nranks, id, part.rank);
+            if (r != ncclSuccess) { fail(std::string("ncclCommInitRank: ") + ncclGetErrorString(r)); return err_; }
+        } else {
+            if (!part.xchg) { fail("host exchange callback missing"); return err_; }
+            HIPCHECK(hipHostMalloc((void**)&d->hostX, ((size_t)p.xflag + 8) * sizeof(double), hipHostMallocDefault));
+        }
+    }
     p.partials = devAlloc<double>(d, (size_t)d->gridEnd * kNumPartials, &e);
     if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
     p.ctl = devAlloc<StepCtl>(d, 1, &e);
@@ -1541,7 +1714,9 @@ int Router::init(Project& prj, int device)
     }
 
     // ---- capture the step graph ----------------------------------------------
-    d->useGraph = true;
+    // (the host-callback test transport synchronises inside the step: eager)
+    d->useGraph = !(part.active() && part.transport == XCHG_HOST);
+    if (!d->useGraph) { ok_ = true; return 0; }
     hipGraph_t g;
     HIPCHECK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
     launchStep(d);
@@ -1603,14 +1778,20 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
         HIPCHECK(hipEventSynchronize(d->ringEv[s]));
         double* slot = d->hostPinned + (size_t)s * d->slotDoubles;
         size_t nN = p.nN, nq = (size_t)p.P * nN;
-        memcpy(slot, latFlow, nN * sizeof(double));
+        const Partition& part = d->part;
+        if (part.active()) {                       // this rank's nodes; owners add inflow
+            for (size_t i = 0; i < nN; i++) slot[i] = part.owned[i] ? latFlow[part.lnode[i]] : 0.0;
+        } else {
+            memcpy(slot, latFlow, nN * sizeof(double));
+        }
         if (nq) {
             if (qualLoad) memcpy(slot + nN, qualLoad, nq * sizeof(double));
             else memset(slot + nN, 0, nq * sizeof(double));
         }
-        slot[nN + nq + 0] = tot[0];
-        slot[nN + nq + 1] = tot[1];
-        slot[nN + nq + 2] = tot[2];
+        bool countTotals = part.rank == 0;         // system totals counted once
+        slot[nN + nq + 0] = countTotals ? tot[0] : 0.0;
+        slot[nN + nq + 1] = countTotals ? tot[1] : 0.0;
+        slot[nN + nq + 2] = countTotals ? tot[2] : 0.0;
         HIPCHECK(hipMemcpyAsync(d->latBase, slot, nN * sizeof(double), hipMemcpyHostToDevice, d->stream));
         if (nq)
             HIPCHECK(hipMemcpyAsync(d->qualBase, slot + nN, nq * sizeof(double), hipMemcpyHostToDevice, d->stream));
@@ -1641,8 +1822,10 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
         HIPCHECK(hipMemcpyAsync(t.pinned + 1, d->ctl->linkWork, kMaxTrialsCap * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, d->stream));
         HIPCHECK(hipMemsetAsync(d->ctl->linkWork, 0, kMaxTrialsCap * sizeof(unsigned long long), d->stream));
-    } else {
+    } else if (d->useGraph) {
         HIPCHECK(hipGraphLaunch(d->graph, d->stream));
+    } else {
+        launchStep(d);
     }
     // completion marker of this step: k_finalize has by then written the next
     // step's dt into the host-mapped ring (Router::launchedDt)
@@ -1707,42 +1890,68 @@ int Router::download(Project& prj)
     Impl* d = d_;
     Params& p = d->p;
     State& st = prj.st;
+    const Partition& part = d->part;
+    const bool multi = part.active();
     size_t nN = p.nN, nL = p.nL;
-    auto dn = [&](std::vector<double>& v, const double* src, size_t n) {
-        v.resize(n);
-        return hipMemcpyAsync(v.data(), src, n * sizeof(double), hipMemcpyDeviceToHost, d->stream);
+    std::vector<double> tmp;
+    // one GPU: straight into the host mirror; several: this rank's owned
+    // nodes and its conduits are scattered to their global positions
+    auto dnN = [&](std::vector<double>& v, const double* src) -> hipError_t {
+        if (!multi) {
+            v.resize(nN);
+            return hipMemcpyAsync(v.data(), src, nN * sizeof(double), hipMemcpyDeviceToHost, d->stream);
+        }
+        tmp.resize(nN);
+        hipError_t r = hipMemcpy(tmp.data(), src, nN * sizeof(double), hipMemcpyDeviceToHost);
+        for (size_t i = 0; i < nN; i++)
+            if (part.owned[i]) v[part.lnode[i]] = tmp[i];
+        return r;
     };
-    HIPCHECK(dn(st.newDepth, p.nNewDepth, nN));
-    HIPCHECK(dn(st.oldDepth, p.nOldDepth, nN));
-    HIPCHECK(dn(st.newVolume, p.nNewVolume, nN));
-    HIPCHECK(dn(st.oldVolume, p.nOldVolume, nN));
-    HIPCHECK(dn(st.inflow, p.inflow, nN));
-    HIPCHECK(dn(st.outflow, p.outflow, nN));
-    HIPCHECK(dn(st.overflow, p.overflow, nN));
-    HIPCHECK(dn(st.newLatFlow, p.newLat, nN));
-    HIPCHECK(dn(st.oldLatFlow, p.oldLat, nN));
-    HIPCHECK(dn(st.oldNetInflow, p.oldNetInflow, nN));
-    HIPCHECK(dn(st.oldFlowInflow, p.oldFlowInflow, nN));
-    HIPCHECK(dn(st.oldSurfArea, p.oldSurfArea, nN));
-    HIPCHECK(dn(st.dYdT, p.dYdT, nN));
-    HIPCHECK(dn(st.lNewFlow, p.lNewFlow, nL));
-    HIPCHECK(dn(st.lOldFlow, p.lOldFlow, nL));
-    HIPCHECK(dn(st.lNewDepth, p.lNewDepth, nL));
-    HIPCHECK(dn(st.lOldDepth, p.lOldDepth, nL));
-    HIPCHECK(dn(st.lNewVolume, p.lNewVolume, nL));
-    HIPCHECK(dn(st.lOldVolume, p.lOldVolume, nL));
-    HIPCHECK(dn(st.a1, p.a1, nL));
-    HIPCHECK(dn(st.a2, p.a2, nL));
-    HIPCHECK(dn(st.q1, p.q1, nL));
-    HIPCHECK(dn(st.dqdh, p.dqdh, nL));
-    HIPCHECK(dn(st.froude, p.froude, nL));
-    HIPCHECK(dn(st.surfArea1, p.sa1, nL));
-    HIPCHECK(dn(st.surfArea2, p.sa2, nL));
-    HIPCHECK(dn(st.evapLossRate, p.evapLoss, nL));
-    HIPCHECK(dn(st.seepLossRate, p.seepLoss, nL));
-    HIPCHECK(dn(st.setting, p.setting, nL));
-    size_t P = p.P;
+    auto dnL = [&](std::vector<double>& v, const double* src) -> hipError_t {
+        if (!multi) {
+            v.resize(nL);
+            return hipMemcpyAsync(v.data(), src, nL * sizeof(double), hipMemcpyDeviceToHost, d->stream);
+        }
+        tmp.resize(nL);
+        hipError_t r = hipMemcpy(tmp.data(), src, nL * sizeof(double), hipMemcpyDeviceToHost);
+        for (size_t j = 0; j < nL; j++) v[part.llink[j]] = tmp[j];
+        return r;
+    };
+    HIPCHECK(dnN(st.newDepth, p.nNewDepth));
+    HIPCHECK(dnN(st.oldDepth, p.nOldDepth));
+    HIPCHECK(dnN(st.newVolume, p.nNewVolume));
+    HIPCHECK(dnN(st.oldVolume, p.nOldVolume));
+    HIPCHECK(dnN(st.inflow, p.inflow));
+    HIPCHECK(dnN(st.outflow, p.outflow));
+    HIPCHECK(dnN(st.overflow, p.overflow));
+    HIPCHECK(dnN(st.newLatFlow, p.newLat));
+    HIPCHECK(dnN(st.oldLatFlow, p.oldLat));
+    HIPCHECK(dnN(st.oldNetInflow, p.oldNetInflow));
+    HIPCHECK(dnN(st.oldFlowInflow, p.oldFlowInflow));
+    HIPCHECK(dnN(st.oldSurfArea, p.oldSurfArea));
+    HIPCHECK(dnN(st.dYdT, p.dYdT));
+    HIPCHECK(dnL(st.lNewFlow, p.lNewFlow));
+    HIPCHECK(dnL(st.lOldFlow, p.lOldFlow));
+    HIPCHECK(dnL(st.lNewDepth, p.lNewDepth));
+    HIPCHECK(dnL(st.lOldDepth, p.lOldDepth));
+    HIPCHECK(dnL(st.lNewVolume, p.lNewVolume));
+    HIPCHECK(dnL(st.lOldVolume, p.lOldVolume));
+    HIPCHECK(dnL(st.a1, p.a1));
+    HIPCHECK(dnL(st.a2, p.a2));
+    HIPCHECK(dnL(st.q1, p.q1));
+    HIPCHECK(dnL(st.dqdh, p.dqdh));
+    HIPCHECK(dnL(st.froude, p.froude));
+    HIPCHECK(dnL(st.surfArea1, p.sa1));
+    HIPCHECK(dnL(st.surfArea2, p.sa2));
+    HIPCHECK(dnL(st.evapLossRate, p.evapLoss));
+    HIPCHECK(dnL(st.seepLossRate, p.seepLoss));
+    HIPCHECK(dnL(st.setting, p.setting));
+    size_t P = p.P;                                 // (quality: one GPU only)
     if (P) {
+        auto dn = [&](std::vector<double>& v, const double* src, size_t n) {
+            v.resize(n);
+            return hipMemcpyAsync(v.data(), src, n * sizeof(double), hipMemcpyDeviceToHost, d->stream);
+        };
         HIPCHECK(dn(st.nOldQual, p.nOldQual, P * nN));
         HIPCHECK(dn(st.nNewQual, p.nNewQual, P * nN));
         HIPCHECK(dn(st.lOldQual, p.lOldQual, P * nL));
@@ -1753,14 +1962,18 @@ int Router::download(Project& prj)
     HIPCHECK(hipMemcpyAsync(cv.data(), p.conv, nN * sizeof(int), hipMemcpyDeviceToHost, d->stream));
     HIPCHECK(hipMemcpyAsync(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost, d->stream));
     HIPCHECK(hipStreamSynchronize(d->stream));
-    st.flowClass.resize(nL); st.fullState.resize(nL); st.normalFlow.resize(nL); st.capacityLimited.resize(nL);
+    size_t gL = multi ? prj.net.nLinks() : nL, gN = multi ? prj.net.nNodes() : nN;
+    st.flowClass.resize(gL); st.fullState.resize(gL); st.normalFlow.resize(gL); st.capacityLimited.resize(gL);
+    st.converged.resize(gN);
     for (size_t j = 0; j < nL; j++) {
-        st.flowClass[j] = ls[j] & 0xF;
-        st.fullState[j] = (ls[j] >> 4) & 0xF;
-        st.normalFlow[j] = (ls[j] >> 8) & 1;
-        st.capacityLimited[j] = (ls[j] >> 9) & 1;
+        size_t g = multi ? part.llink[j] : j;
+        st.flowClass[g] = ls[j] & 0xF;
+        st.fullState[g] = (ls[j] >> 4) & 0xF;
+        st.normalFlow[g] = (ls[j] >> 8) & 1;
+        st.capacityLimited[g] = (ls[j] >> 9) & 1;
     }
-    st.converged = cv;
+    for (size_t i = 0; i < nN; i++)
+        if (!multi || part.owned[i]) st.converged[multi ? part.lnode[i] : i] = cv[i];
     st.variableStep = d->hostCtl->variableStep;
     return 0;
 }
@@ -1771,22 +1984,40 @@ int Router::upload(Project& prj)
     Impl* d = d_;
     Params& p = d->p;
     State& st = prj.st;
+    const Partition& part = d->part;
+    const bool multi = part.active();
     size_t nN = p.nN, nL = p.nL;
-    auto up = [&](double* dst, const std::vector<double>& v, size_t n) {
-        return hipMemcpyAsync(dst, v.data(), n * sizeof(double), hipMemcpyHostToDevice, d->stream);
+    // stage buffers live until the final synchronize
+    std::vector<std::vector<double>> stage;
+    auto upN = [&](double* dst, const std::vector<double>& v) {
+        if (!multi) return hipMemcpyAsync(dst, v.data(), nN * sizeof(double), hipMemcpyHostToDevice, d->stream);
+        // replicas keep their device values (their owner's mirror is elsewhere)
+        stage.emplace_back(nN);
+        hipError_t r = hipMemcpy(stage.back().data(), dst, nN * sizeof(double), hipMemcpyDeviceToHost);
+        if (r != hipSuccess) return r;
+        for (size_t i = 0; i < nN; i++)
+            if (part.owned[i]) stage.back()[i] = v[part.lnode[i]];
+        return hipMemcpyAsync(dst, stage.back().data(), nN * sizeof(double), hipMemcpyHostToDevice, d->stream);
     };
-    HIPCHECK(up(p.nNewDepth, st.newDepth, nN));
-    HIPCHECK(up(p.nOldDepth, st.oldDepth, nN));
-    HIPCHECK(up(p.nNewVolume, st.newVolume, nN));
-    HIPCHECK(up(p.inflow, st.inflow, nN));
-    HIPCHECK(up(p.outflow, st.outflow, nN));
-    HIPCHECK(up(p.newLat, st.newLatFlow, nN));
-    HIPCHECK(up(p.lNewFlow, st.lNewFlow, nL));
-    HIPCHECK(up(p.lNewDepth, st.lNewDepth, nL));
-    HIPCHECK(up(p.lNewVolume, st.lNewVolume, nL));
-    HIPCHECK(up(p.q1, st.q1, nL));
-    HIPCHECK(up(p.a1, st.a1, nL));
-    HIPCHECK(up(p.setting, st.setting, nL));
+    auto upL = [&](double* dst, const std::vector<double>& v) {
+        if (!multi) return hipMemcpyAsync(dst, v.data(), nL * sizeof(double), hipMemcpyHostToDevice, d->stream);
+        stage.emplace_back(nL);
+        for (size_t j = 0; j < nL; j++) stage.back()[j] = v[part.llink[j]];
+        return hipMemcpyAsync(dst, stage.back().data(), nL * sizeof(double), hipMemcpyHostToDevice, d->stream);
+    };
+    stage.reserve(16);
+    HIPCHECK(upN(p.nNewDepth, st.newDepth));
+    HIPCHECK(upN(p.nOldDepth, st.oldDepth));
+    HIPCHECK(upN(p.nNewVolume, st.newVolume));
+    HIPCHECK(upN(p.inflow, st.inflow));
+    HIPCHECK(upN(p.outflow, st.outflow));
+    HIPCHECK(upN(p.newLat, st.newLatFlow));
+    HIPCHECK(upL(p.lNewFlow, st.lNewFlow));
+    HIPCHECK(upL(p.lNewDepth, st.lNewDepth));
+    HIPCHECK(upL(p.lNewVolume, st.lNewVolume));
+    HIPCHECK(upL(p.q1, st.q1));
+    HIPCHECK(upL(p.a1, st.a1));
+    HIPCHECK(upL(p.setting, st.setting));
     HIPCHECK(hipStreamSynchronize(d->stream));
     return 0;
 }
@@ -1834,6 +2065,31 @@ void Router::setTiming(bool on)
     d_->p.countWork = on ? 1 : 0;                  // eager launches only; the graph keeps 0
     for (int k = 0; k < Impl::kClasses; k++) { d_->kms[k] = 0; d_->kcnt[k] = 0; d_->kbytesSum[k] = 0; }
     d_->workSum = 0;
+}
+
+const Partition& Router::partition() const { return d_->part; }
+
+int Router::allreduceHost(double* buf, int n, int op)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    if (!d->part.active() || n <= 0) return 0;
+    if (d->part.transport == XCHG_HOST) {
+        if (d->part.xchg(buf, n, op, d->part.xuser)) { fail("host exchange failed"); return err_; }
+        return 0;
+    }
+    double* tmp = nullptr;
+    HIPCHECK(hipMalloc(&tmp, n * sizeof(double)));
+    hipError_t e = hipMemcpyAsync(tmp, buf, n * sizeof(double), hipMemcpyHostToDevice, d->stream);
+    if (e == hipSuccess) {
+        ncclResult_t r = ncclAllReduce(tmp, tmp, n, ncclDouble, op ? ncclMin : ncclSum, d->comm, d->stream);
+        if (r != ncclSuccess) { (void)hipFree(tmp); fail(std::string("ncclAllReduce: ") + ncclGetErrorString(r)); return err_; }
+        e = hipMemcpyAsync(buf, tmp, n * sizeof(double), hipMemcpyDeviceToHost, d->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
+    (void)hipFree(tmp);
+    if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+    return 0;
 }
 
 void Router::timedWork(double* updated, double* hot)

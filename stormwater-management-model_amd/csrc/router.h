@@ -12,6 +12,7 @@
 #include <string>
 #include <vector>
 
+#include "partition.h"
 #include "project.h"
 
 namespace swx {
@@ -25,8 +26,10 @@ class Router {
 public:
     Router();
     ~Router();
-    // Allocate + upload static network and initial state; build graph.
-    int init(Project& prj, int device);
+    // Allocate + upload static network and initial state; build graph.  With
+    // a multi-rank partition only this rank's part of the network is uploaded
+    // and every Picard iteration all-reduces the shared-node sums.
+    int init(Project& prj, int device, const Partition* part = nullptr);
     // Enqueue one routing step.  The step length and the simulation clock
     // live on the device (k_finalize computes the next dt exactly as
     // dynwave_getRoutingStep + execRouting's clamp do), so a fixed-step run
@@ -34,14 +37,18 @@ public:
     // loads (nullptr = the constant arrays evaluated at init); totals =
     // {dwInflow, exInflow, exOutflow} rates of those inflows.
     int step(const double* latFlow, const double* qualLoad, const double totals[3]);
-    // Read the device clock after the last enqueued step (synchronises):
-    // routing time (msec) and the step length used by that step.
     // dt (sec) of the step most recently passed to step(); waits only for the
     // previous step to finish, so one step stays queued on the device
+    int launchedDt(double* dt);
+    // Read the device clock after the last enqueued step (synchronises):
+    // routing time (msec) and the step length used by that step.
+    int readClock(double* newRoutingTime, double* lastDt, double* nextDt);
     // conduits updated by the timed iterations >= 1, and streaming conduits
     void timedWork(double* updated, double* hot);
-    int launchedDt(double* dt);
-    int readClock(double* newRoutingTime, double* lastDt, double* nextDt);
+    // Sum (op 0) or min (op 1) of n host doubles over the ranks (no-op on one GPU).
+    int allreduceHost(double* buf, int n, int op);
+    // this rank's partition (whole network when running on one GPU)
+    const Partition& partition() const;
     // Change the routing duration (msec) used for the end-of-run clamp.
     int setDuration(double msec);
     // Copy device state into the host mirror (prj.st); synchronises.

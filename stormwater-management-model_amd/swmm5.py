@@ -86,6 +86,10 @@ def load_library(path: str | None = None):
         "swmmx_getKernelBytes": (c_int, [P(c_dbl), c_int]),
         "swmmx_getBackend": (c_int, [ctypes.c_char_p, c_int]),
         "swmmx_setDevice": (c_int, [c_int]),
+        "swmmx_ncclUniqueId": (c_int, [ctypes.c_void_p, c_int]),
+        "swmmx_setPartition": (c_int, [c_int, c_int, ctypes.c_void_p, c_int]),
+        "swmmx_setExchange": (c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+        "swmmx_getOwner": (c_int, [c_int, P(c_int), c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -249,3 +253,44 @@ class SWMM:
 
     def set_device(self, ordinal: int):
         return self.L.swmmx_setDevice(int(ordinal))
+
+    # ---- multi-GPU (include/swmm5_mi355x.h) ----------------------------------
+    def nccl_unique_id(self) -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        n = self.L.swmmx_ncclUniqueId(buf, 128)
+        if n <= 0:
+            raise RuntimeError("ncclGetUniqueId failed (%d)" % n)
+        return buf.raw[:n]
+
+    def set_partition(self, rank: int, nranks: int, nccl_id: bytes | None = None):
+        if nccl_id is None:
+            return self.L.swmmx_setPartition(int(rank), int(nranks), None, 0)
+        buf = ctypes.create_string_buffer(nccl_id, len(nccl_id))
+        return self.L.swmmx_setPartition(int(rank), int(nranks), buf, len(nccl_id))
+
+    def set_exchange(self, fn):
+        """fn(array: numpy float64 view, op: 0 sum / 1 min) -> None, reducing in
+        place over the ranks; None restores RCCL.  The ctypes trampoline is kept
+        alive on this object."""
+        if fn is None:
+            self._xchg = None
+            return self.L.swmmx_setExchange(None, None)
+        import numpy as np
+        CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_long,
+                              ctypes.c_int, ctypes.c_void_p)
+
+        def tramp(buf, n, op, user):
+            try:
+                fn(np.ctypeslib.as_array(buf, shape=(n,)), op)
+                return 0
+            except Exception:           # noqa: BLE001 -- reported as an engine error
+                return 1
+        self._xchg = CB(tramp)
+        return self.L.swmmx_setExchange(ctypes.cast(self._xchg, ctypes.c_void_p), None)
+
+    def owners(self, obj_type: int):
+        import numpy as np
+        n = self.getCount(obj_type)
+        a = (ctypes.c_int * max(n, 1))()
+        self.L.swmmx_getOwner(obj_type, a, n)
+        return np.array(a[:n], dtype=np.int32)

@@ -1,0 +1,69 @@
+"""Worker process for tests/test_multigpu.py (test infrastructure).
+
+Runs the engine on one rank of a partitioned network.  Transport:
+  host  -- swmmx_setExchange with a gloo all-reduce callback (works with all
+           ranks on one GPU, which RCCL refuses)
+  rccl  -- RCCL (one rank only on a one-GPU box: exercises the captured
+           ncclAllReduce path)
+Writes the owned part of the final state to an .npz.
+
+usage: python _mgpu_worker.py INP STEPS OUT.npz TRANSPORT     (env: RANK, WORLD_SIZE, MASTER_*)
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "stormwater-management-model_amd"))
+
+import swmm5  # noqa: E402
+
+
+def main():
+    inp, steps, out, transport = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    s = swmm5.SWMM()
+    if transport == "host":
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+        def xchg(arr, op):
+            t = torch.from_numpy(arr)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MIN)
+
+        s.set_partition(rank, world)
+        s.set_exchange(xchg)
+    else:
+        assert world == 1
+        s.set_partition(0, 1, s.nccl_unique_id())
+    tag = os.path.join(os.path.dirname(out), "r%d" % rank)
+    assert s.open(inp, tag + ".rpt", tag + ".out") == 0, s.getError()
+    assert s.start(False) == 0, s.getError()
+    err, _ = s.run_steps(steps)
+    assert err == 0, s.getError()
+    c = s.counters()
+    res = {
+        "node_owner": s.owners(swmm5.NODE),
+        "link_owner": s.owners(swmm5.LINK),
+        "counters": np.array([c["steps"], c["iterations"], c["nonconverged"]]),
+    }
+    for f in ("newDepth", "newVolume", "inflow", "outflow", "overflow"):
+        res["node." + f] = s.get_array("node." + f)
+    for f in ("newFlow", "newDepth", "newVolume", "froude", "a1", "q1"):
+        res["link." + f] = s.get_array("link." + f)
+    s.end()
+    _, ferr, _ = s.getMassBalErr()
+    res["flow_error"] = np.array([ferr])
+    s.close()
+    np.savez(out, **res)
+    if transport == "host":
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

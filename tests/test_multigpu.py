@@ -1,0 +1,217 @@
+"""Multi-GPU partitioned routing (include/swmm5_mi355x.h).
+
+CPU (no GPU needed):
+  * owner rules of the partition (node blocks, conduit -> node1's rank,
+    outfall -> its conduit's rank) checked against a numpy restatement;
+  * world_size-2 gloo run of the exchange arithmetic: each rank sums its own
+    conduits' contributions to the shared nodes (the owner adds the node's own
+    inflow), one all_reduce, and the result equals the whole-network sums.
+GPU:
+  * 2 ranks on the one GPU with the host (gloo) transport against the same
+    network on one GPU: owned node / link state within rtol 1e-9 (only the
+    shared nodes' sums are reassociated), same iteration counts;
+  * 1 rank through the RCCL path (captured ncclAllReduce): bitwise equal to
+    the single-GPU engine.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import netgen
+import swmm5
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+WORKER = os.path.join(HERE, "_mgpu_worker.py")
+
+
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _grid(tmp_path, nx=24, ny=20, **kw):
+    inp = str(tmp_path / "g.inp")
+    kw.setdefault("end_time", "02:00:00")
+    netgen.write_grid(inp, nx, ny, **kw)
+    return inp
+
+
+def _topology(inp, tmp_path):
+    s = swmm5.SWMM()
+    assert s.open(inp, str(tmp_path / "t.rpt"), str(tmp_path / "t.out")) == 0
+    assert s.start_host() == 0
+    dump = str(tmp_path / "t.bin")
+    s.export_state(dump)
+    s.close()
+    from _dumpio import read_dump
+    return read_dump(dump)
+
+
+def _owners(inp, tmp_path, rank, world):
+    s = swmm5.SWMM()
+    s.set_partition(rank, world)
+    try:
+        assert s.open(inp, str(tmp_path / "o.rpt"), str(tmp_path / "o.out")) == 0
+        return s.owners(swmm5.NODE), s.owners(swmm5.LINK)
+    finally:
+        s.close()
+        s.set_partition(0, 1)
+
+
+def _ref_owners(n1, n2, ntype, nN, world):
+    node = (np.arange(nN, dtype=np.int64) * world // nN).astype(np.int32)
+    link = node[n1].copy()
+    OUTFALL = 1
+    for j in range(len(n1)):
+        if ntype[n2[j]] == OUTFALL:
+            node[n2[j]] = link[j]
+        elif ntype[n1[j]] == OUTFALL:
+            node[n1[j]] = link[j]
+    return node, link
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_partition_owner_rules(world, tmp_path):
+    inp = _grid(tmp_path)
+    d = _topology(inp, tmp_path)
+    n1, n2 = d["link.node1"].astype(int), d["link.node2"].astype(int)
+    ntype = d["node.type"].astype(int)
+    ref_node, ref_link = _ref_owners(n1, n2, ntype, len(ntype), world)
+    for rank in (0, world - 1):
+        node, link = _owners(inp, tmp_path, rank, world)
+        np.testing.assert_array_equal(node, ref_node)
+        np.testing.assert_array_equal(link, ref_link)
+    # every rank owns a contiguous strip of rows and about 1/world of the conduits
+    counts = np.bincount(ref_link, minlength=world)
+    assert counts.min() > 0.5 * len(n1) / world
+
+
+def _decompose_worker(rank, world, port, n1, n2, q, lat, node_owner, link_owner, outq):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    nN = len(lat)
+    # the kernels' rules: owner adds the node's lateral inflow, each rank adds
+    # its own conduits (link-index order), shared sums are all-reduced
+    inflow = np.where((node_owner == rank) & (lat >= 0), lat, 0.0)
+    outflow = np.where((node_owner == rank) & (lat < 0), -lat, 0.0)
+    for j in np.nonzero(link_owner == rank)[0]:
+        a, b, f = n1[j], n2[j], q[j]
+        if f >= 0:
+            outflow[a] += f
+            inflow[b] += f
+        else:
+            inflow[a] -= f
+            outflow[b] -= f
+    buf = torch.from_numpy(np.concatenate([inflow, outflow]))
+    dist.all_reduce(buf)
+    outq.put((rank, buf.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_exchange_sums_gloo_world2(tmp_path):
+    import torch.multiprocessing as mp
+    inp = _grid(tmp_path)
+    d = _topology(inp, tmp_path)
+    n1, n2 = d["link.node1"].astype(int), d["link.node2"].astype(int)
+    ntype = d["node.type"].astype(int)
+    nN, nL = len(ntype), len(n1)
+    rng = np.random.default_rng(20250215)
+    q = rng.normal(0.0, 1.0, nL)
+    lat = np.abs(rng.normal(0.0, 0.1, nN))
+    world = 2
+    node_owner, link_owner = _ref_owners(n1, n2, ntype, nN, world)
+    ctx = mp.get_context("spawn")
+    outq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_decompose_worker,
+                         args=(r, world, port, n1, n2, q, lat, node_owner, link_owner, outq))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(outq.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # whole-network sums (serial, link order)
+    inflow = np.where(lat >= 0, lat, 0.0)
+    outflow = np.where(lat < 0, -lat, 0.0)
+    for j in range(nL):
+        a, b, f = n1[j], n2[j], q[j]
+        if f >= 0:
+            outflow[a] += f
+            inflow[b] += f
+        else:
+            inflow[a] -= f
+            outflow[b] -= f
+    for r in range(world):
+        np.testing.assert_allclose(res[r][:nN], inflow, rtol=1e-13, atol=1e-13)
+        np.testing.assert_allclose(res[r][nN:], outflow, rtol=1e-13, atol=1e-13)
+    np.testing.assert_array_equal(res[0], res[1])      # every replica sees the same sums
+
+
+def _run_workers(inp, steps, tmp_path, world, transport, tag):
+    port = _free_port()
+    procs = []
+    outs = []
+    for r in range(world):
+        out = str(tmp_path / ("%s_r%d.npz" % (tag, r)))
+        outs.append(out)
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, WORKER, inp, str(steps), out, transport],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    for p in procs:
+        o, _ = p.communicate(timeout=600)
+        assert p.returncode == 0, o.decode()[-3000:]
+    return [dict(np.load(o)) for o in outs]
+
+
+def _merge(parts):
+    node = {k: np.zeros_like(v) for k, v in parts[0].items() if k.startswith("node.")}
+    link = {k: np.zeros_like(v) for k, v in parts[0].items() if k.startswith("link.")}
+    for r, part in enumerate(parts):
+        nm = part["node_owner"] == r
+        lm = part["link_owner"] == r
+        for k in node:
+            node[k][nm] = part[k][nm]
+        for k in link:
+            link[k][lm] = part[k][lm]
+    return node, link
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [dict(route_step=1.0),
+                                dict(route_step=5.0, variable_step=0.75, diameter=1.0, q=0.1)])
+def test_two_ranks_match_one_gpu(kw, tmp_path):
+    inp = _grid(tmp_path, 30, 30, **kw)
+    steps = 120
+    one = _run_workers(inp, steps, tmp_path, 1, "host", "one")[0]
+    parts = _run_workers(inp, steps, tmp_path, 2, "host", "two")
+    node, link = _merge(parts)
+    for k, v in node.items():
+        np.testing.assert_allclose(v, one[k], rtol=1e-9, atol=1e-12, err_msg=k)
+    for k, v in link.items():
+        np.testing.assert_allclose(v, one[k], rtol=1e-9, atol=1e-12, err_msg=k)
+    for part in parts:
+        np.testing.assert_array_equal(part["counters"], one["counters"])
+        assert abs(part["flow_error"][0] - one["flow_error"][0]) < 1e-3
+
+
+@pytest.mark.gpu
+def test_rccl_single_rank_bitwise(tmp_path):
+    inp = _grid(tmp_path, 30, 30, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.1)
+    one = _run_workers(inp, 80, tmp_path, 1, "host", "plain")[0]
+    rc = _run_workers(inp, 80, tmp_path, 1, "rccl", "rccl")[0]
+    for k in one:
+        if k.startswith(("node.", "link.")):
+            np.testing.assert_array_equal(rc[k], one[k], err_msg=k)
+    np.testing.assert_array_equal(rc["counters"], one["counters"])
