@@ -104,6 +104,8 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=12)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--timing-steps", type=int, default=10)
+    ap.add_argument("--exchange", choices=["rccl", "host"], default="rccl",
+                    help="multi-GPU transport (host = gloo through the host: rehearsal on one GPU)")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per link-momentum launch from rocprofv3 PMC (profiles/)")
     args = ap.parse_args()
@@ -144,6 +146,11 @@ def main():
             idt = torch.frombuffer(bytearray(s.nccl_unique_id().ljust(128, b"\0")), dtype=torch.uint8)
         dist.broadcast(idt, 0)
         s.set_partition(rank, world, bytes(idt.numpy().tobytes()))
+        if args.exchange == "host":
+            def xchg(arr, op):
+                t = torch.from_numpy(arr)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MIN)
+            s.set_exchange(xchg)
     tmpd = "/tmp/swmm_bench"
     err = s.open(inp, os.path.join(tmpd, "r%d.rpt" % rank), os.path.join(tmpd, "r%d.out" % rank))
     if err:
