@@ -58,6 +58,12 @@ int    DLLEXPORT swmmx_getKernelTimes(double *out, int n);
  * or the model value for a full launch when nothing has been timed. */
 int    DLLEXPORT swmmx_getKernelBytes(double *out, int n);
 
+/* Average duration (microseconds) of `reps` back-to-back launches of one
+ * kernel on the live state: which = 0 link momentum of Picard iteration 0,
+ * 1 node update of iteration 0.  Measurement only: it advances the state, so
+ * call it after the run being measured. */
+int    DLLEXPORT swmmx_timeKernel(int which, int reps, double *avgUs);
+
 /* Name of the compute backend ("hip:gfx950:<device name>" or "none"). */
 int    DLLEXPORT swmmx_getBackend(char *buf, int size);
 

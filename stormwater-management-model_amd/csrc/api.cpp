@@ -859,6 +859,13 @@ int DLLEXPORT swmmx_getBackend(char* buf, int size)
     return 0;
 }
 
+int DLLEXPORT swmmx_timeKernel(int which, int reps, double* avgUs)
+{
+    if (!G || !G->router || !G->router->ok() || !avgUs) return 502;
+    G->mirrorValid = false;
+    return G->router->timeKernel(which, reps, avgUs);
+}
+
 int DLLEXPORT swmmx_ncclUniqueId(void* out, int bytes)
 {
     if (!out || bytes < (int)sizeof(ncclUniqueId)) return -1;

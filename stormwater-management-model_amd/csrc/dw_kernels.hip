@@ -2067,6 +2067,37 @@ void Router::setTiming(bool on)
     d_->workSum = 0;
 }
 
+// Back-to-back replays of one kernel between two events (average duration per
+// launch, dispatch gaps amortised).  The kernels run on the live state; this
+// is a measurement tool (bench.py calls it after the timed run).
+int Router::timeKernel(int which, int reps, double* avgUs)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    Params p = d->p;
+    p.countWork = 0;
+    hipEvent_t a, b;
+    HIPCHECK(hipEventCreate(&a));
+    HIPCHECK(hipEventCreate(&b));
+    HIPCHECK(hipStreamSynchronize(d->stream));
+    HIPCHECK(hipEventRecord(a, d->stream));
+    for (int r = 0; r < reps; r++) {
+        if (which == 0)
+            hipLaunchKernelGGL(linkKernel(true, d->linkWaves, d->fastLinks), dim3(d->gridL), dim3(kBlock), 0,
+                               d->stream, p, 0);
+        else
+            hipLaunchKernelGGL(k_node<true>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, 0);
+    }
+    HIPCHECK(hipEventRecord(b, d->stream));
+    HIPCHECK(hipEventSynchronize(b));
+    float ms = 0;
+    HIPCHECK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *avgUs = 1000.0 * ms / std::max(reps, 1);
+    return 0;
+}
+
 const Partition& Router::partition() const { return d_->part; }
 
 int Router::allreduceHost(double* buf, int n, int op)

@@ -47,6 +47,9 @@ public:
     void timedWork(double* updated, double* hot);
     // Sum (op 0) or min (op 1) of n host doubles over the ranks (no-op on one GPU).
     int allreduceHost(double* buf, int n, int op);
+    // average duration (us) of `reps` back-to-back launches of kernel `which`
+    // (0 k_link<first>, 1 k_node<first>) on the live state -- measurement only
+    int timeKernel(int which, int reps, double* avgUs);
     // this rank's partition (whole network when running on one GPU)
     const Partition& partition() const;
     // Change the routing duration (msec) used for the end-of-run clamp.

@@ -86,6 +86,7 @@ def load_library(path: str | None = None):
         "swmmx_getKernelBytes": (c_int, [P(c_dbl), c_int]),
         "swmmx_getBackend": (c_int, [ctypes.c_char_p, c_int]),
         "swmmx_setDevice": (c_int, [c_int]),
+        "swmmx_timeKernel": (c_int, [c_int, c_int, P(c_dbl)]),
         "swmmx_ncclUniqueId": (c_int, [ctypes.c_void_p, c_int]),
         "swmmx_setPartition": (c_int, [c_int, c_int, ctypes.c_void_p, c_int]),
         "swmmx_setExchange": (c_int, [ctypes.c_void_p, ctypes.c_void_p]),
@@ -250,6 +251,13 @@ class SWMM:
         buf = ctypes.create_string_buffer(256)
         self.L.swmmx_getBackend(buf, 256)
         return buf.value.decode()
+
+    def time_kernel(self, which: int, reps: int = 20) -> float:
+        v = ctypes.c_double(0.0)
+        rc = self.L.swmmx_timeKernel(int(which), int(reps), ctypes.byref(v))
+        if rc:
+            raise RuntimeError("swmmx_timeKernel failed (%d)" % rc)
+        return v.value
 
     def set_device(self, ordinal: int):
         return self.L.swmmx_setDevice(int(ordinal))
