@@ -97,6 +97,98 @@ CD(a1) CD(a2) CD(q1) CD(q2) CD(evapLossRate) CD(seepLossRate)
 CI(barrels) CI(hasLosses) CI(fullState) CI(capacityLimited) CI(superCritical)
 
 static int NP = 0;
+
+/* ---- run statistics (stats.c exportable arrays, read before swmm_end) ---- */
+extern TNodeStats* NodeStats;
+extern TLinkStats* LinkStats;
+extern TOutfallStats* OutfallStats;
+extern double MaxOutfallFlow;
+extern double RoutingTimeSpan;
+#define NSD(f) static double nsd_##f(int j) { return NodeStats[j].f; }
+#define LSD(f) static double lsd_##f(int j) { return LinkStats[j].f; }
+NSD(avgDepth) NSD(maxDepth) NSD(maxDepthDate) NSD(maxRptDepth) NSD(volFlooded) NSD(timeFlooded)
+NSD(timeSurcharged) NSD(timeCourantCritical) NSD(totLatFlow) NSD(maxLatFlow) NSD(maxInflow)
+NSD(maxOverflow) NSD(maxPondedVol) NSD(maxInflowDate) NSD(maxOverflowDate)
+static double nsd_nonConvergedCount(int j) { return NodeStats[j].nonConvergedCount; }
+LSD(maxFlow) LSD(maxFlowDate) LSD(maxVeloc) LSD(maxDepth) LSD(timeNormalFlow) LSD(timeInletControl)
+LSD(timeSurcharged) LSD(timeFullUpstream) LSD(timeFullDnstream) LSD(timeFullFlow)
+LSD(timeCapacityLimited) LSD(timeCourantCritical)
+static double lsd_flowTurns(int j) { return (double)LinkStats[j].flowTurns; }
+static double lsd_flowTurnSign(int j) { return (double)LinkStats[j].flowTurnSign; }
+static int StatClass = 0;
+static double lsd_timeInFlowClass(int j) { return LinkStats[j].timeInFlowClass[StatClass]; }
+static double osd_avgFlow(int j) { return Node[j].type == OUTFALL ? OutfallStats[Node[j].subIndex].avgFlow : 0.0; }
+static double osd_maxFlow(int j) { return Node[j].type == OUTFALL ? OutfallStats[Node[j].subIndex].maxFlow : 0.0; }
+static double osd_totalPeriods(int j) { return Node[j].type == OUTFALL ? OutfallStats[Node[j].subIndex].totalPeriods : 0.0; }
+static int StatPollut = 0;
+static double osd_totalLoad(int j)
+{
+    return (Node[j].type == OUTFALL && OutfallStats[Node[j].subIndex].totalLoad)
+        ? OutfallStats[Node[j].subIndex].totalLoad[StatPollut] : 0.0;
+}
+
+static void writeStats(void)
+{
+    int nn = Nobjects[NODE], nl = Nobjects[LINK], k, p;
+    Series* s;
+    /* one-shot series written as plain records (count = N) */
+#define ONE_N(NM, fn) do { NSer = 0; pushd(NM, nn, fn); rec(Ser[0].name, 'd', Ser[0].used, Ser[0].d); free(Ser[0].d); } while (0)
+#define ONE_L(NM, fn) do { NSer = 0; pushd(NM, nl, fn); rec(Ser[0].name, 'd', Ser[0].used, Ser[0].d); free(Ser[0].d); } while (0)
+    memset(Ser, 0, sizeof Ser);
+    ONE_N("st.node.avgDepth", nsd_avgDepth);
+    ONE_N("st.node.maxDepth", nsd_maxDepth);
+    ONE_N("st.node.maxDepthDate", nsd_maxDepthDate);
+    ONE_N("st.node.maxRptDepth", nsd_maxRptDepth);
+    ONE_N("st.node.volFlooded", nsd_volFlooded);
+    ONE_N("st.node.timeFlooded", nsd_timeFlooded);
+    ONE_N("st.node.timeSurcharged", nsd_timeSurcharged);
+    ONE_N("st.node.timeCourantCritical", nsd_timeCourantCritical);
+    ONE_N("st.node.totLatFlow", nsd_totLatFlow);
+    ONE_N("st.node.maxLatFlow", nsd_maxLatFlow);
+    ONE_N("st.node.maxInflow", nsd_maxInflow);
+    ONE_N("st.node.maxInflowDate", nsd_maxInflowDate);
+    ONE_N("st.node.maxOverflow", nsd_maxOverflow);
+    ONE_N("st.node.maxOverflowDate", nsd_maxOverflowDate);
+    ONE_N("st.node.maxPondedVol", nsd_maxPondedVol);
+    ONE_N("st.node.nonConvergedCount", nsd_nonConvergedCount);
+    ONE_N("st.outfall.avgFlow", osd_avgFlow);
+    ONE_N("st.outfall.maxFlow", osd_maxFlow);
+    ONE_N("st.outfall.totalPeriods", osd_totalPeriods);
+    for (p = 0; p < NP; p++) {
+        char nm[48];
+        StatPollut = p;
+        snprintf(nm, sizeof nm, "st.outfall.totalLoad%d", p);
+        ONE_N(nm, osd_totalLoad);
+    }
+    ONE_L("st.link.maxFlow", lsd_maxFlow);
+    ONE_L("st.link.maxFlowDate", lsd_maxFlowDate);
+    ONE_L("st.link.maxVeloc", lsd_maxVeloc);
+    ONE_L("st.link.maxDepth", lsd_maxDepth);
+    ONE_L("st.link.timeNormalFlow", lsd_timeNormalFlow);
+    ONE_L("st.link.timeInletControl", lsd_timeInletControl);
+    ONE_L("st.link.timeSurcharged", lsd_timeSurcharged);
+    ONE_L("st.link.timeFullUpstream", lsd_timeFullUpstream);
+    ONE_L("st.link.timeFullDnstream", lsd_timeFullDnstream);
+    ONE_L("st.link.timeFullFlow", lsd_timeFullFlow);
+    ONE_L("st.link.timeCapacityLimited", lsd_timeCapacityLimited);
+    ONE_L("st.link.timeCourantCritical", lsd_timeCourantCritical);
+    ONE_L("st.link.flowTurns", lsd_flowTurns);
+    ONE_L("st.link.flowTurnSign", lsd_flowTurnSign);
+    for (k = 0; k < MAX_FLOW_CLASSES; k++) {
+        char nm[48];
+        StatClass = k;
+        snprintf(nm, sizeof nm, "st.link.timeInFlowClass%d", k);
+        ONE_L(nm, lsd_timeInFlowClass);
+    }
+    {
+        double sys[2] = { MaxOutfallFlow, RoutingTimeSpan };
+        rec("st.sys", 'd', 2, sys);
+    }
+    (void)s;
+#undef ONE_N
+#undef ONE_L
+}
+
 static double nq_buf(int j) { return 0.0; }
 
 static void pushState(void)
@@ -247,6 +339,7 @@ int main(int argc, char** argv)
         int nc[2] = { (int)NonConvergeCount, (int)TotalStepCount };
         rec("run.counts", 'i', 2, nc);
     }
+    writeStats();
     swmm_end();
     swmm_getMassBalErr(&e1, &e2, &e3);
     {

@@ -656,6 +656,38 @@ long DLLEXPORT swmmx_getArray(const char* name, double* dst, long n)
     ARR("link.seepRate", net.seepRate) ARR("link.length", net.length) ARR("link.roughness", net.roughness)
     ARR("link.modLength", net.modLength) ARR("link.roughFactor", net.roughFactor) ARR("link.slope", net.slope)
     ARR("link.beta", net.beta) ARR("link.qMax", net.qMax) ARR("link.qFull", net.qFull)
+    if (k.compare(0, 5, "stat.") == 0) {          // run statistics (stats.c), device accumulators
+        if (G->router && G->router->ok() && G->router->downloadStats(prj))
+            return -1;
+        RunStats& R = prj.stats;
+        ARR("stat.node.avgDepth", R.avgDepth) ARR("stat.node.maxDepth", R.maxDepth)
+        ARR("stat.node.maxDepthDate", R.maxDepthDate) ARR("stat.node.maxRptDepth", R.maxRptDepth)
+        ARR("stat.node.volFlooded", R.volFlooded) ARR("stat.node.timeFlooded", R.timeFlooded)
+        ARR("stat.node.timeSurcharged", R.timeSurcharged)
+        ARR("stat.node.timeCourantCritical", R.timeCourantCritical) ARR("stat.node.totLatFlow", R.totLatFlow)
+        ARR("stat.node.maxLatFlow", R.maxLatFlow) ARR("stat.node.maxInflow", R.maxInflow)
+        ARR("stat.node.maxInflowDate", R.maxInflowDate) ARR("stat.node.maxOverflow", R.maxOverflow)
+        ARR("stat.node.maxOverflowDate", R.maxOverflowDate) ARR("stat.node.maxPondedVol", R.maxPondedVol)
+        ARR("stat.node.nonConvergedCount", R.nonConvergedCount)
+        ARR("stat.node.inflowVolume", R.nodeInflowVol) ARR("stat.node.outflowVolume", R.nodeOutflowVol)
+        ARR("stat.outfall.avgFlow", R.outfallAvgFlow) ARR("stat.outfall.maxFlow", R.outfallMaxFlow)
+        ARR("stat.outfall.totalPeriods", R.outfallPeriods) ARR("stat.outfall.totalLoad", R.outfallLoad)
+        ARR("stat.link.maxFlow", R.lMaxFlow) ARR("stat.link.maxFlowDate", R.lMaxFlowDate)
+        ARR("stat.link.maxVeloc", R.lMaxVeloc) ARR("stat.link.maxDepth", R.lMaxDepth)
+        ARR("stat.link.timeNormalFlow", R.lTimeNormalFlow) ARR("stat.link.timeSurcharged", R.lTimeSurcharged)
+        ARR("stat.link.timeFullUpstream", R.lTimeFullUpstream)
+        ARR("stat.link.timeFullDnstream", R.lTimeFullDnstream) ARR("stat.link.timeFullFlow", R.lTimeFullFlow)
+        ARR("stat.link.timeCapacityLimited", R.lTimeCapacityLimited)
+        ARR("stat.link.timeInFlowClass", R.lTimeInFlowClass)
+        ARR("stat.link.timeCourantCritical", R.lTimeCourantCritical)
+        ARR("stat.link.flowTurns", R.lFlowTurns) ARR("stat.link.flowTurnSign", R.lFlowTurnSign)
+        if (k == "stat.sys") {
+            tmp = {R.reportStepCount, R.routingTimeSpan, R.maxOutfallFlow, R.minTimeStep, R.maxTimeStep,
+                   R.routingTime, R.steadyStateTime, R.timeStepCount, R.trialsCount};
+            for (int j = 0; j < RunStats::kLevels; j++) tmp.push_back(R.timeStepCounts[j]);
+            v = &tmp;
+        }
+    }
 #undef ARR
     auto fromInt = [&](const std::vector<int>& iv) { tmp.assign(iv.begin(), iv.end()); v = &tmp; };
     if (k == "node.type") fromInt(net.nodeType);

@@ -50,9 +50,15 @@ namespace swx {
 
 constexpr int kBlock = 256;
 constexpr int kMaxTrialsCap = 32;
-constexpr int kNumPartials = 8;
+// per-block partials written by k_step_end: [0] outflow [1] flooding [2] extra
+// external inflow [3] evap [4] seep (sums), [5] link Courant step [6] node
+// Courant step (min, with their first-occurrence indices in [8] [9]),
+// [7] system outfall flow (sum)
+constexpr int kNumPartials = 10;
+__host__ __device__ inline bool partialIsMin(int q) { return q == 5 || q == 6; }
+constexpr int kTimeLevels = 6;     // TIMELEVELS (objects.h:941)
 constexpr int kDtRing = 4;          // host-mapped per-step dt ring (k_finalize -> host)
-constexpr int kLinkWavesDefault = 3;   // measured best on MI355X   // per-block partial sums written by k_step_end
+constexpr int kLinkWavesDefault = 3;   // measured best on MI355X
 
 // ---- packed per-link flags -------------------------------------------------
 enum : uint32_t {
@@ -77,6 +83,7 @@ enum : uint32_t {
     NF_CANPOND = 1u << 6,
     NF_SHARED = 1u << 7,          // multi-GPU: touched by conduits of several ranks
     NF_REPLICA = 1u << 8,         // multi-GPU: replica of a node another rank owns
+    NF_DEG0 = 1u << 9,            // degree 0 (no outflow link; massbal.c:622)
 };
 // ---- packed link state word ------------------------------------------------
 // bits 0-3 flowClass, 4-7 fullState code (0 / 8 / 9 / 10), 8 normalFlow,
@@ -101,6 +108,32 @@ struct StepCtl {
     double routeStep;                 // fixed step (sec)
     unsigned long long linkWork[kMaxTrialsCap];   // timing mode: conduits updated per iteration
     double stepRed[kNumPartials];     // this step's reduced block partials (k_finalize)
+    // run statistics (stats.c): report-period step count / span, max system
+    // outfall flow, routing time-step statistics (stats_updateTimeStepStats)
+    double statsStart;                // ReportStart (DateTime)
+    double dateBase, dateSecs0;       // floor(StartDateTime), its time of day (sec)
+    long long reportStepCount;
+    double routingTimeSpan, maxOutfallFlow;
+    double tsMin, tsMax, tsRoutingTime, tsSteadyTime;
+    long long tsCount, tsTrials;
+    long long tsCounts[kTimeLevels];
+    double tsIntervals[kTimeLevels];
+};
+
+// device run statistics (stats.c TNodeStats / TLinkStats / TOutfallStats and
+// massbal.c NodeInflow / NodeOutflow), one SoA array per field
+struct StatsDev {
+    double *avgDepth, *maxDepth, *maxDepthDate, *volFlooded, *timeFlooded, *timeSurch;
+    double *timeCourant, *totLat, *maxLat, *maxInflow, *maxInflowDate, *maxOverflow;
+    double *maxOverflowDate, *maxPonded;
+    int* nonConv;
+    double *mbIn, *mbOut, *mbPendIn, *mbPendOut;      // node volume totals + pending rates
+    double *oAvgFlow, *oMaxFlow, *oLoad;               // outfalls ([p][node] loads)
+    int* oPeriods;
+    double *lMaxFlow, *lMaxFlowDate, *lMaxVeloc, *lMaxDepth, *lTimeNormal, *lTimeSurch;
+    double *lTimeFullUp, *lTimeFullDn, *lTimeFullFlow, *lTimeCapLim, *lTimeClass, *lTimeCourant;
+    int *lTurns, *lTurnSign;
+    const double* qFull;
 };
 
 struct Params {
@@ -139,6 +172,8 @@ struct Params {
     const double* gTables;        // global copy of the 5x51 circular tables
     double* partials;             // [nBlocksEnd][kNumPartials]
     int nBlocksEnd;
+    StatsDev st;
+    int multi;                    // partitioned (multi-GPU) run
     int countWork;                // timing mode: count updated conduits per iteration
     // multi-GPU exchange (partition.h): per local node its global shared slot
     // (-1 if interior); partial sums {inflow, outflow, surfArea, sumdqdh} of
@@ -940,17 +975,63 @@ __global__ __launch_bounds__(kBlock) void k_qual_link(Params p)
     }
 }
 
+// combine two partial vectors (sums; mins keep the first occurrence)
+__device__ __forceinline__ void combinePartials(double* a, const double* b)
+{
+    for (int q = 0; q < kNumPartials; q++) {
+        if (q == 8 || q == 9) continue;
+        if (partialIsMin(q)) {
+            if (b[q] < a[q] || (b[q] == a[q] && b[q + 3] < a[q + 3])) { a[q] = b[q]; a[q + 3] = b[q + 3]; }
+        } else {
+            a[q] += b[q];
+        }
+    }
+}
+
+// link_getVelocity (link.c:809-830) for a conduit
+template <bool kFast>
+__device__ __forceinline__ double conduitVelocity(const Params& p, int j, uint32_t f, double q, double depth,
+                                                  const double* ct)
+{
+    if (depth <= 0.01) return 0.0;
+    double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
+    q /= barrels;
+    Geom x = loadGeom<kFast>(p, j, f);
+    double area = getAofY(x, depth, ct);
+    return (area > 0.0001) ? q / area : 0.0;
+}
+
 // Step end: findLimitedLinks (dynwave.c:349-378), removeConduitLosses /
 // removeOutflows (routing.c:841-925, node.c:438-493), Courant partials
-// (dynwave.c:836-921).  Block partials:
-//   [0] outflow rate  [1] flooding rate  [2] extra external inflow
-//   [3] evap loss     [4] seep loss      [5] min link step  [6] min node step
+// (dynwave.c:836-921), run statistics (stats_updateFlowStats, stats.c:449-752)
+// and the per-node volume totals (massbal_updateRoutingTotals, massbal.c:619-633).
+// Block partials: see kNumPartials.
+template <bool kFast>
 __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
 {
     __shared__ double red[kNumPartials][kBlock / 64];
+    __shared__ double ct[5 * SWX_CIRC_N];
+    stageTables(ct, p.gTables);
     double acc[kNumPartials];
     for (int q = 0; q < kNumPartials; q++) acc[q] = 0.0;
-    double tLink = p.routeStep, tNode = p.routeStep;
+    acc[5] = p.routeStep; acc[8] = 1.0e300;
+    acc[6] = p.routeStep; acc[9] = 1.0e300;
+    StepCtl* c = p.ctl;
+    const double dt = c->dt;
+    const double half = dt / 2.;
+    // date at the end of this step (getDateTime(NewRoutingTime), swmm5.c:1543)
+    const double tEnd = c->newRoutingTime + 1000.0 * c->dt;
+    const double aDate = c->dateBase + (c->dateSecs0 + (tEnd + 1) / 1000.0) / 86400.0;
+    const bool stats = !(aDate < c->statsStart);
+    // convergence of this step (dynwave.c:242-257): nodes count non-convergence
+    bool converged;
+    if (p.maxTrials <= 1) converged = false;
+    else {
+        int steps = 2;
+        while (steps < p.maxTrials && c->unconv[steps - 1]) steps++;
+        converged = (c->unconv[steps - 1] == 0);
+    }
+    const StatsDev& S = p.st;
     int n = gridDim.x * kBlock;
     int tid = blockIdx.x * kBlock + threadIdx.x;
     // links (fixed order within a thread: j = tid, tid + n, ...)
@@ -966,17 +1047,49 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
             if ((h1 - h2) > fabs(p.slope[j]) * p.length[j]) s |= (1 << 9);
         }
         p.lstate[j] = s;
-        acc[3] += p.evapLoss[j] * barrels;
-        acc[4] += p.seepLoss[j] * barrels;
+        if (f & LF_SEEP) {
+            acc[3] += p.evapLoss[j] * barrels;
+            acc[4] += p.seepLoss[j] * barrels;
+        }
+        double newFlow = p.lNewFlow[j];
         if (p.varStep) {
-            double q = fabs(p.lNewFlow[j]) / barrels;
+            double q = fabs(newFlow) / barrels;
             double fr = p.froude[j];
             if (!(q <= 0.0001 || a1 <= 0.0001 || fr <= 0.01)) {
                 double t = p.lNewVolume[j] / barrels / q;
                 t = t * p.modLength[j] / p.length[j];
                 t = t * fr / (1.0 + fr) * p.courantFactor;
-                if (t < tLink) tLink = t;
+                if (t < acc[5]) { acc[5] = t; acc[8] = (double)j; }
             }
+        }
+        if (stats) {                                       // stats_updateLinkStats
+            double dq = newFlow - p.lOldFlow[j];
+            double q = fabs(newFlow);
+            if (q > S.lMaxFlow[j]) { S.lMaxFlow[j] = q; S.lMaxFlowDate[j] = aDate; }
+            double depth = p.lNewDepth[j];
+            double v = (f & LF_COLD) ? conduitVelocity<false>(p, j, f, q, depth, ct)
+                                     : conduitVelocity<kFast>(p, j, f, q, depth, ct);
+            if (v > S.lMaxVeloc[j]) S.lMaxVeloc[j] = v;
+            if (depth > S.lMaxDepth[j]) S.lMaxDepth[j] = depth;
+            if (s & (1 << 8)) S.lTimeNormal[j] += dt;
+            int fc = s & 0xF;
+            if (fc < 7) S.lTimeClass[(size_t)fc * p.nL + j] += dt;
+            if (q >= S.qFull[j] * barrels) S.lTimeFullFlow[j] += dt;
+            if (s & (1 << 9)) S.lTimeCapLim[j] += dt;
+            int fs = (s >> 4) & 0xF;
+            if (fs == FS_ALL_FULL) {
+                S.lTimeSurch[j] += dt;
+                S.lTimeFullUp[j] += dt;
+                S.lTimeFullDn[j] += dt;
+            } else if (fs == FS_UP_FULL) {
+                S.lTimeFullUp[j] += dt;
+            } else if (fs == FS_DN_FULL) {
+                S.lTimeFullDn[j] += dt;
+            }
+            int k = S.lTurnSign[j];
+            int sg = (dq < 0) ? -1 : 1;
+            S.lTurnSign[j] = sg;
+            if (fabs(dq) > 0.001 && k * sg < 0) S.lTurns[j] += 1;
         }
     }
     for (int i = tid; i < p.nN; i += n) {
@@ -1003,39 +1116,88 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
         } else {
             acc[2] += -q;
         }
+        double newDepth = p.nNewDepth[i];
         if (p.varStep && type != OUTFALL) {
-            double y = p.nNewDepth[i];
+            double y = newDepth;
             double yc = p.crownElev[i] - p.invert[i];
             if (!(y <= 0.0001) && !(y + 0.0001 >= yc)) {
                 double maxDepth = yc * 0.25;
                 double d = p.dYdT[i];
                 if (!(maxDepth < 0.0001) && !(d < 0.0001)) {
                     double t1 = maxDepth / d;
-                    if (t1 < tNode) tNode = t1;
+                    if (t1 < acc[6]) { acc[6] = t1; acc[9] = (double)i; }
                 }
             }
         }
+        // per-node volume totals: the pending half step (state at the end of
+        // the previous step) then this step's end state, each over dt/2
+        double inflow = p.inflow[i], outflow = p.outflow[i], overflow = p.overflow[i];
+        double newVolume = p.nNewVolume[i], fullVolume = p.fullVolume[i];
+        {
+            double in = S.mbIn[i], out = S.mbOut[i];
+            in += S.mbPendIn[i] * half;
+            out += S.mbPendOut[i] * half;
+            double ovfPrev = S.mbPendOut[p.nN + i];
+            out += ovfPrev * half;
+            double o1, o2;
+            if (type == OUTFALL || (nf & NF_DEG0)) { o1 = inflow; o2 = 0.0; }
+            else { o1 = outflow; o2 = (newVolume <= fullVolume) ? overflow : 0.0; }
+            in += inflow * half;
+            out += o1 * half;
+            out += o2 * half;
+            S.mbIn[i] = in;
+            S.mbOut[i] = out;
+            S.mbPendIn[i] = inflow;
+            S.mbPendOut[i] = o1;
+            S.mbPendOut[p.nN + i] = o2;
+        }
+        if (!converged && !p.conv[i]) S.nonConv[i] += 1;  // stats_updateConvergenceStats
+        if (!stats) continue;
+        // stats_updateNodeStats (stats.c:543-643)
+        S.avgDepth[i] += newDepth;
+        if (newDepth > S.maxDepth[i]) { S.maxDepth[i] = newDepth; S.maxDepthDate[i] = aDate; }
+        if (type != OUTFALL) {
+            if (newVolume > fullVolume || overflow > 0.0) {
+                S.timeFlooded[i] += dt;
+                S.volFlooded[i] += overflow * dt;
+                if (nf & NF_CANPOND) S.maxPonded[i] = gmax(S.maxPonded[i], (newVolume - fullVolume));
+            }
+            if (newDepth + p.invert[i] + 0.0001 >= p.crownElev[i]) S.timeSurch[i] += dt;
+        } else {
+            if (inflow >= 0.001) {
+                S.oAvgFlow[i] += inflow;
+                S.oMaxFlow[i] = gmax(S.oMaxFlow[i], inflow);
+                S.oPeriods[i] += 1;
+            }
+            for (int pp = 0; pp < p.P; pp++)
+                S.oLoad[(size_t)pp * p.nN + i] += inflow * p.nNewQual[(size_t)pp * p.nN + i] * dt;
+            acc[7] += inflow;
+        }
+        double newLat = p.newLat[i];
+        S.totLat[i] += ((p.oldLat[i] + newLat) * 0.5 * dt);
+        if (fabs(newLat) > fabs(S.maxLat[i])) S.maxLat[i] = newLat;
+        if (inflow > S.maxInflow[i]) { S.maxInflow[i] = inflow; S.maxInflowDate[i] = aDate; }
+        if (overflow > S.maxOverflow[i]) { S.maxOverflow[i] = overflow; S.maxOverflowDate[i] = aDate; }
     }
-    acc[5] = tLink;
-    acc[6] = tNode;
     // wave reduction (fixed butterfly order), then wave partials in LDS
     int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int q = 0; q < kNumPartials; q++) {
-        double v = acc[q];
-        for (int off = 32; off > 0; off >>= 1) {
-            double o = __shfl_down(v, off, 64);
-            if (q == 5 || q == 6) v = (o < v) ? o : v; else v += o;
-        }
-        if (lane == 0) red[q][wv] = v;
+    for (int off = 32; off > 0; off >>= 1) {
+        double o[kNumPartials];
+        for (int q = 0; q < kNumPartials; q++) o[q] = __shfl_down(acc[q], off, 64);
+        if (lane + off < 64) combinePartials(acc, o);
     }
+    if (lane == 0)
+        for (int q = 0; q < kNumPartials; q++) red[q][wv] = acc[q];
     __syncthreads();
-    if (threadIdx.x < kNumPartials) {
-        int q = threadIdx.x;
-        double v = red[q][0];
+    if (threadIdx.x == 0) {
+        double v[kNumPartials];
+        for (int q = 0; q < kNumPartials; q++) v[q] = red[q][0];
         for (int w = 1; w < kBlock / 64; w++) {
-            if (q == 5 || q == 6) v = (red[q][w] < v) ? red[q][w] : v; else v += red[q][w];
+            double o[kNumPartials];
+            for (int q = 0; q < kNumPartials; q++) o[q] = red[q][w];
+            combinePartials(v, o);
         }
-        p.partials[(size_t)blockIdx.x * kNumPartials + q] = v;
+        for (int q = 0; q < kNumPartials; q++) p.partials[(size_t)blockIdx.x * kNumPartials + q] = v[q];
     }
 }
 
@@ -1051,20 +1213,20 @@ __global__ void k_finalize(Params p)
     StepCtl* c = p.ctl;
     if (kPhase != 2) {
         double acc[kNumPartials];
-        for (int q = 0; q < kNumPartials; q++) acc[q] = (q == 5 || q == 6) ? 1.0e300 : 0.0;
-        for (int b = t; b < p.nBlocksEnd; b += kBlock)
-            for (int q = 0; q < kNumPartials; q++) {
-                double v = p.partials[(size_t)b * kNumPartials + q];
-                if (q == 5 || q == 6) acc[q] = (v < acc[q]) ? v : acc[q]; else acc[q] += v;
-            }
+        for (int q = 0; q < kNumPartials; q++) acc[q] = partialIsMin(q) || q == 8 || q == 9 ? 1.0e300 : 0.0;
+        for (int b = t; b < p.nBlocksEnd; b += kBlock) {
+            double v[kNumPartials];
+            for (int q = 0; q < kNumPartials; q++) v[q] = p.partials[(size_t)b * kNumPartials + q];
+            combinePartials(acc, v);
+        }
         for (int q = 0; q < kNumPartials; q++) sum[q][t] = acc[q];
         __syncthreads();
         for (int h = kBlock / 2; h > 0; h >>= 1) {      // fixed-shape tree: deterministic
             if (t < h) {
-                for (int q = 0; q < kNumPartials; q++) {
-                    double a = sum[q][t], b = sum[q][t + h];
-                    sum[q][t] = (q == 5 || q == 6) ? ((b < a) ? b : a) : a + b;
-                }
+                double a[kNumPartials], b[kNumPartials];
+                for (int q = 0; q < kNumPartials; q++) { a[q] = sum[q][t]; b[q] = sum[q][t + h]; }
+                combinePartials(a, b);
+                for (int q = 0; q < kNumPartials; q++) sum[q][t] = a[q];
             }
             __syncthreads();
         }
@@ -1097,6 +1259,27 @@ __global__ void k_finalize(Params p)
         c->flowTot[q] += step[q] * half;
         c->prevStepTot[q] = step[q];
     }
+    // run statistics of this step (routing.c:255-260): stats_updateFlowStats'
+    // system part and stats_updateTimeStepStats (stats.c:449-518)
+    {
+        double dt = c->dt;
+        double tEnd = c->newRoutingTime + 1000.0 * c->dt;
+        double aDate = c->dateBase + (c->dateSecs0 + (tEnd + 1) / 1000.0) / 86400.0;
+        if (!(aDate < c->statsStart)) {
+            c->reportStepCount += 1;
+            c->routingTimeSpan += dt;
+            c->maxOutfallFlow = gmax(c->maxOutfallFlow, tot[7]);
+        }
+        if (c->newRoutingTime > 0) {
+            c->tsMin = gmin(c->tsMin, dt);
+            for (int j = 1; j < kTimeLevels; j++)
+                if (dt >= c->tsIntervals[j]) { c->tsCounts[j] += 1; break; }
+        }
+        c->tsMax = gmax(c->tsMax, dt);
+        c->tsRoutingTime += dt;
+        c->tsCount += 1;
+        c->tsTrials += steps;
+    }
     // advance the clock (routing.c:301-302)
     c->newRoutingTime = c->newRoutingTime + 1000.0 * c->dt;
     // step length of the next step: dynwave_getRoutingStep (dynwave.c:195-220,
@@ -1105,6 +1288,12 @@ __global__ void k_finalize(Params p)
     if (p.varStep) {
         double tMin = tot[5];
         if (tot[6] < tMin) tMin = tot[6];
+        // getVariableStep's critical element (dynwave.c:815-828) -- counted
+        // when that next step will actually be routed (swmm5.c:531)
+        if (!p.multi && c->newRoutingTime < c->routingDuration) {
+            if (tot[6] < tot[5]) p.st.timeCourant[(int)tot[9]] += 1.0;
+            else if (tot[8] < 1.0e299) p.st.lTimeCourant[(int)tot[8]] += 1.0;
+        }
         if (tMin < p.minRouteStep) tMin = p.minRouteStep;
         c->variableStep = floor(1000.0 * tMin) / 1000.0;
         dtn = c->variableStep;
@@ -1289,7 +1478,8 @@ static void launchStep(Router::Impl* d)
         hipLaunchKernelGGL(k_qual_link, dim3(d->gridL), dim3(kBlock), 0, d->stream, p);
     }
     if (d->timing) (void)hipEventRecord(d->curEv[base + 1], d->stream);
-    hipLaunchKernelGGL(k_step_end, dim3(d->gridEnd), dim3(kBlock), 0, d->stream, p);
+    if (d->fastLinks) hipLaunchKernelGGL(k_step_end<true>, dim3(d->gridEnd), dim3(kBlock), 0, d->stream, p);
+    else hipLaunchKernelGGL(k_step_end<false>, dim3(d->gridEnd), dim3(kBlock), 0, d->stream, p);
     if (d->part.active() && p.varStep) {           // global Courant limits (min over ranks)
         hipLaunchKernelGGL(k_finalize<1>, dim3(1), dim3(kBlock), 0, d->stream, p);
         exchange(d, &p.ctl->stepRed[5], &p.ctl->stepRed[5], 2, 1);
@@ -1501,6 +1691,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (net.nodeType[g] == OUTFALL) f |= ((uint32_t)net.outfallType[g] & 0x7u) << NF_OTYPE_SHIFT;
         if (net.degree[g] < 0) f |= NF_DEGNEG;
         if (prj.opt.allowPonding && net.pondedArea[g] > 0.0) f |= NF_CANPOND;
+        if (net.degree[g] == 0) f |= NF_DEG0;
         if (part.sharedSlot[i] >= 0) { f |= NF_SHARED; sharedNodes.push_back(i); }
         if (!part.owned[i]) f |= NF_REPLICA;
         nflags[i] = (int)f;
@@ -1622,6 +1813,48 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     d->gridC = std::max(1, std::min((p.nCold + kBlock - 1) / kBlock, maxBlocks));
     d->gridEnd = std::max(1, std::min((std::max(nN, nL) + kBlock - 1) / kBlock, 2 * prop.multiProcessorCount));
     p.nBlocksEnd = d->gridEnd;
+    p.multi = part.active() ? 1 : 0;
+    // ---- run statistics (stats_open, stats.c:150-240; massbal_open NodeInflow) ----
+    {
+        StatsDev& S = p.st;
+        auto zN = [&](double v) { return std::vector<double>(nN, v); };
+        auto zL = [&](double v) { return std::vector<double>(nL, v); };
+        std::vector<double> z0 = zN(0.0), l0 = zL(0.0), dStart = zN(prj.opt.startDateTime);
+        for (double** a : {&S.avgDepth, &S.maxDepth, &S.volFlooded, &S.timeFlooded, &S.timeSurch,
+                           &S.timeCourant, &S.totLat, &S.maxLat, &S.maxInflow, &S.maxOverflow,
+                           &S.maxPonded, &S.oAvgFlow, &S.oMaxFlow})
+            UPD(*a, z0, nN);
+        for (double** a : {&S.maxDepthDate, &S.maxInflowDate, &S.maxOverflowDate}) UPD(*a, dStart, nN);
+        std::vector<int> iz(std::max(nN, nL), 0);
+        UPI(S.nonConv, iz, nN);
+        UPI(S.oPeriods, iz, nN);
+        UPI(S.lTurns, iz, nL);
+        UPI(S.lTurnSign, iz, nL);
+        for (double** a : {&S.lMaxFlow, &S.lMaxFlowDate, &S.lMaxVeloc, &S.lMaxDepth, &S.lTimeNormal,
+                           &S.lTimeSurch, &S.lTimeFullUp, &S.lTimeFullDn, &S.lTimeFullFlow,
+                           &S.lTimeCapLim, &S.lTimeCourant})
+            UPD(*a, l0, nL);
+        std::vector<double> cls((size_t)7 * nL, 0.0);
+        UPD(S.lTimeClass, cls, cls.size());
+        std::vector<double> ol((size_t)std::max(P, 1) * nN, 0.0);
+        UPD(S.oLoad, ol, ol.size());
+        UPD(tmp, gl(net.qFull), nL); S.qFull = tmp;
+        // per-node volume totals start from the initial volume; the pending
+        // half-step rates are the initial state's (massbal.c:239, 619-633)
+        std::vector<double> vin(nN), pin(nN), pout((size_t)2 * nN);
+        for (int i = 0; i < nN; i++) {
+            const int g = LN[i];
+            vin[i] = st.newVolume[g];
+            pin[i] = st.inflow[g];
+            bool passthru = net.nodeType[g] == OUTFALL || net.degree[g] == 0;
+            pout[i] = passthru ? st.inflow[g] : st.outflow[g];
+            pout[nN + i] = (!passthru && st.newVolume[g] <= net.fullVolume[g]) ? st.overflow[g] : 0.0;
+        }
+        UPD(S.mbIn, vin, nN);
+        UPD(S.mbOut, z0, nN);
+        UPD(S.mbPendIn, pin, nN);
+        UPD(S.mbPendOut, pout, pout.size());
+    }
     // ---- multi-GPU exchange ----------------------------------------------------
     p.nShared = (int)sharedNodes.size();
     p.xflag = 4 * part.nSharedGlobal;
@@ -1669,6 +1902,23 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     hc->latTot[0] = d->latTot0[0];
     hc->latTot[1] = d->latTot0[1];
     hc->latTot[2] = d->latTot0[2];
+    hc->statsStart = prj.opt.reportStart;
+    {
+        int h, m, sec;
+        decodeTime(prj.opt.startDateTime, &h, &m, &sec);
+        hc->dateBase = floor(prj.opt.startDateTime);
+        hc->dateSecs0 = 3600.0 * h + 60.0 * m + sec;       // datetime_addSeconds' operand order
+    }
+    // stats_open's time-step intervals (stats.c:288-312)
+    hc->tsMax = 0.0;
+    hc->tsMin = prj.opt.routeStep;
+    {
+        double lmax = log10(prj.opt.routeStep), lmin = log10(prj.opt.minRouteStep);
+        double delta = (lmax - lmin) / (double)(kTimeLevels - 1);
+        hc->tsIntervals[0] = prj.opt.routeStep;
+        for (int j = 1; j < kTimeLevels; j++) hc->tsIntervals[j] = pow(10., lmax - j * delta);
+        hc->tsIntervals[kTimeLevels - 1] = prj.opt.minRouteStep;
+    }
     HIPCHECK(hipMemcpy(d->ctl, d->hostCtl, sizeof(StepCtl), hipMemcpyHostToDevice));
     d->slotDoubles = (size_t)nN * (1 + P) + 8;
     d->pinnedSize = d->slotDoubles * Impl::kRing;
@@ -1975,6 +2225,115 @@ int Router::download(Project& prj)
     for (size_t i = 0; i < nN; i++)
         if (!multi || part.owned[i]) st.converged[multi ? part.lnode[i] : i] = cv[i];
     st.variableStep = d->hostCtl->variableStep;
+    return 0;
+}
+
+int Router::downloadStats(Project& prj)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    const Params& p = d->p;
+    const StatsDev& S = p.st;
+    const Partition& part = d->part;
+    const bool multi = part.active();
+    RunStats& R = prj.stats;
+    const size_t nN = p.nN, nL = p.nL, gN = prj.net.nNodes(), gL = prj.net.nLinks();
+    std::vector<double> tmp;
+    std::vector<int> itmp;
+    auto node = [&](std::vector<double>& out, const double* src) -> hipError_t {
+        out.assign(gN, 0.0);
+        tmp.resize(nN);
+        hipError_t e = hipMemcpy(tmp.data(), src, nN * sizeof(double), hipMemcpyDeviceToHost);
+        for (size_t i = 0; i < nN; i++)
+            if (!multi || part.owned[i]) out[multi ? part.lnode[i] : i] = tmp[i];
+        return e;
+    };
+    auto nodeI = [&](std::vector<double>& out, const int* src) -> hipError_t {
+        out.assign(gN, 0.0);
+        itmp.resize(nN);
+        hipError_t e = hipMemcpy(itmp.data(), src, nN * sizeof(int), hipMemcpyDeviceToHost);
+        for (size_t i = 0; i < nN; i++)
+            if (!multi || part.owned[i]) out[multi ? part.lnode[i] : i] = itmp[i];
+        return e;
+    };
+    auto link = [&](std::vector<double>& out, const double* src, size_t rows) -> hipError_t {
+        out.assign(rows * gL, 0.0);
+        tmp.resize(rows * nL);
+        hipError_t e = hipMemcpy(tmp.data(), src, rows * nL * sizeof(double), hipMemcpyDeviceToHost);
+        for (size_t r = 0; r < rows; r++)
+            for (size_t j = 0; j < nL; j++) out[r * gL + (multi ? part.llink[j] : j)] = tmp[r * nL + j];
+        return e;
+    };
+    auto linkI = [&](std::vector<double>& out, const int* src) -> hipError_t {
+        out.assign(gL, 0.0);
+        itmp.resize(nL);
+        hipError_t e = hipMemcpy(itmp.data(), src, nL * sizeof(int), hipMemcpyDeviceToHost);
+        for (size_t j = 0; j < nL; j++) out[multi ? part.llink[j] : j] = itmp[j];
+        return e;
+    };
+    HIPCHECK(hipStreamSynchronize(d->stream));
+    HIPCHECK(node(R.avgDepth, S.avgDepth));
+    HIPCHECK(node(R.maxDepth, S.maxDepth));
+    HIPCHECK(node(R.maxDepthDate, S.maxDepthDate));
+    HIPCHECK(node(R.volFlooded, S.volFlooded));
+    HIPCHECK(node(R.timeFlooded, S.timeFlooded));
+    HIPCHECK(node(R.timeSurcharged, S.timeSurch));
+    HIPCHECK(node(R.timeCourantCritical, S.timeCourant));
+    HIPCHECK(node(R.totLatFlow, S.totLat));
+    HIPCHECK(node(R.maxLatFlow, S.maxLat));
+    HIPCHECK(node(R.maxInflow, S.maxInflow));
+    HIPCHECK(node(R.maxInflowDate, S.maxInflowDate));
+    HIPCHECK(node(R.maxOverflow, S.maxOverflow));
+    HIPCHECK(node(R.maxOverflowDate, S.maxOverflowDate));
+    HIPCHECK(node(R.maxPondedVol, S.maxPonded));
+    HIPCHECK(nodeI(R.nonConvergedCount, S.nonConv));
+    HIPCHECK(node(R.nodeInflowVol, S.mbIn));
+    HIPCHECK(node(R.nodeOutflowVol, S.mbOut));
+    HIPCHECK(node(R.outfallAvgFlow, S.oAvgFlow));
+    HIPCHECK(node(R.outfallMaxFlow, S.oMaxFlow));
+    HIPCHECK(nodeI(R.outfallPeriods, S.oPeriods));
+    {
+        size_t P = p.P;
+        R.outfallLoad.assign(P * gN, 0.0);
+        if (P) {
+            tmp.resize(P * nN);
+            HIPCHECK(hipMemcpy(tmp.data(), S.oLoad, P * nN * sizeof(double), hipMemcpyDeviceToHost));
+            for (size_t q = 0; q < P; q++)
+                for (size_t i = 0; i < nN; i++)
+                    if (!multi || part.owned[i]) R.outfallLoad[q * gN + (multi ? part.lnode[i] : i)] = tmp[q * nN + i];
+        }
+    }
+    HIPCHECK(link(R.lMaxFlow, S.lMaxFlow, 1));
+    HIPCHECK(link(R.lMaxFlowDate, S.lMaxFlowDate, 1));
+    HIPCHECK(link(R.lMaxVeloc, S.lMaxVeloc, 1));
+    HIPCHECK(link(R.lMaxDepth, S.lMaxDepth, 1));
+    HIPCHECK(link(R.lTimeNormalFlow, S.lTimeNormal, 1));
+    HIPCHECK(link(R.lTimeSurcharged, S.lTimeSurch, 1));
+    HIPCHECK(link(R.lTimeFullUpstream, S.lTimeFullUp, 1));
+    HIPCHECK(link(R.lTimeFullDnstream, S.lTimeFullDn, 1));
+    HIPCHECK(link(R.lTimeFullFlow, S.lTimeFullFlow, 1));
+    HIPCHECK(link(R.lTimeCapacityLimited, S.lTimeCapLim, 1));
+    HIPCHECK(link(R.lTimeInFlowClass, S.lTimeClass, RunStats::kClasses));
+    HIPCHECK(link(R.lTimeCourantCritical, S.lTimeCourant, 1));
+    HIPCHECK(linkI(R.lFlowTurns, S.lTurns));
+    HIPCHECK(linkI(R.lFlowTurnSign, S.lTurnSign));
+    HIPCHECK(hipMemcpy(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost));
+    const StepCtl* c = d->hostCtl;
+    R.reportStepCount = (double)c->reportStepCount;
+    R.routingTimeSpan = c->routingTimeSpan;
+    R.maxOutfallFlow = c->maxOutfallFlow;
+    R.minTimeStep = c->tsMin;
+    R.maxTimeStep = c->tsMax;
+    R.routingTime = c->tsRoutingTime;
+    R.steadyStateTime = c->tsSteadyTime;
+    R.timeStepCount = (double)c->tsCount;
+    R.trialsCount = (double)c->tsTrials;
+    for (int j = 0; j < RunStats::kLevels; j++) {
+        R.timeStepCounts[j] = (double)c->tsCounts[j];
+        R.timeStepIntervals[j] = c->tsIntervals[j];
+    }
+    if (R.maxRptDepth.size() != gN) R.maxRptDepth.assign(gN, 0.0);   // host side (saveResults)
+    R.valid = true;
     return 0;
 }
 

@@ -181,4 +181,26 @@ struct State {
     double variableStep = 0.0;
 };
 
+// Run statistics (stats.c TNodeStats / TLinkStats / TOutfallStats, the
+// routing time-step statistics, massbal.c NodeInflow / NodeOutflow), host copy
+// of the device accumulators (Router::downloadStats).  Node / link indexed.
+struct RunStats {
+    static constexpr int kClasses = 7;       // MAX_FLOW_CLASSES
+    static constexpr int kLevels = 6;        // TIMELEVELS
+    std::vector<double> avgDepth, maxDepth, maxDepthDate, maxRptDepth, volFlooded, timeFlooded,
+        timeSurcharged, timeCourantCritical, totLatFlow, maxLatFlow, maxInflow, maxInflowDate,
+        maxOverflow, maxOverflowDate, maxPondedVol, nonConvergedCount;
+    std::vector<double> nodeInflowVol, nodeOutflowVol;           // NodeInflow / NodeOutflow
+    std::vector<double> outfallAvgFlow, outfallMaxFlow, outfallPeriods, outfallLoad;   // load [p][node]
+    std::vector<double> lMaxFlow, lMaxFlowDate, lMaxVeloc, lMaxDepth, lTimeNormalFlow,
+        lTimeSurcharged, lTimeFullUpstream, lTimeFullDnstream, lTimeFullFlow, lTimeCapacityLimited,
+        lTimeInFlowClass, lTimeCourantCritical, lFlowTurns, lFlowTurnSign;   // class: [k][link]
+    double reportStepCount = 0, routingTimeSpan = 0, maxOutfallFlow = 0;
+    double minTimeStep = 0, maxTimeStep = 0, routingTime = 0, steadyStateTime = 0;
+    double timeStepCount = 0, trialsCount = 0;
+    double timeStepCounts[kLevels] = {0, 0, 0, 0, 0, 0};
+    double timeStepIntervals[kLevels] = {0, 0, 0, 0, 0, 0};
+    bool valid = false;
+};
+
 }  // namespace swx

@@ -117,6 +117,8 @@ int OutFile::saveResults(Project& prj, double reportTime, double oldT, double ne
     double f1 = 1.0 - f;
     buf_.resize(std::max(nNodeVars_, nLinkVars_));
     float* x = buf_.data();
+    std::vector<double>& rpt = prj.stats.maxRptDepth;
+    if ((int)rpt.size() != nn) rpt.assign(nn, 0.0);
     for (int j = 0; j < nn; j++) {              // node_getResults node.c:497-528
         double z = (f1 * s.oldDepth[j] + f * s.newDepth[j]) * uL;
         x[0] = (float)z;
@@ -135,6 +137,8 @@ int OutFile::saveResults(Project& prj, double reportTime, double oldT, double ne
             x[6 + p] = (float)z;
         }
         if (net.rptFlag[j]) fwrite(x, 4, nNodeVars_, f_);
+        // stats_updateMaxNodeDepth (stats.c:436-445) with the reported value
+        rpt[j] = (rpt[j] >= (double)x[0]) ? rpt[j] : (double)x[0];
         sysr[12] += x[2];
     }
     for (int j = 0; j < nl; j++) {              // link_getResults link.c:674-724

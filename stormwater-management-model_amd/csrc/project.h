@@ -34,6 +34,7 @@ public:
     ReportFlags rpt;
     Network net;
     State st;
+    RunStats stats;                        // filled by Router::downloadStats
     std::vector<int> rptNodes, rptLinks;   // explicit [REPORT] lists
     int errorCode = 0;
     std::string errorMsg;

@@ -56,6 +56,8 @@ public:
     int setDuration(double msec);
     // Copy device state into the host mirror (prj.st); synchronises.
     int download(Project& prj);
+    // Copy the run statistics accumulators into prj.stats; synchronises.
+    int downloadStats(Project& prj);
     // Upload the host mirror's dynamic state (after swmm_setValue edits).
     int upload(Project& prj);
     int sync();

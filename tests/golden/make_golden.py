@@ -9,7 +9,10 @@ For every case it writes the input file (<case>.inp, produced by the
 deterministic generators in stormwater-management-model_amd/netgen.py) and
 <case>.npz: the reference's static parameters, its state right after
 swmm_start and its full-precision state after every `every`-th routing step
-(oracle/refdump.c reads them from the reference's exported globals).
+(oracle/refdump.c reads them from the reference's exported globals), plus
+the run statistics (NodeStats / LinkStats / OutfallStats, "st.*") after the
+last step, the reference's binary results (<case>.ref_out.npy) and its report
+file (<case>.ref_rpt.txt).
 """
 import os
 import subprocess
@@ -60,6 +63,9 @@ def make(name):
     with open(tmp + ".out", "rb") as f:
         out = f.read()
     np.save(os.path.join(HERE, name + ".ref_out.npy"), np.frombuffer(out, dtype=np.uint8))
+    # the reference's report file (summary tables after swmm_report)
+    with open(tmp + ".rpt") as f, open(os.path.join(HERE, name + ".ref_rpt.txt"), "w") as g:
+        g.write(f.read())
     print(name, len(d["s.dt"]), "steps", os.path.getsize(os.path.join(HERE, name + ".npz")), "bytes")
 
 

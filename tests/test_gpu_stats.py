@@ -1,0 +1,92 @@
+"""Run statistics (stats.c / massbal.c per-node totals) against the reference.
+
+The reference's accumulators (NodeStats, LinkStats, OutfallStats, read by
+oracle/refdump.c after the last step, "st.*" in the golden fixtures) are
+compared with the engine's device accumulators (swmmx_getArray "stat.*").
+
+Tolerances: accumulated values within rtol 1e-6 (the north_star tolerance);
+quantities that count time steps in a discrete class (time surcharged, time
+in a flow class, ...) may differ by a few steps where the two builds' libm
+ulps put a state on different sides of a class boundary; dates of maxima
+must agree for >= 97 % of objects (a plateau of equal maxima can move the
+first occurrence by one step).
+"""
+import numpy as np
+import pytest
+
+import _golden
+import swmm5
+
+RTOL, ATOL = 1e-6, 1e-9
+
+
+def _run(name, tmp_path):
+    d = _golden.load(name)
+    s = swmm5.SWMM()
+    assert s.open(_golden.inp(name), str(tmp_path / "s.rpt"), str(tmp_path / "s.out")) == 0
+    assert s.start(True) == 0, s.getError()
+    while True:
+        err, t = s.step()
+        assert err == 0, s.getError()
+        if t == 0.0:
+            break
+    return d, s
+
+
+def _dates_agree(a, b, frac=0.97):
+    same = np.isclose(a, b, rtol=0, atol=1e-9)
+    assert same.mean() >= frac, (same.mean(), np.nonzero(~same)[0][:10])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", _golden.CASES)
+def test_stats_match_reference(name, tmp_path):
+    d, s = _run(name, tmp_path)
+    dtmax = float(np.max(d["s.dt"]))
+    g = lambda k: s.get_array(k)                      # noqa: E731
+    for f in ("avgDepth", "maxDepth", "totLatFlow", "maxLatFlow", "maxInflow", "maxOverflow",
+              "volFlooded", "maxPondedVol"):
+        np.testing.assert_allclose(g("stat.node." + f), d["st.node." + f], rtol=RTOL, atol=ATOL,
+                                   err_msg=f)
+    for f in ("timeFlooded", "timeSurcharged"):
+        np.testing.assert_allclose(g("stat.node." + f), d["st.node." + f], rtol=0, atol=3 * dtmax + 1e-9,
+                                   err_msg=f)
+    np.testing.assert_array_equal(g("stat.node.nonConvergedCount"), d["st.node.nonConvergedCount"])
+    for f in ("maxDepthDate", "maxInflowDate"):
+        _dates_agree(g("stat.node." + f), d["st.node." + f])
+    for f in ("avgFlow", "maxFlow"):
+        np.testing.assert_allclose(g("stat.outfall." + f), d["st.outfall." + f], rtol=RTOL, atol=ATOL,
+                                   err_msg=f)
+    np.testing.assert_allclose(g("stat.outfall.totalPeriods"), d["st.outfall.totalPeriods"], atol=2)
+    P = int(d["counts"][2])
+    if P:
+        nn = int(d["counts"][0])
+        load = g("stat.outfall.totalLoad").reshape(P, nn)
+        for p in range(P):
+            np.testing.assert_allclose(load[p], d["st.outfall.totalLoad%d" % p], rtol=1e-6, atol=1e-6)
+    for f in ("maxFlow", "maxVeloc", "maxDepth"):
+        np.testing.assert_allclose(g("stat.link." + f), d["st.link." + f], rtol=RTOL, atol=ATOL,
+                                   err_msg=f)
+    _dates_agree(g("stat.link.maxFlowDate"), d["st.link.maxFlowDate"])
+    for f in ("timeNormalFlow", "timeSurcharged", "timeFullUpstream", "timeFullDnstream", "timeFullFlow",
+              "timeCapacityLimited"):
+        np.testing.assert_allclose(g("stat.link." + f), d["st.link." + f], rtol=0, atol=3 * dtmax + 1e-9,
+                                   err_msg=f)
+    nl = int(d["counts"][1])
+    cls = g("stat.link.timeInFlowClass").reshape(7, nl)
+    for k in range(7):
+        np.testing.assert_allclose(cls[k], d["st.link.timeInFlowClass%d" % k], rtol=0,
+                                   atol=3 * dtmax + 1e-9, err_msg="class %d" % k)
+    np.testing.assert_allclose(g("stat.link.flowTurns"), d["st.link.flowTurns"], atol=2)
+    sysv = g("stat.sys")
+    np.testing.assert_allclose(sysv[2], d["st.sys"][0], rtol=RTOL)   # MaxOutfallFlow
+    np.testing.assert_allclose(sysv[1], d["st.sys"][1], rtol=1e-12)  # RoutingTimeSpan
+    # Courant-critical counts (variable step only): same total, same leaders
+    crit_n = g("stat.node.timeCourantCritical")
+    crit_l = g("stat.link.timeCourantCritical")
+    ref_n, ref_l = d["st.node.timeCourantCritical"], d["st.link.timeCourantCritical"]
+    assert abs(crit_n.sum() + crit_l.sum() - ref_n.sum() - ref_l.sum()) <= 1
+    np.testing.assert_allclose(crit_n, ref_n, atol=3)
+    np.testing.assert_allclose(crit_l, ref_l, atol=3)
+    s.end()
+    s.close()
