@@ -1811,7 +1811,8 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     d->gridL = resident((const void*)linkKernel(false, d->linkWaves, d->fastLinks), nL);
     d->gridN = resident((const void*)k_node<false>, nN);
     d->gridC = std::max(1, std::min((p.nCold + kBlock - 1) / kBlock, maxBlocks));
-    d->gridEnd = std::max(1, std::min((std::max(nN, nL) + kBlock - 1) / kBlock, 2 * prop.multiProcessorCount));
+    d->gridEnd = resident(d->fastLinks ? (const void*)k_step_end<true> : (const void*)k_step_end<false>,
+                          std::max(nN, nL));
     p.nBlocksEnd = d->gridEnd;
     p.multi = part.active() ? 1 : 0;
     // ---- run statistics (stats_open, stats.c:150-240; massbal_open NodeInflow) ----
