@@ -20,6 +20,7 @@
 #include "../../include/swmm5_mi355x.h"
 #include "output.h"
 #include "project.h"
+#include "report.h"
 #include "router.h"
 #include "xsect.h"
 
@@ -310,45 +311,32 @@ static double computeFlowError()   // massbal.c:858-902
     return pct;
 }
 
-static void writeReportSummary()
+static void writeReportSummary()   // massbal_report + stats_report (swmm5.c:628-632)
 {
-    FILE* f = G->rpt;
-    if (!f || G->prj->rpt.disabled) return;
+    if (!G->rpt || G->prj->rpt.disabled) return;
     Project& prj = *G->prj;
-    double uV = prj.ucfVolume();
-    double* T = G->flowTot;
-    const double ac = prj.opt.unitSystem ? 1.0e4 : 43560.0;   // acre-ft or ha-m volume units
-    const double mg = prj.opt.unitSystem ? 1.0e3 : 7.48052e-6 * 1.0e6 / 1.0e6 * 1.0;
-    (void)mg;
-    double vcf = prj.opt.unitSystem ? 1.0e-4 : 1.0 / 43560.0;   // ft3 -> ac-ft / m3 -> ha-m
-    auto line = [&](const char* name, double v) {
-        fprintf(f, "  %-27s %9.3f\n", name, v * uV * vcf);
-    };
-    (void)ac;
-    fprintf(f, "\n  **************************\n");
-    fprintf(f, "  Flow Routing Continuity     %s\n", prj.opt.unitSystem ? "hectare-m" : "acre-feet");
-    fprintf(f, "  **************************  ---------\n");
-    line("Dry Weather Inflow .......", T[0]);
-    line("Wet Weather Inflow .......", 0.0);
-    line("Groundwater Inflow .......", 0.0);
-    line("RDII Inflow ..............", 0.0);
-    line("External Inflow ..........", T[1]);
-    line("External Outflow .........", T[3]);
-    line("Flooding Loss ............", T[2]);
-    line("Evaporation Loss .........", T[4]);
-    line("Exfiltration Loss ........", T[5]);
-    line("Initial Stored Volume ....", G->initStorage);
-    line("Final Stored Volume ......", G->finalStorage);
-    fprintf(f, "  Continuity Error (%%) ..... %9.3f\n", G->flowError);
     long long iters = 0, nonConv = 0;
     int last = 0;
     G->router->counters(&iters, &nonConv, &last);
-    long long steps = G->totalStepCount > 0 ? G->totalStepCount : 1;
-    fprintf(f, "\n  *************************\n  Routing Time Step Summary\n  *************************\n");
-    fprintf(f, "  Average Iterations per Step : %8.2f\n", (double)iters / (double)steps);
-    fprintf(f, "  %% of Steps Not Converging   : %8.2f\n", 100.0 * (double)nonConv / (double)steps);
-    std::string dev = G->router->deviceName();
-    fprintf(f, "  Routing device              : %s\n", dev.c_str());
+    if (G->router->partition().active()) {
+        // statistics are per rank (owned objects); the tables need all of them
+        fprintf(G->rpt, "\n  Summary tables are written by single-GPU runs only (rank %d of %d).\n",
+                G->router->partition().rank, G->router->partition().nranks);
+        return;
+    }
+    if (G->router->downloadStats(prj)) return;
+    const double* T = G->flowTot;         // dw, ex, flooding, outflow, evap, seep
+    ReportTotals t;
+    t.dwInflow = T[0];
+    t.exInflow = T[1];
+    t.flooding = T[2];
+    t.outflow = T[3];
+    t.evapLoss = T[4];
+    t.seepLoss = T[5];
+    t.initStorage = G->initStorage;
+    t.finalStorage = G->finalStorage;
+    t.pctError = G->flowError;
+    writeRunReport(G->rpt, prj, t, nonConv);
 }
 
 int DLLEXPORT swmm_end(void)   // swmm5.c:618-660

@@ -1,0 +1,446 @@
+// report.cpp -- end-of-run report tables (see report.h).
+//
+// Table layouts follow the reference's report file: massbal_report
+// (report.c:737-798), stats_report (stats.c:342-365, 756-863, report.c:923-1112)
+// and statsrpt_writeReport (statsrpt.c:87-865).  Each line is written as
+// "\n  <text>", the reference's report_writeLine convention.
+#include "report.h"
+
+#include <cmath>
+#include <cstdarg>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace swx {
+namespace {
+
+const char* const kFlowWords[] = {"CFS", "GPM", "MGD", "CMS", "LPS", "MLD"};
+const char* const kNodeWords[] = {"JUNCTION", "OUTFALL", "STORAGE", "DIVIDER"};
+const char* const kLinkWords[] = {"CONDUIT", "PUMP", "ORIFICE", "WEIR", "OUTLET"};
+const char* const kVolWords[] = {"10^6 gal", "10^6 ltr"};
+const char* const kVolWords2[] = {"gal", "ltr"};
+const char* const kPondWords[] = {"Feet", "Meters"};
+const char* const kLoadWords[] = {"lbs", "kg", "LogN"};
+constexpr double kUcfLandArea[2] = {2.2956e-5, 0.92903e-5};   // swmm5.c Ucf[LANDAREA]
+constexpr double kMgdPerCfs = 0.64632, kMldPerCfs = 2.4466, kSecsPerDayRpt = 86400.0;
+constexpr double kLperFt3 = 28.317;
+constexpr int kMaxStats = 5;
+constexpr double kMaxFlowBalanceErr = 10.0;
+
+class Writer {
+public:
+    explicit Writer(FILE* f) : f_(f) {}
+    void line(const char* s) { std::fprintf(f_, "\n  %s", s); }
+    void blank() { line(""); }
+    void title(const char* t)              // three-line starred title
+    {
+        std::string stars(std::strlen(t), '*');
+        blank();
+        line(stars.c_str());
+        line(t);
+        line(stars.c_str());
+    }
+    void printf(const char* fmt, ...) __attribute__((format(printf, 2, 3)))
+    {
+        va_list ap;
+        va_start(ap, fmt);
+        std::vfprintf(f_, fmt, ap);
+        va_end(ap);
+    }
+private:
+    FILE* f_;
+};
+
+struct Ranked {                            // TMaxStats (objects.h)
+    int objType = 0;                       // 0 node, 1 link
+    int index = -1;
+    double value = -1.0;
+};
+
+// stats_updateMaxStats (stats.c:841-863): keep the kMaxStats largest |value|
+void rankInsert(Ranked* top, int objType, int index, double x)
+{
+    Ranked cand{objType, index, x};
+    for (int k = 0; k < kMaxStats; k++)
+        if (std::fabs(cand.value) > std::fabs(top[k].value)) std::swap(cand, top[k]);
+}
+
+// getElapsedTime (swmm5.c:1518-1540), measured from the report start
+void elapsed(double date, double reportStart, int* days, int* hrs, int* mins)
+{
+    double x = date - reportStart;
+    if (x <= 0.0) { *days = *hrs = *mins = 0; return; }
+    *days = (int)x;
+    int secs;
+    decodeTime(x, hrs, mins, &secs);
+}
+
+}  // namespace
+
+void writeRunReport(FILE* f, Project& prj, const ReportTotals& tot, long long nonConvergeCount)
+{
+    if (!f || prj.rpt.disabled) return;
+    Writer w(f);
+    const Network& net = prj.net;
+    RunStats& R = prj.stats;
+    const Options& o = prj.opt;
+    const int us = o.unitSystem ? 1 : 0;
+    const int nN = net.nNodes(), nL = net.nLinks(), P = o.ignoreQuality ? 0 : net.nPollut();
+    const double ucfL = prj.ucfLength(), ucfQ = prj.ucfFlow();
+    const char* flowFmt = (o.flowUnits == MGD || o.flowUnits == CMS) ? "%9.3f" : "%9.2f";
+    const double vcf = us ? 28.317 / 1.0e6 : 7.48 / 1.0e6;
+    const double rptStart = o.reportStart;
+
+    // ---- flow routing continuity (report_writeFlowError) ------------------
+    if (tot.pctError > kMaxFlowBalanceErr || prj.rpt.continuity) {
+        double ucf1 = ucfL * kUcfLandArea[us];
+        double ucf2 = (us ? kMldPerCfs : kMgdPerCfs) / kSecsPerDayRpt;
+        w.blank();
+        w.printf("\n  **************************        Volume        Volume");
+        w.printf(us ? "\n  Flow Routing Continuity        hectare-m      10^6 ltr"
+                    : "\n  Flow Routing Continuity        acre-feet      10^6 gal");
+        w.printf("\n  **************************     ---------     ---------");
+        const struct { const char* name; double v; } rows[] = {
+            {"Dry Weather Inflow .......", tot.dwInflow},  {"Wet Weather Inflow .......", tot.wwInflow},
+            {"Groundwater Inflow .......", tot.gwInflow},  {"RDII Inflow ..............", tot.iiInflow},
+            {"External Inflow ..........", tot.exInflow},  {"External Outflow .........", tot.outflow},
+            {"Flooding Loss ............", tot.flooding},  {"Evaporation Loss .........", tot.evapLoss},
+            {"Exfiltration Loss ........", tot.seepLoss},  {"Initial Stored Volume ....", tot.initStorage},
+            {"Final Stored Volume ......", tot.finalStorage}};
+        for (const auto& r : rows) w.printf("\n  %s%14.3f%14.3f", r.name, r.v * ucf1, r.v * ucf2);
+        w.printf("\n  Continuity Error (%%) .....%14.3f", tot.pctError);
+        w.blank();
+    }
+
+    // the final stored volume closes each node's balance (massbal.c:649-653)
+    for (int j = 0; j < nN; j++) R.nodeOutflowVol[j] += prj.st.newVolume[j];
+
+    // ---- accuracy statistics (stats_findMaxStats) -------------------------
+    Ranked turns[kMaxStats], balErr[kMaxStats], nonConv[kMaxStats], courant[kMaxStats];
+    for (auto& r : nonConv) r.value = 0.0;
+    if (R.reportStepCount > 2) {
+        double z = 100.0 / (2. / 3. * (R.reportStepCount - 2.));
+        for (int j = 0; j < nL; j++) rankInsert(turns, 1, j, R.lFlowTurns[j] * z);
+    }
+    for (int j = 0; j < nN; j++) {
+        if (net.degree[j] <= 0) continue;
+        double in = R.nodeInflowVol[j], out = R.nodeOutflowVol[j];
+        if (in <= 0.1) continue;
+        double x = (in > 0.0) ? 1.0 - out / in : (out > 0.0 ? -1.0 : 0.0);
+        rankInsert(balErr, 0, j, 100.0 * x);
+    }
+    const double stepCount = R.timeStepCount;
+    for (int j = 0; j < nN; j++) rankInsert(nonConv, 0, j, R.nonConvergedCount[j] / stepCount);
+    const bool varStep = o.courantFactor != 0.0;
+    if (varStep && stepCount != 0) {
+        for (int j = 0; j < nN; j++) rankInsert(courant, 0, j, 100.0 * (R.timeCourantCritical[j] / stepCount));
+        for (int j = 0; j < nL; j++) rankInsert(courant, 1, j, 100.0 * (R.lTimeCourantCritical[j] / stepCount));
+    }
+
+    if (prj.rpt.flowStats) {
+        // report_writeMaxStats
+        if (balErr[0].index >= 0) {
+            w.title("Highest Continuity Errors");
+            for (const auto& r : balErr)
+                if (r.index >= 0) w.printf("\n  Node %s (%.2f%%)", net.nodeId[r.index].c_str(), r.value);
+            w.blank();
+        }
+        if (varStep) {
+            w.title("Time-Step Critical Elements");
+            int k = 0;
+            for (const auto& r : courant) {
+                if (r.index < 0) continue;
+                k++;
+                if (r.objType == 0) w.printf("\n  Node %s", net.nodeId[r.index].c_str());
+                else w.printf("\n  Link %s", net.linkId[r.index].c_str());
+                w.printf(" (%.2f%%)", r.value);
+            }
+            if (k == 0) w.printf("\n  None");
+            w.blank();
+        }
+        // report_writeMaxFlowTurns
+        w.title("Highest Flow Instability Indexes");
+        if (turns[0].index <= 0) w.printf("\n  All links are stable.");
+        else
+            for (const auto& r : turns)
+                if (r.index >= 0) w.printf("\n  Link %s (%.0f)", net.linkId[r.index].c_str(), r.value);
+        w.blank();
+        // report_writeNonconvergedStats
+        w.title("Most Frequent Nonconverging Nodes");
+        if (nonConv[0].index <= 0 || nonConv[0].value < 0.00005)
+            w.printf("\n  Convergence obtained at all time steps.");
+        else
+            for (const auto& r : nonConv)
+                if (r.index >= 0 && r.value > 0.0)
+                    w.printf("\n  Node %s (%.2f%%)", net.nodeId[r.index].c_str(), 100.0 * r.value);
+        w.blank();
+        // report_writeTimeStepStats
+        if (stepCount != 0.0) {
+            double total = R.steadyStateTime + R.routingTime, fSteady = 0.0;
+            if (total > 0.0) fSteady = 100.0 * R.steadyStateTime / total;
+            w.title("Routing Time Step Summary");
+            w.printf("\n  Minimum Time Step           :  %7.2f sec", R.minTimeStep);
+            w.printf("\n  Average Time Step           :  %7.2f sec", R.routingTime / stepCount);
+            w.printf("\n  Maximum Time Step           :  %7.2f sec", R.maxTimeStep);
+            w.printf("\n  %% of Time in Steady State   :  %7.2f", fSteady <= 100.0 ? fSteady : 100.0);
+            w.printf("\n  Average Iterations per Step :  %7.2f", R.trialsCount / stepCount);
+            w.printf("\n  %% of Steps Not Converging   :  %7.2f", 100.0 * (double)nonConvergeCount / stepCount);
+            if (varStep) {                 // report_RouteStepFreq
+                double steps = 0.0;
+                for (int i = 1; i < RunStats::kLevels; i++) steps += R.timeStepCounts[i];
+                if (steps != 0) {
+                    w.printf("\n  Time Step Frequencies       :");
+                    for (int i = 1; i < RunStats::kLevels; i++)
+                        w.printf("\n     %6.3f - %6.3f sec      :  %7.2f %%", R.timeStepIntervals[i - 1],
+                                 R.timeStepIntervals[i], 100.0 * R.timeStepCounts[i] / steps);
+                }
+            }
+            w.blank();
+        }
+    }
+
+    // ---- summary tables (statsrpt_writeReport) -------------------------------
+    const double steps = R.reportStepCount;
+    int d, h, m;
+    // Node Depth Summary
+    w.title("Node Depth Summary");
+    w.blank();
+    w.printf("\n  ---------------------------------------------------------------------------------"
+             "\n                                 Average  Maximum  Maximum  Time of Max    Reported"
+             "\n                                   Depth    Depth      HGL   Occurrence   Max Depth");
+    w.printf(us ? "\n  Node                 Type       Meters   Meters   Meters  days hr:min      Meters"
+                : "\n  Node                 Type         Feet     Feet     Feet  days hr:min        Feet");
+    w.printf("\n  ---------------------------------------------------------------------------------");
+    for (int j = 0; j < nN; j++) {
+        w.printf("\n  %-20s", net.nodeId[j].c_str());
+        w.printf(" %-9s ", kNodeWords[net.nodeType[j]]);
+        elapsed(R.maxDepthDate[j], rptStart, &d, &h, &m);
+        w.printf("%7.2f  %7.2f  %7.2f  %4d  %02d:%02d  %10.2f", R.avgDepth[j] / steps * ucfL,
+                 R.maxDepth[j] * ucfL, (R.maxDepth[j] + net.invertElev[j]) * ucfL, d, h, m,
+                 R.maxRptDepth[j]);
+    }
+    w.blank();
+
+    // Node Inflow Summary
+    w.title("Node Inflow Summary");
+    w.blank();
+    w.printf("\n  -------------------------------------------------------------------------------------------------"
+             "\n                                  Maximum  Maximum                  Lateral       Total        Flow"
+             "\n                                  Lateral    Total  Time of Max      Inflow      Inflow     Balance"
+             "\n                                   Inflow   Inflow   Occurrence      Volume      Volume       Error"
+             "\n  Node                 Type           %3s      %3s  days hr:min    %8s    %8s     Percent",
+             kFlowWords[o.flowUnits], kFlowWords[o.flowUnits], kVolWords[us], kVolWords[us]);
+    w.printf("\n  -------------------------------------------------------------------------------------------------");
+    for (int j = 0; j < nN; j++) {
+        w.printf("\n  %-20s", net.nodeId[j].c_str());
+        w.printf(" %-9s", kNodeWords[net.nodeType[j]]);
+        elapsed(R.maxInflowDate[j], rptStart, &d, &h, &m);
+        w.printf(flowFmt, R.maxLatFlow[j] * ucfQ);
+        w.printf(flowFmt, R.maxInflow[j] * ucfQ);
+        w.printf("  %4d  %02d:%02d", d, h, m);
+        w.printf("%12.3g", R.totLatFlow[j] * vcf);
+        w.printf("%12.3g", R.nodeInflowVol[j] * vcf);
+        double in = R.nodeInflowVol[j], out = R.nodeOutflowVol[j];
+        if (std::fabs(out) < 1.0) w.printf("%12.3f %s", (in - out) * vcf * 1.0e6, kVolWords2[us]);
+        else w.printf("%12.3f", (in - out) / out * 100.);
+    }
+    w.blank();
+
+    // Node Surcharge Summary (dynamic wave)
+    w.title("Node Surcharge Summary");
+    w.blank();
+    {
+        int n = 0;
+        for (int j = 0; j < nN; j++) {
+            if (net.nodeType[j] == OUTFALL || R.timeSurcharged[j] == 0.0) continue;
+            double t = R.timeSurcharged[j] / 3600.0;
+            if (t < 0.01) t = 0.01;
+            if (n++ == 0) {
+                w.line("Surcharging occurs when water rises above the top of the highest conduit.");
+                w.printf("\n  ---------------------------------------------------------------------"
+                         "\n                                               Max. Height   Min. Depth"
+                         "\n                                   Hours       Above Crown    Below Rim");
+                w.printf(us ? "\n  Node                 Type      Surcharged         Meters       Meters"
+                            : "\n  Node                 Type      Surcharged           Feet         Feet");
+                w.printf("\n  ---------------------------------------------------------------------");
+            }
+            w.printf("\n  %-20s", net.nodeId[j].c_str());
+            w.printf(" %-9s", kNodeWords[net.nodeType[j]]);
+            double d1 = R.maxDepth[j] + net.invertElev[j] - net.crownElev[j];
+            double d2 = net.fullDepth[j] - R.maxDepth[j];
+            w.printf("  %9.2f      %9.3f    %9.3f", t, (d1 < 0.0 ? 0.0 : d1) * ucfL, (d2 < 0.0 ? 0.0 : d2) * ucfL);
+        }
+        if (n == 0) w.line("No nodes were surcharged.");
+        w.blank();
+    }
+
+    // Node Flooding Summary
+    w.title("Node Flooding Summary");
+    w.blank();
+    {
+        int n = 0;
+        for (int j = 0; j < nN; j++) {
+            if (net.nodeType[j] == OUTFALL || R.timeFlooded[j] == 0.0) continue;
+            double t = R.timeFlooded[j] / 3600.0;
+            if (t < 0.01) t = 0.01;
+            if (n++ == 0) {
+                w.line("Flooding refers to all water that overflows a node, whether it ponds or not.");
+                w.printf("\n  --------------------------------------------------------------------------"
+                         "\n                                                             Total   Maximum"
+                         "\n                                 Maximum   Time of Max       Flood    Ponded"
+                         "\n                        Hours       Rate    Occurrence      Volume");
+                w.printf("     Depth");
+                w.printf("\n  Node                 Flooded       %3s   days hr:min    %8s", kFlowWords[o.flowUnits],
+                         kVolWords[us]);
+                w.printf("    %6s", kPondWords[us]);
+                w.printf("\n  --------------------------------------------------------------------------");
+            }
+            w.printf("\n  %-20s", net.nodeId[j].c_str());
+            w.printf(" %7.2f ", t);
+            w.printf(flowFmt, R.maxOverflow[j] * ucfQ);
+            elapsed(R.maxOverflowDate[j], rptStart, &d, &h, &m);
+            w.printf("   %4d  %02d:%02d", d, h, m);
+            w.printf("%12.3f", R.volFlooded[j] * vcf);
+            w.printf(" %9.3f", (R.maxDepth[j] - net.fullDepth[j]) * ucfL);
+        }
+        if (n == 0) w.line("No nodes were flooded.");
+        w.blank();
+    }
+
+    // Outfall Loading Summary
+    int nOut = 0;
+    for (int j = 0; j < nN; j++) nOut += net.nodeType[j] == OUTFALL;
+    if (nOut > 0) {
+        std::vector<double> totals(P, 0.0);
+        double flowSum = 0.0, freqSum = 0.0, volSum = 0.0;
+        w.title("Outfall Loading Summary");
+        w.blank();
+        auto dashes = [&]() {
+            w.printf("\n  -----------------------------------------------------------");
+            for (int p = 0; p < P; p++) w.printf("--------------");
+        };
+        dashes();
+        w.printf("\n                         Flow       Avg       Max       Total");
+        for (int p = 0; p < P; p++) w.printf("         Total");
+        w.printf("\n                         Freq      Flow      Flow      Volume");
+        for (int p = 0; p < P; p++) w.printf("%14s", net.pollut[p].id.c_str());
+        w.printf("\n  Outfall Node           Pcnt       %3s       %3s    %8s", kFlowWords[o.flowUnits],
+                 kFlowWords[o.flowUnits], kVolWords[us]);
+        for (int p = 0; p < P; p++) {
+            int k = (net.pollut[p].units == CU_COUNT) ? 2 : us;
+            w.printf("%14s", kLoadWords[k]);
+        }
+        dashes();
+        for (int j = 0; j < nN; j++) {
+            if (net.nodeType[j] != OUTFALL) continue;
+            double count = R.outfallPeriods[j];
+            w.printf("\n  %-20s", net.nodeId[j].c_str());
+            double x = 100. * count / steps;
+            w.printf("%7.2f", x);
+            freqSum += x;
+            x = (count > 0) ? R.outfallAvgFlow[j] * ucfQ / count : 0.0;
+            flowSum += x;
+            w.printf(" ");
+            w.printf(flowFmt, x);
+            w.printf(" ");
+            w.printf(flowFmt, R.outfallMaxFlow[j] * ucfQ);
+            w.printf("%12.3f", R.nodeInflowVol[j] * vcf);
+            volSum += R.nodeInflowVol[j];
+            for (int p = 0; p < P; p++) {
+                x = R.outfallLoad[(size_t)p * nN + j] * kLperFt3 * net.pollut[p].mcf;
+                totals[p] += x;
+                if (net.pollut[p].units == CU_COUNT) x = (x > 0.0) ? log10(x) : x;
+                w.printf("%14.3f", x);
+            }
+        }
+        dashes();
+        w.printf("\n  System              %7.2f ", freqSum / nOut);
+        w.printf(flowFmt, flowSum);
+        w.printf(" ");
+        w.printf(flowFmt, R.maxOutfallFlow * ucfQ);
+        w.printf("%12.3f", volSum * vcf);
+        for (int p = 0; p < P; p++) {
+            double x = totals[p];
+            if (net.pollut[p].units == CU_COUNT) x = (x > 0.0) ? log10(x) : x;
+            w.printf("%14.3f", x);
+        }
+        w.blank();
+    }
+
+    // Link Flow Summary
+    if (nL > 0) {
+        w.title("Link Flow Summary");
+        w.blank();
+        w.printf("\n  -----------------------------------------------------------------------------"
+                 "\n                                 Maximum  Time of Max   Maximum    Max/    Max/"
+                 "\n                                  |Flow|   Occurrence   |Veloc|    Full    Full");
+        w.printf(us ? "\n  Link                 Type          %3s  days hr:min     m/sec    Flow   Depth"
+                    : "\n  Link                 Type          %3s  days hr:min    ft/sec    Flow   Depth",
+                 kFlowWords[o.flowUnits]);
+        w.printf("\n  -----------------------------------------------------------------------------");
+        for (int j = 0; j < nL; j++) {
+            w.printf("\n  %-20s", net.linkId[j].c_str());
+            if (net.xsect[j].type == X_DUMMY) w.printf(" DUMMY   ");
+            else w.printf(" %-7s ", kLinkWords[net.linkType[j]]);
+            elapsed(R.lMaxFlowDate[j], rptStart, &d, &h, &m);
+            w.printf(flowFmt, R.lMaxFlow[j] * ucfQ);
+            w.printf("  %4d  %02d:%02d", d, h, m);
+            if (net.xsect[j].type == X_DUMMY) continue;
+            double v = R.lMaxVeloc[j] * ucfL;
+            if (v > 50.0) w.printf("    >50.00");
+            else w.printf("   %7.2f", v);
+            w.printf("  %6.2f", R.lMaxFlow[j] / net.qFull[j] / (double)net.barrels[j]);
+            double full = net.xsect[j].yFull;
+            if (full > 0.0) w.printf("  %6.2f", R.lMaxDepth[j] / full);
+            else w.printf("        ");
+        }
+        w.blank();
+    }
+
+    // Flow Classification Summary (dynamic wave)
+    w.title("Flow Classification Summary");
+    w.blank();
+    w.printf("\n  -------------------------------------------------------------------------------------"
+             "\n                      Adjusted    ---------- Fraction of Time in Flow Class ---------- "
+             "\n                       /Actual         Up    Down  Sub   Sup   Up    Down  Norm  Inlet "
+             "\n  Conduit               Length    Dry  Dry   Dry   Crit  Crit  Crit  Crit  Ltd   Ctrl  "
+             "\n  -------------------------------------------------------------------------------------");
+    for (int j = 0; j < nL; j++) {
+        if (net.linkType[j] != CONDUIT || net.xsect[j].type == X_DUMMY) continue;
+        w.printf("\n  %-20s", net.linkId[j].c_str());
+        w.printf("  %6.2f ", net.modLength[j] / net.length[j]);
+        for (int i = 0; i < RunStats::kClasses; i++)
+            w.printf("  %4.2f", R.lTimeInFlowClass[(size_t)i * nL + j] / R.routingTimeSpan);
+        w.printf("  %4.2f", R.lTimeNormalFlow[j] / R.routingTimeSpan);
+        w.printf("  %4.2f", 0.0 / R.routingTimeSpan);          // inlet control: culverts only
+    }
+    w.blank();
+
+    // Conduit Surcharge Summary
+    w.title("Conduit Surcharge Summary");
+    w.blank();
+    {
+        int n = 0;
+        for (int j = 0; j < nL; j++) {
+            if (net.linkType[j] != CONDUIT || net.xsect[j].type == X_DUMMY) continue;
+            double t[5] = {R.lTimeSurcharged[j] / 3600.0, R.lTimeFullUpstream[j] / 3600.0,
+                           R.lTimeFullDnstream[j] / 3600.0, R.lTimeFullFlow[j] / 3600.0, 0.0};
+            if (t[0] + t[1] + t[2] + t[3] == 0.0) continue;
+            t[4] = R.lTimeCapacityLimited[j] / 3600.0;
+            for (double& x : t) x = (0.01 >= x) ? 0.01 : x;
+            if (n++ == 0)
+                w.printf("\n  ----------------------------------------------------------------------------"
+                         "\n                                                           Hours        Hours "
+                         "\n                         --------- Hours Full --------   Above Full   Capacity"
+                         "\n  Conduit                Both Ends  Upstream  Dnstream   Normal Flow   Limited"
+                         "\n  ----------------------------------------------------------------------------");
+            w.printf("\n  %-20s", net.linkId[j].c_str());
+            w.printf("    %8.2f  %8.2f  %8.2f  %8.2f     %8.2f", t[0], t[1], t[2], t[3], t[4]);
+        }
+        if (n == 0) w.line("No conduits were surcharged.");
+        w.blank();
+    }
+}
+
+}  // namespace swx
