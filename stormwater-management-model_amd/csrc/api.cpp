@@ -207,7 +207,6 @@ static int execRouting()   // swmm5.c:514-575 + routing.c:203-265 on the device
 static void saveResults()   // swmm5.c:579-613
 {
     if (G->newRoutingTime >= G->reportTime) {
-        if (syncMirror()) return;
         double sys[6];
         // StepFlowTotals of this step: {flooding, outflow, dw, gw, ii, ex}
         sys[0] = G->sysStep[2];
@@ -216,8 +215,19 @@ static void saveResults()   // swmm5.c:579-613
         sys[3] = 0.0;
         sys[4] = 0.0;
         sys[5] = G->sysStep[1];
-        int e = G->out.saveResults(*G->prj, G->reportTime, G->oldRoutingTime, G->newRoutingTime, sys);
-        if (e) setErr(e, "ERROR 309: cannot write to binary results file.");
+        Project& prj = *G->prj;
+        double reportDate = prj.getDateTime(G->reportTime);
+        if (reportDate >= prj.opt.reportStart) {
+            // interpolation weight between the bracketing steps (output.c:645)
+            double f = (G->reportTime - G->oldRoutingTime) / (G->newRoutingTime - G->oldRoutingTime);
+            const float *nv = nullptr, *lv = nullptr;
+            if (G->router->packResults(f, prj.ucfLength(), prj.ucfVolume(), prj.ucfFlow(), &nv, &lv)) {
+                setErr(G->router->lastError(), G->router->lastErrorMsg());
+                return;
+            }
+            int e = G->out.saveResults(prj, reportDate, nv, lv, sys);
+            if (e) setErr(e, "ERROR 309: cannot write to binary results file.");
+        }
         G->reportTime = G->reportTime + 1000 * (double)G->prj->opt.reportStep;
     }
 }

@@ -1310,6 +1310,74 @@ __global__ void k_finalize(Params p)
     __threadfence_system();
 }
 
+// Results of one reporting period (node_getResults node.c:497-528,
+// link_getResults link.c:674-724, output.c:636-695): interpolation between the
+// step's old and new state with weight f, converted to user units and packed
+// as float32 in the .out variable order.  Host code writes the reported rows
+// and sums the system storage from the same floats.
+template <bool kFast>
+__global__ __launch_bounds__(kBlock) void k_pack_results(Params p, double f, double uL, double uV,
+                                                         double uQ, float* outN, float* outL)
+{
+    __shared__ double ct[5 * SWX_CIRC_N];
+    stageTables(ct, p.gTables);
+    const double f1 = 1.0 - f;
+    const int nv = 6 + p.P, lv = 5 + p.P;
+    int n = gridDim.x * kBlock;
+    for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nN; j += n) {
+        float* x = outN + (size_t)j * nv;
+        double z = (f1 * p.nOldDepth[j] + f * p.nNewDepth[j]) * uL;
+        x[0] = (float)z;
+        z = p.invert[j] * uL;
+        x[1] = x[0] + (float)z;
+        z = (f1 * p.nOldVolume[j] + f * p.nNewVolume[j]) * uV;
+        x[2] = (float)z;
+        z = (f1 * p.oldLat[j] + f * p.newLat[j]) * uQ;
+        x[3] = (float)z;
+        z = (f1 * p.oldFlowInflow[j] + f * p.inflow[j]) * uQ;
+        x[4] = (float)z;
+        z = p.overflow[j] * uQ;
+        x[5] = (float)z;
+        for (int q = 0; q < p.P; q++) {
+            size_t k = (size_t)q * p.nN + j;
+            z = f1 * p.nOldQual[k] + f * p.nNewQual[k];
+            x[6 + q] = (float)z;
+        }
+    }
+    for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nL; j += n) {
+        float* x = outL + (size_t)j * lv;
+        uint32_t fl = p.lflags[j];
+        Geom g = (fl & LF_COLD) ? loadGeom<false>(p, j, fl) : loadGeom<kFast>(p, j, fl);
+        double y = f1 * p.lOldDepth[j] + f * p.lNewDepth[j];
+        double q = f1 * p.lOldFlow[j] + f * p.lNewFlow[j];
+        double v = f1 * p.lOldVolume[j] + f * p.lNewVolume[j];
+        double u = 0.0;
+        if (y > 0.01) {                                  // link_getVelocity link.c:821-843
+            double barrels = (double)((fl >> LF_BARREL_SHIFT) & 0xFF);
+            double fq = q / barrels;
+            double area = getAofY(g, y, ct);
+            if (area > 0.0001) u = fq / area;
+        }
+        double c = 0.0;
+        if (g.type != G_DUMMY) c = getAofY(g, y, ct) / g.aFull;
+        double dir = (fl & LF_DIRNEG) ? -1.0 : 1.0;
+        y *= uL;
+        v *= uV;
+        q *= uQ * dir;
+        u *= uL * dir;
+        x[0] = (float)q;
+        x[1] = (float)y;
+        x[2] = (float)u;
+        x[3] = (float)v;
+        x[4] = (float)c;
+        for (int qq = 0; qq < p.P; qq++) {
+            size_t k = (size_t)qq * p.nL + j;
+            c = f1 * p.lOldQual[k] + f * p.lNewQual[k];
+            x[5 + qq] = (float)c;
+        }
+    }
+}
+
 // ===========================================================================
 //  Router implementation
 // ===========================================================================
@@ -1321,6 +1389,8 @@ struct Router::Impl {
     ncclComm_t comm = nullptr;       // RCCL communicator (multi-GPU, RCCL transport)
     int gridS = 1;                   // k_node_shared grid
     double* hostX = nullptr;         // host staging for the test transport
+    float *resN = nullptr, *resL = nullptr;          // packed period results (device)
+    float *resNHost = nullptr, *resLHost = nullptr;  // pinned copies
     hipEvent_t forkEv[kMaxTrialsCap] = {}, joinEv[kMaxTrialsCap] = {};
     hipGraphExec_t graph = nullptr;
     bool useGraph = true;
@@ -1379,6 +1449,8 @@ Router::~Router()
         if (d_->hostCtl) (void)hipHostFree(d_->hostCtl);
         if (d_->hostDt) (void)hipHostFree(d_->hostDt);
         if (d_->hostX) (void)hipHostFree(d_->hostX);
+        if (d_->resNHost) (void)hipHostFree(d_->resNHost);
+        if (d_->resLHost) (void)hipHostFree(d_->resLHost);
         if (d_->comm) (void)ncclCommDestroy(d_->comm);
         for (auto e : d_->clockEv) if (e) (void)hipEventDestroy(e);
         for (auto e : d_->ringEv) if (e) (void)hipEventDestroy(e);
@@ -2455,6 +2527,38 @@ int Router::timeKernel(int which, int reps, double* avgUs)
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     *avgUs = 1000.0 * ms / std::max(reps, 1);
+    return 0;
+}
+
+int Router::packResults(double f, double uL, double uV, double uQ, const float** nodeVals,
+                        const float** linkVals)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    const Params& p = d->p;
+    size_t nb = (size_t)p.nN * (6 + p.P), lb = (size_t)p.nL * (5 + p.P);
+    if (!d->resN) {
+        hipError_t e;
+        d->resN = devAlloc<float>(d, nb, &e);
+        if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+        d->resL = devAlloc<float>(d, lb, &e);
+        if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+        HIPCHECK(hipHostMalloc((void**)&d->resNHost, std::max<size_t>(nb, 1) * sizeof(float), hipHostMallocDefault));
+        HIPCHECK(hipHostMalloc((void**)&d->resLHost, std::max<size_t>(lb, 1) * sizeof(float), hipHostMallocDefault));
+    }
+    int grid = std::max(d->gridL, d->gridN);
+    if (d->fastLinks)
+        hipLaunchKernelGGL(k_pack_results<true>, dim3(grid), dim3(kBlock), 0, d->stream, p, f, uL, uV, uQ,
+                           d->resN, d->resL);
+    else
+        hipLaunchKernelGGL(k_pack_results<false>, dim3(grid), dim3(kBlock), 0, d->stream, p, f, uL, uV, uQ,
+                           d->resN, d->resL);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(d->resNHost, d->resN, nb * sizeof(float), hipMemcpyDeviceToHost, d->stream));
+    HIPCHECK(hipMemcpyAsync(d->resLHost, d->resL, lb * sizeof(float), hipMemcpyDeviceToHost, d->stream));
+    HIPCHECK(hipStreamSynchronize(d->stream));
+    *nodeVals = d->resNHost;
+    *linkVals = d->resLHost;
     return 0;
 }
 

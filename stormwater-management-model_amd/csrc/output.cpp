@@ -99,82 +99,33 @@ int OutFile::open(const std::string& path, Project& prj)  // output.c:121-405
     return ferror(f_) ? 309 : 0;
 }
 
-int OutFile::saveResults(Project& prj, double reportTime, double oldT, double newT,
+int OutFile::saveResults(Project& prj, double reportDate, const float* nodeVals, const float* linkVals,
                          const double sys[6])   // output.c:457-505, 636-695
 {
     if (!f_) return 0;
-    double reportDate = prj.getDateTime(reportTime);
-    if (reportDate < prj.opt.reportStart) return 0;
     Network& net = prj.net;
-    State& s = prj.st;
-    const double* ct = &SWX_CIRC_TABLES[0][0];
     int nn = net.nNodes(), nl = net.nLinks(), P = nPoll_;
-    double uL = prj.ucfLength(), uV = prj.ucfVolume(), uQ = prj.ucfFlow();
+    const int nv = 6 + P, lv = 5 + P;
+    double uQ = prj.ucfFlow();
     float sysr[kMaxSysResults];
     for (float& x : sysr) x = 0.0f;
     fwrite(&reportDate, 8, 1, f_);
-    double f = (reportTime - oldT) / (newT - oldT);
-    double f1 = 1.0 - f;
-    buf_.resize(std::max(nNodeVars_, nLinkVars_));
-    float* x = buf_.data();
     std::vector<double>& rpt = prj.stats.maxRptDepth;
     if ((int)rpt.size() != nn) rpt.assign(nn, 0.0);
-    for (int j = 0; j < nn; j++) {              // node_getResults node.c:497-528
-        double z = (f1 * s.oldDepth[j] + f * s.newDepth[j]) * uL;
-        x[0] = (float)z;
-        z = net.invertElev[j] * uL;
-        x[1] = x[0] + (float)z;
-        z = (f1 * s.oldVolume[j] + f * s.newVolume[j]) * uV;
-        x[2] = (float)z;
-        z = (f1 * s.oldLatFlow[j] + f * s.newLatFlow[j]) * uQ;
-        x[3] = (float)z;
-        z = (f1 * s.oldFlowInflow[j] + f * s.inflow[j]) * uQ;
-        x[4] = (float)z;
-        z = s.overflow[j] * uQ;
-        x[5] = (float)z;
-        for (int p = 0; p < P; p++) {
-            z = f1 * s.nOldQual[(size_t)p * nn + j] + f * s.nNewQual[(size_t)p * nn + j];
-            x[6 + p] = (float)z;
-        }
+    // node rows (node_getResults node.c:497-528, packed on the device)
+    for (int j = 0; j < nn; j++) {
+        const float* x = nodeVals + (size_t)j * nv;
         if (net.rptFlag[j]) fwrite(x, 4, nNodeVars_, f_);
         // stats_updateMaxNodeDepth (stats.c:436-445) with the reported value
         rpt[j] = (rpt[j] >= (double)x[0]) ? rpt[j] : (double)x[0];
         sysr[12] += x[2];
     }
-    for (int j = 0; j < nl; j++) {              // link_getResults link.c:674-724
-        if (net.linkRpt[j]) {
-            const Xsect& xs = net.xsect[j];
-            Geom g{xs.type, xs.yFull, xs.wMax, xs.ywMax, xs.aFull, xs.rFull, xs.sFull, xs.sMax,
-                   xs.yBot, xs.aBot, xs.sBot, xs.rBot};
-            double y = f1 * s.lOldDepth[j] + f * s.lNewDepth[j];
-            double q = f1 * s.lOldFlow[j] + f * s.lNewFlow[j];
-            double v = f1 * s.lOldVolume[j] + f * s.lNewVolume[j];
-            double u = 0.0;
-            if (y > 0.01) {                     // link_getVelocity link.c:821-843
-                double fl = q / net.barrels[j];
-                double area = getAofY(g, y, ct);
-                if (area > kFudge) u = fl / area;
-            }
-            double c = 0.0;
-            if (xs.type != X_DUMMY) c = getAofY(g, y, ct) / xs.aFull;
-            double dir = (double)net.direction[j];
-            y *= uL;
-            v *= uV;
-            q *= uQ * dir;
-            u *= uL * dir;
-            x[0] = (float)q;
-            x[1] = (float)y;
-            x[2] = (float)u;
-            x[3] = (float)v;
-            x[4] = (float)c;
-            for (int p = 0; p < P; p++) {
-                c = f1 * s.lOldQual[(size_t)p * nl + j] + f * s.lNewQual[(size_t)p * nl + j];
-                x[5 + p] = (float)c;
-            }
-            fwrite(x, 4, nLinkVars_, f_);
-        }
-        double z = ((1.0 - f) * s.lOldVolume[j] + f * s.lNewVolume[j]) * uV;
-        sysr[12] += (float)z;
+    // link rows (link_getResults link.c:674-724); system storage adds every
+    // link's volume in link order (output.c:668-671)
+    for (int j = 0; j < nl; j++) {
+        const float* x = linkVals + (size_t)j * lv;
+        if (net.linkRpt[j]) fwrite(x, 4, nLinkVars_, f_);
+        sysr[12] += x[3];
     }
     sysr[10] = (float)(sys[0] * uQ);
     sysr[11] = (float)(sys[1] * uQ);

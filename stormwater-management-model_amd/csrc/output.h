@@ -15,11 +15,12 @@ class OutFile {
 public:
     ~OutFile();
     int open(const std::string& path, Project& prj);
-    // write one reporting period; state = host mirror at the routing step
-    // that brackets reportTime; sysFlows = {flooding, outflow, dwInflow,
-    // gwInflow, iiInflow, exInflow} rates of that step (StepFlowTotals)
-    int saveResults(Project& prj, double reportTime, double oldRoutingTime,
-                    double newRoutingTime, const double sysFlows[6]);
+    // write one reporting period from the device-packed rows (Router::
+    // packResults: nodes 6 + P floats, links 5 + P floats, all objects);
+    // sysFlows = {flooding, outflow, dwInflow, gwInflow, iiInflow, exInflow}
+    // rates of the bracketing step (StepFlowTotals)
+    int saveResults(Project& prj, double reportDate, const float* nodeVals, const float* linkVals,
+                    const double sysFlows[6]);
     int end(int errorCode);
     void close();
     int periods() const { return nPeriods_; }

@@ -56,6 +56,12 @@ public:
     int setDuration(double msec);
     // Copy device state into the host mirror (prj.st); synchronises.
     int download(Project& prj);
+    // Results of one reporting period packed on the device in the .out
+    // variable order (nodes: 6 + P floats each, links: 5 + P), interpolated
+    // with weight f and converted with the unit factors; pointers to pinned
+    // host copies valid until the next call.  Synchronises.
+    int packResults(double f, double uL, double uV, double uQ, const float** nodeVals,
+                    const float** linkVals);
     // Copy the run statistics accumulators into prj.stats; synchronises.
     int downloadStats(Project& prj);
     // Upload the host mirror's dynamic state (after swmm_setValue edits).
