@@ -286,6 +286,32 @@ static void writeStatic(void)
     free(db);
 }
 
+static char* ActText = NULL;
+
+static void applyActions(int step)
+{
+    char buf[4096];
+    char* save = NULL;
+    char* tok;
+    if (!ActText) return;
+    strncpy(buf, ActText, sizeof(buf) - 1);
+    buf[sizeof(buf) - 1] = 0;
+    for (tok = strtok_r(buf, ";", &save); tok; tok = strtok_r(NULL, ";", &save))
+    {
+        int at = 0, prop = 0, idx = -1;
+        char name[256];
+        double value = 0.0;
+        if (sscanf(tok, "%d:%d:%255[^:]:%lf", &at, &prop, name, &value) != 4) continue;
+        if (at != step) continue;
+        if (strcmp(name, "-"))
+        {
+            idx = swmm_getIndex(prop >= 400 ? swmm_LINK : swmm_NODE, name);
+            if (idx < 0) { fprintf(stderr, "refdump: unknown object %s\n", name); exit(3); }
+        }
+        swmm_setValue(prop, idx, value);
+    }
+}
+
 int main(int argc, char** argv)
 {
     double elapsed = 0.0;
@@ -309,9 +335,17 @@ int main(int argc, char** argv)
     if (!F) return 1;
     fwrite("SWDUMP1\0", 1, 8, F);
     writeStatic();
+    /* optional swmm_setValue calls between steps, for the API golden cases:
+       REFDUMP_ACTIONS="afterStep:property:objectName:value;..." (objectName
+       "-" for system properties); applied once `afterStep` steps are done */
+    {
+        const char* env = getenv("REFDUMP_ACTIONS");
+        if (env) ActText = strdup(env);
+    }
     do
     {
         double told = NewRoutingTime;
+        applyActions(step);
         swmm_step(&elapsed);
         step++;
         if (step % every == 0 || elapsed <= 0.0)

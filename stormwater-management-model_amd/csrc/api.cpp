@@ -116,7 +116,7 @@ int DLLEXPORT swmmx_startHost(void)
     if (G->errorCode) return G->errorCode;
     if (!G->isOpen) return (G->errorCode = 501);
     if (G->isStarted) return (G->errorCode = 503);
-    G->prj->initState();
+    if (G->prj->initState()) return setErr(G->prj->errorCode, G->prj->errorMsg);
     G->hostOnly = true;
     G->isStarted = true;
     G->mirrorValid = true;
@@ -137,11 +137,12 @@ int DLLEXPORT swmm_start(int saveFlag)
     G->routingDuration = prj.opt.totalDuration;
     G->totalStepCount = 0;
     G->elapsedTime = 0.0;
-    prj.initState();
+    // project_init, output_open and hotstart_open (swmm5.c:370-385); the
+    // results file is opened first, as in the reference
+    if (G->out.open(G->outPath, prj)) return setErr(307, "ERROR 307: cannot open binary results file.");
+    if (prj.initState()) return setErr(prj.errorCode, prj.errorMsg);
     G->apiExtInflow.assign(prj.net.nNodes(), 0.0);
     G->constantInflow = prj.inflowsAreConstant();
-    // output_open (swmm5.c:379) -- the reference always opens the binary file
-    if (G->out.open(G->outPath, prj)) return setErr(307, "ERROR 307: cannot open binary results file.");
     // massbal_open: initial storage
     double s = 0.0;
     for (int j = 0; j < prj.net.nNodes(); j++) s += prj.st.newVolume[j];
@@ -149,6 +150,8 @@ int DLLEXPORT swmm_start(int saveFlag)
     G->initStorage = s;
     G->router.reset(new Router());
     int dev = (gDevice >= 0) ? gDevice : defaultDevice();
+    if (gPart.active() && !prj.hotstartSave.empty())
+        return setErr(500, "ERROR 500: saving a hot start file is not yet supported with more than one GPU");
     if (gPart.active() && G->saveFlag)
         return setErr(500, "ERROR 500: the results file is not yet supported with more than one GPU "
                            "(swmm_start(0))");
@@ -360,6 +363,8 @@ int DLLEXPORT swmm_end(void)   // swmm5.c:618-660
             G->flowError = computeFlowError();
             G->out.end(G->errorCode);
             if (!G->errorCode) writeReportSummary();
+            // hotstart_close (swmm5.c:647): the final state as a hot start file
+            if (G->prj->saveHotstart()) setErr(G->prj->errorCode, G->prj->errorMsg);
         }
         G->isStarted = false;
     }
@@ -472,11 +477,30 @@ double DLLEXPORT swmm_getValue(int property, int index)   // swmm5.c:842-1213
     }
     if (property >= 300 && property < 400) {
         if (index < 0 || index >= prj.net.nNodes()) return 0;
-        if (property >= swmm_NODE_DEPTH && property <= swmm_NODE_OVERFLOW && G->isStarted) syncMirror();
         const Network& n = prj.net;
         const State& s = prj.st;
         double uL = prj.ucfLength(), uQ = prj.ucfFlow();
         bool st = !s.newDepth.empty();
+        if (property >= swmm_NODE_DEPTH && property <= swmm_NODE_OVERFLOW && G->isStarted &&
+            !G->mirrorValid) {
+            // one value straight from HBM instead of a full state download
+            int f = -1;
+            switch (property) {
+            case swmm_NODE_DEPTH: case swmm_NODE_HEAD: f = Router::PK_NODE_DEPTH; break;
+            case swmm_NODE_VOLUME: f = Router::PK_NODE_VOLUME; break;
+            case swmm_NODE_LATFLOW: f = Router::PK_NODE_LATFLOW; break;
+            case swmm_NODE_INFLOW: f = Router::PK_NODE_INFLOW; break;
+            case swmm_NODE_OVERFLOW: f = Router::PK_NODE_OVERFLOW; break;
+            }
+            double v = 0.0;
+            if (G->router->peek(f, index, &v)) return 0.0;
+            switch (property) {
+            case swmm_NODE_DEPTH: return v * uL;
+            case swmm_NODE_HEAD: return (v + n.invertElev[index]) * uL;
+            case swmm_NODE_VOLUME: return v * prj.ucfVolume();
+            default: return v * uQ;
+            }
+        }
         switch (property) {
         case swmm_NODE_TYPE: return n.nodeType[index];
         case swmm_NODE_ELEV: return n.invertElev[index] * uL;
@@ -493,7 +517,6 @@ double DLLEXPORT swmm_getValue(int property, int index)   // swmm5.c:842-1213
     }
     if (property >= 400 && property < 500) {
         if (index < 0 || index >= prj.net.nLinks()) return 0;
-        if (property >= swmm_LINK_FLOW && property <= swmm_LINK_TOPWIDTH && G->isStarted) syncMirror();
         const Network& n = prj.net;
         const State& s = prj.st;
         double uL = prj.ucfLength(), uQ = prj.ucfFlow();
@@ -501,6 +524,35 @@ double DLLEXPORT swmm_getValue(int property, int index)   // swmm5.c:842-1213
         const Xsect& x = n.xsect[index];
         Geom g{x.type, x.yFull, x.wMax, x.ywMax, x.aFull, x.rFull, x.sFull, x.sMax, x.yBot, x.aBot, x.sBot, x.rBot};
         const double* ct = &SWX_CIRC_TABLES[0][0];
+        bool dyn = (property >= swmm_LINK_FLOW && property <= swmm_LINK_TOPWIDTH) ||
+                   property == swmm_LINK_SETTING;
+        if (dyn && G->isStarted && !G->mirrorValid) {
+            // flow / depth / setting of this link straight from HBM
+            double q = 0.0, y = 0.0, set = 1.0;
+            Router& r = *G->router;
+            if (property == swmm_LINK_SETTING) {
+                if (r.peek(Router::PK_LINK_SETTING, index, &set)) return 0.0;
+                return set;
+            }
+            if (property != swmm_LINK_DEPTH && property != swmm_LINK_TOPWIDTH &&
+                r.peek(Router::PK_LINK_FLOW, index, &q)) return 0.0;
+            if (property != swmm_LINK_FLOW && r.peek(Router::PK_LINK_DEPTH, index, &y)) return 0.0;
+            switch (property) {
+            case swmm_LINK_FLOW: return q * uQ * (double)n.direction[index];
+            case swmm_LINK_DEPTH: return y * uL;
+            case swmm_LINK_TOPWIDTH: return getWofY(g, y, ct) * uL;
+            case swmm_LINK_VELOCITY: {                     // link_getVelocity link.c:821-843
+                double v = 0.0;
+                if (y > 0.01) {
+                    double fl = fabs(q) / n.barrels[index];
+                    double area = getAofY(g, y, ct);
+                    if (area > kFudge) v = fl / area;
+                }
+                return v * uL;
+            }
+            default: return 0.0;
+            }
+        }
         switch (property) {
         case swmm_LINK_TYPE: return n.linkType[index];
         case swmm_LINK_NODE1: return n.node1[index];
@@ -541,6 +593,13 @@ void DLLEXPORT swmm_setValue(int property, int index, double value)
         G->apiExtInflow[index] = value / prj.ucfFlow();
         G->constantInflow = false;
         return;
+    case swmm_NODE_HEAD:                      // setOutfallStage (swmm5.c:1173-1188)
+        if (index < 0 || index >= prj.net.nNodes() || prj.net.nodeType[index] != OUTFALL) return;
+        prj.net.fixedStage[index] = value / prj.ucfLength();
+        prj.net.outfallType[index] = O_FIXED;
+        if (G->isStarted && G->router && G->router->setOutfallStage(index, prj.net.fixedStage[index]))
+            setErr(G->router->lastError(), G->router->lastErrorMsg());
+        return;
     case swmm_NODE_RPTFLAG:
         if (!G->isStarted && index >= 0 && index < prj.net.nNodes()) prj.net.rptFlag[index] = value > 0.0;
         return;
@@ -555,8 +614,20 @@ void DLLEXPORT swmm_setValue(int property, int index, double value)
     case swmm_NOREPORT:
         if (!G->isStarted) prj.rpt.disabled = value > 0.0;
         return;
-    case swmm_ROUTESTEP:
-        if (!G->isStarted && value > 0.0) { prj.opt.courantFactor = 0.0; prj.opt.routeStep = value; }
+    case swmm_ROUTESTEP:                      // setRoutingStep (swmm5.c:1360-1370)
+        if (value <= 0.0) return;
+        if (value <= prj.opt.minRouteStep) value = prj.opt.minRouteStep;
+        prj.opt.courantFactor = 0.0;
+        prj.opt.routeStep = value;
+        if (G->isStarted && G->router && !G->hostOnly) {
+            // the next step is fixed too: execRouting's clamp (swmm5.c:538-546)
+            double dt = value;
+            if (G->newRoutingTime + 1000.0 * dt > G->routingDuration) {
+                dt = (G->routingDuration - G->newRoutingTime) / 1000.0;
+                dt = (dt >= 1. / 1000.0) ? dt : 1. / 1000.0;
+            }
+            if (G->router->setRouteStep(value, dt)) setErr(G->router->lastError(), G->router->lastErrorMsg());
+        }
         return;
     default:
         return;

@@ -97,7 +97,7 @@ struct StepCtl {
     double variableStep;          // dynwave.c:84 VariableStep
     int unconv[kMaxTrialsCap];    // per-iteration "some node not converged" flag
     int lastSteps;
-    int pad;
+    int varStepOff;               // swmm_setValue(ROUTESTEP) mid-run: CourantFactor = 0
     long long totalSteps, totalIters, nonConverge;
     double stepTot[kNumPartials];     // this step's system totals (rates)
     double prevStepTot[kNumPartials]; // previous step's totals (massbal half step)
@@ -1285,7 +1285,7 @@ __global__ void k_finalize(Params p)
     // step length of the next step: dynwave_getRoutingStep (dynwave.c:195-220,
     // 799-832) then execRouting's end-of-run clamp (swmm5.c:538-546)
     double dtn = c->routeStep;
-    if (p.varStep) {
+    if (p.varStep && !c->varStepOff) {
         double tMin = tot[5];
         if (tot[6] < tMin) tMin = tot[6];
         // getVariableStep's critical element (dynwave.c:815-828) -- counted
@@ -2527,6 +2527,76 @@ int Router::timeKernel(int which, int reps, double* avgUs)
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     *avgUs = 1000.0 * ms / std::max(reps, 1);
+    return 0;
+}
+
+// ---- fine-grained state access (swmm_getValue / swmm_setValue) ----------
+static int localIndex(const std::vector<int>& g2l, bool multi, int g)
+{
+    if (!multi) return g;
+    return (g >= 0 && g < (int)g2l.size()) ? g2l[g] : -1;
+}
+
+int Router::peek(int field, int g, double* v)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    const Params& p = d->p;
+    const bool multi = d->part.active();
+    const double* src = nullptr;
+    int i = -1;
+    if (field < PK_LINK_FLOW) {
+        i = localIndex(d->part.gnode, multi, g);
+        if (i < 0 || i >= p.nN) return 1;
+        switch (field) {
+        case PK_NODE_DEPTH: src = p.nNewDepth; break;
+        case PK_NODE_VOLUME: src = p.nNewVolume; break;
+        case PK_NODE_LATFLOW: src = p.newLat; break;
+        case PK_NODE_INFLOW: src = p.inflow; break;
+        case PK_NODE_OVERFLOW: src = p.overflow; break;
+        default: return 1;
+        }
+    } else {
+        i = localIndex(d->part.glink, multi, g);
+        if (i < 0 || i >= p.nL) return 1;
+        switch (field) {
+        case PK_LINK_FLOW: src = p.lNewFlow; break;
+        case PK_LINK_DEPTH: src = p.lNewDepth; break;
+        case PK_LINK_SETTING: src = p.setting; break;
+        default: return 1;
+        }
+    }
+    HIPCHECK(hipMemcpyAsync(v, src + i, sizeof(double), hipMemcpyDeviceToHost, d->stream));
+    HIPCHECK(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+int Router::setOutfallStage(int g, double stage)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    Params& p = d->p;
+    int i = localIndex(d->part.gnode, d->part.active(), g);
+    if (i < 0 || i >= p.nN) return 0;                   // not on this rank
+    HIPCHECK(hipStreamSynchronize(d->stream));
+    int f = 0;
+    HIPCHECK(hipMemcpy(&f, p.nflags + i, sizeof(int), hipMemcpyDeviceToHost));
+    f = (int)(((uint32_t)f & ~(0x7u << NF_OTYPE_SHIFT)) | ((uint32_t)O_FIXED << NF_OTYPE_SHIFT));
+    HIPCHECK(hipMemcpy((void*)(p.nflags + i), &f, sizeof(int), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy((void*)(p.fixedStage + i), &stage, sizeof(double), hipMemcpyHostToDevice));
+    return 0;
+}
+
+int Router::setRouteStep(double step, double dtNext)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    HIPCHECK(hipStreamSynchronize(d->stream));
+    StepCtl* c = d->p.ctl;
+    int off = 1;
+    HIPCHECK(hipMemcpy(&c->routeStep, &step, sizeof(double), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(&c->varStepOff, &off, sizeof(int), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(&c->dt, &dtNext, sizeof(double), hipMemcpyHostToDevice));
     return 0;
 }
 

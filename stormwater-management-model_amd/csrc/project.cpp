@@ -207,11 +207,11 @@ static bool getDouble(const char* s, double* y)
 
 enum Sect {
     S_NONE = -1, S_TITLE, S_OPTION, S_EVAP, S_JUNC, S_OUTFALL, S_CONDUIT, S_XSECT, S_LOSS,
-    S_POLLUT, S_INFLOW, S_DWF, S_PATTERN, S_TSERIES, S_REPORT, S_SKIP, S_UNSUPPORTED
+    S_POLLUT, S_INFLOW, S_DWF, S_PATTERN, S_TSERIES, S_REPORT, S_FILES, S_SKIP, S_UNSUPPORTED
 };
 static const char* const kSectWords[] = {
     "[TITLE", "[OPTION", "[EVAP", "[JUNC", "[OUTFALL", "[CONDUIT", "[XSECT", "[LOSS",
-    "[POLLUT", "[INFLOW", "[DWF", "[PATTERN", "[TIMESERIES", "[REPORT", nullptr};
+    "[POLLUT", "[INFLOW", "[DWF", "[PATTERN", "[TIMESERIES", "[REPORT", "[FILES", nullptr};
 static const char* const kSkipWords[] = {
     "[MAP", "[COORDINATE", "[VERTICES", "[POLYGON", "[SYMBOL", "[LABEL", "[BACKDROP", "[TAG",
     "[PROFILE", nullptr};
@@ -281,6 +281,14 @@ int Project::setError(int code, const std::string& msg)
 // ============================================================ .inp reading
 int Project::open(const char* path)
 {
+    // InpDir: directory of the input file with its trailing delimiter
+    // (getAbsolutePath, swmm5.c:1571-1606)
+    {
+        char buf[4096];
+        std::string full = (path[0] != '/' && realpath(path, buf)) ? std::string(buf) : std::string(path);
+        size_t k = full.rfind('/');
+        inpDir = (k == std::string::npos) ? std::string() : full.substr(0, k + 1);
+    }
     if (readFile(path)) return errorCode;
     // project.c:147-181 -- run dates and durations
     opt.startDateTime = opt.startDate + opt.startTime;
@@ -447,6 +455,7 @@ int Project::parseLine(int sect, std::vector<char*>& tok, int pass)
     case S_PATTERN: return readPattern(tok);
     case S_TSERIES: return readTimeseries(tok);
     case S_REPORT: return readReport(tok);
+    case S_FILES: return readFiles(tok);
     default: return 0;
     }
 }
@@ -1023,6 +1032,143 @@ int Project::readTimeseries(std::vector<char*>& tok)  // table.c:113-202
     return 0;
 }
 
+// [FILES] USE|SAVE FileType FileName (iface.c:66-134).  Hot start files are
+// supported; rainfall / runoff files belong to the runoff model (no
+// subcatchments here) and are ignored; routing interface files change the
+// routed inflows and are rejected.
+int Project::readFiles(std::vector<char*>& tok)
+{
+    static const char* const kModes[] = {"NO", "SCRATCH", "USE", "SAVE", nullptr};
+    static const char* const kTypes[] = {"RAINFALL", "RUNOFF", "HOTSTART", "RDII", "INFLOWS",
+                                         "OUTFLOWS", nullptr};
+    int nt = (int)tok.size();
+    if (nt < 2) return 203;
+    int k = kfind(tok[0], kModes);
+    if (k < 0) return 205;
+    int j = kfind(tok[1], kTypes);
+    if (j < 0) return 205;
+    if (nt < 3) return 0;
+    std::string fname = tok[2];
+    // addAbsolutePath (swmm5.c:1620-1633)
+    bool rel = !(strchr(fname.c_str(), ':') || fname[0] == '\\' || fname[0] == '/');
+    if (rel) fname = inpDir + fname;
+    switch (j) {
+    case 2:
+        if (k == 2) hotstartUse = fname;
+        else if (k == 3) hotstartSave = fname;
+        return 0;
+    case 4:
+        if (k != 2) return 203;
+        break;
+    case 5:
+        if (k != 3) return 203;
+        break;
+    case 3:
+        if (k != 2 && k != 3) return 0;
+        break;
+    default:
+        return 0;
+    }
+    return setError(200, std::string("ERROR 200: ") + kTypes[j] +
+                             " interface files are not supported by the MI355X dynamic-wave engine");
+}
+
+// openHotstartFile1 + readRouting (hotstart.c:95-171, 252-330): versions 1-4.
+// The file must describe the same object counts and flow units; node depth,
+// lateral inflow and quality, and link flow, depth and setting are read as
+// float32.
+int Project::readHotstart()
+{
+    FILE* f = fopen(hotstartUse.c_str(), "rb");
+    if (!f) return setError(331, "ERROR 331: cannot open hot start interface file " + hotstartUse + ".");
+    auto fmt = [&]() {
+        fclose(f);
+        return setError(333, "ERROR 333: incompatible data found in hot start interface file.");
+    };
+    char stamp[16] = {0};
+    int version = 0;
+    if (fread(stamp, 1, 15, f) == 15) {
+        if (!strcmp(stamp, "SWMM5-HOTSTART4")) version = 4;
+        else if (!strcmp(stamp, "SWMM5-HOTSTART3")) version = 3;
+        else if (!strcmp(stamp, "SWMM5-HOTSTART2")) version = 2;
+    }
+    if (!version) {
+        rewind(f);
+        char s1[15] = {0};
+        if (fread(s1, 1, 14, f) != 14 || strcmp(s1, "SWMM5-HOTSTART")) return fmt();
+        version = 1;
+    }
+    int nSub = 0, nLand = 0, nNode = -1, nLink = -1, nPoll = -1, units = -1;
+    auto rdi = [&](int* x) { return fread(x, sizeof(int), 1, f) == 1; };
+    if (version >= 2 && !rdi(&nSub)) return fmt();
+    if (version >= 3 && !rdi(&nLand)) return fmt();
+    if (!rdi(&nNode) || !rdi(&nLink) || !rdi(&nPoll) || !rdi(&units)) return fmt();
+    int nn = net.nNodes(), nl = net.nLinks(), P = net.nPollut();
+    if (nSub != 0 || nLand != 0 || nNode != nn || nLink != nl || nPoll != P || units != opt.flowUnits)
+        return fmt();
+    // readRunoff (version >= 3) has nothing to read without subcatchments;
+    // version 2's groundwater records likewise
+    auto rdf = [&](double* y) {
+        float x;
+        if (fread(&x, sizeof(float), 1, f) != 1 || x != x) {
+            setError(335, "ERROR 335: error in reading from hot start interface file.");
+            return false;
+        }
+        *y = x;
+        return true;
+    };
+    State& s = st;
+    double x;
+    for (int i = 0; i < nn; i++) {
+        if (!rdf(&s.newDepth[i]) || !rdf(&s.newLatFlow[i])) break;
+        if (version >= 4 && net.nodeType[i] == STORAGE && !rdf(&x)) break;
+        bool ok = true;
+        for (int p = 0; p < P && ok; p++) ok = rdf(&s.nNewQual[(size_t)p * nn + i]);
+        for (int p = 0; version <= 2 && p < P && ok; p++) ok = rdf(&x);
+        if (!ok) break;
+    }
+    for (int i = 0; i < nl && !errorCode; i++) {
+        if (!rdf(&s.lNewFlow[i]) || !rdf(&s.lNewDepth[i]) || !rdf(&s.setting[i])) break;
+        // link_setTargetSetting / link_setSetting: no effect on conduits
+        bool ok = true;
+        for (int p = 0; p < P && ok; p++) ok = rdf(&s.lNewQual[(size_t)p * nl + i]);
+        if (!ok) break;
+    }
+    fclose(f);
+    return errorCode;
+}
+
+int Project::saveHotstart()   // openHotstartFile2 + saveRouting (hotstart.c:175-250)
+{
+    if (hotstartSave.empty()) return 0;
+    FILE* f = fopen(hotstartSave.c_str(), "w+b");
+    if (!f) return setError(331, "ERROR 331: cannot open hot start interface file " + hotstartSave + ".");
+    int nn = net.nNodes(), nl = net.nLinks(), P = net.nPollut();
+    int hdr[6] = {0, 0, nn, nl, P, opt.flowUnits};
+    fwrite("SWMM5-HOTSTART4", 1, 15, f);
+    fwrite(hdr, sizeof(int), 6, f);
+    std::vector<float> buf;
+    buf.reserve((size_t)(nn + nl) * (3 + P));
+    const State& s = st;
+    for (int i = 0; i < nn; i++) {
+        buf.push_back((float)s.newDepth[i]);
+        buf.push_back((float)s.newLatFlow[i]);
+        if (net.nodeType[i] == STORAGE) buf.push_back(0.0f);   // storage hrt
+        for (int p = 0; p < P; p++) buf.push_back((float)s.nNewQual[(size_t)p * nn + i]);
+    }
+    for (int i = 0; i < nl; i++) {
+        buf.push_back((float)s.lNewFlow[i]);
+        buf.push_back((float)s.lNewDepth[i]);
+        buf.push_back((float)s.setting[i]);
+        for (int p = 0; p < P; p++) buf.push_back((float)s.lNewQual[(size_t)p * nl + i]);
+    }
+    fwrite(buf.data(), sizeof(float), buf.size(), f);
+    bool bad = ferror(f) != 0;
+    fclose(f);
+    if (bad) return setError(331, "ERROR 331: cannot open hot start interface file " + hotstartSave + ".");
+    return 0;
+}
+
 int Project::readReport(std::vector<char*>& tok)  // report.c:report_readOptions
 {
     int nt = (int)tok.size();
@@ -1221,7 +1367,70 @@ void Project::validate()  // project.c:186-270
 }
 
 // ===================================================== initial state (start)
-void Project::initState()
+// initNodeDepths (flowrout.c:337-385) + link_setOutfallDepth for all links +
+// initLinkDepths (flowrout.c:389-421)
+void Project::initDepths()
+{
+    int nn = net.nNodes(), nl = net.nLinks();
+    const double* ct = &SWX_CIRC_TABLES[0][0];
+    auto geom = [&](int j) {
+        const Xsect& x = net.xsect[j];
+        return Geom{x.type, x.yFull, x.wMax, x.ywMax, x.aFull, x.rFull, x.sFull, x.sMax,
+                    x.yBot, x.aBot, x.sBot, x.rBot};
+    };
+    State& s = st;
+    std::vector<double> acc(nn, 0.0), cnt(nn, 0.0);
+    for (int i = 0; i < nl; i++) {
+        double y = (s.lNewDepth[i] > kFudge) ? s.lNewDepth[i] + net.offset1[i] : 0.0;
+        acc[net.node1[i]] += y; cnt[net.node1[i]] += 1.0;
+        acc[net.node2[i]] += y; cnt[net.node2[i]] += 1.0;
+    }
+    for (int i = 0; i < nn; i++) {
+        if (net.nodeType[i] == OUTFALL || net.nodeType[i] == STORAGE) continue;
+        if (net.initDepth[i] > 0.0) continue;
+        if (cnt[i] > 0.0) s.newDepth[i] = acc[i] / cnt[i];
+    }
+    for (int i = 0; i < nl; i++) {                  // link_setOutfallDepth for all links
+        int k;
+        double zz;
+        if (net.nodeType[net.node2[i]] == OUTFALL) { k = net.node2[i]; zz = net.offset2[i]; }
+        else if (net.nodeType[net.node1[i]] == OUTFALL) { k = net.node1[i]; zz = net.offset1[i]; }
+        else continue;
+        Geom g = geom(i);
+        double q = fabs(s.lNewFlow[i] / net.barrels[i]);
+        double yNorm = linkYnorm(g, q, net.qMax[i], net.beta[i], ct);
+        double yCrit = getYcrit(g, q, ct);
+        // outfall_setOutletDepth (node.c:1413-1492), FREE/NORMAL/FIXED/TSERIES
+        double stage, yNew;
+        int ot = net.outfallType[k];
+        if (ot == O_FREE) { s.newDepth[k] = (zz > 0.0) ? 0.0 : gmin(yNorm, yCrit); continue; }
+        if (ot == O_NORMAL) { s.newDepth[k] = (zz > 0.0) ? 0.0 : yNorm; continue; }
+        if (ot == O_FIXED) stage = net.fixedStage[k];
+        else stage = tseriesLookup(net.outfallSeries[k], opt.startDateTime + 0.0 / kMsecPerDay, true) / ucfLength();
+        yCrit = gmin(yCrit, yNorm);
+        if (yCrit + zz + net.invertElev[k] < stage) yNew = stage - net.invertElev[k];
+        else if (zz > 0.0) {
+            if (stage < net.invertElev[k] + zz) yNew = gmax(0.0, (stage - net.invertElev[k]));
+            else yNew = zz + yCrit;
+        } else yNew = yCrit;
+        s.newDepth[k] = yNew;
+    }
+    // initLinkDepths (flowrout.c:389-421)
+    for (int i = 0; i < nl; i++) {
+        if (net.q0[i] != 0.0) continue;
+        double y1 = s.newDepth[net.node1[i]] - net.offset1[i];
+        y1 = gmax(y1, 0.0);
+        y1 = gmin(y1, net.xsect[i].yFull);
+        double y2 = s.newDepth[net.node2[i]] - net.offset2[i];
+        y2 = gmax(y2, 0.0);
+        y2 = gmin(y2, net.xsect[i].yFull);
+        double y = 0.5 * (y1 + y2);
+        y = gmax(y, kFudge);
+        s.lNewDepth[i] = y;
+    }
+}
+
+int Project::initState()
 {
     int nn = net.nNodes(), nl = net.nLinks(), P = net.nPollut();
     const double* ct = &SWX_CIRC_TABLES[0][0];
@@ -1273,6 +1482,9 @@ void Project::initState()
         s.lNewDepth[j] = linkYnorm(g, net.q0[j] / net.barrels[j], net.qMax[j], net.beta[j], ct);
         s.lOldDepth[j] = s.lNewDepth[j];
     }
+    // hotstart_open (swmm5.c:385) between project_init and routing_open
+    bool hot = !hotstartUse.empty();
+    if (hot && readHotstart()) return errorCode;
     // flowrout_init DW (flowrout.c:75-103): dynwave_init crown elevations
     for (int i = 0; i < nl; i++) {
         int j = net.node1[i];
@@ -1284,56 +1496,8 @@ void Project::initState()
         s.flowClass[i] = F_DRY;
         s.dqdh[i] = 0.0;
     }
-    // initNodeDepths (flowrout.c:337-385)
-    std::vector<double> acc(nn, 0.0), cnt(nn, 0.0);
-    for (int i = 0; i < nl; i++) {
-        double y = (s.lNewDepth[i] > kFudge) ? s.lNewDepth[i] + net.offset1[i] : 0.0;
-        acc[net.node1[i]] += y; cnt[net.node1[i]] += 1.0;
-        acc[net.node2[i]] += y; cnt[net.node2[i]] += 1.0;
-    }
-    for (int i = 0; i < nn; i++) {
-        if (net.nodeType[i] == OUTFALL || net.nodeType[i] == STORAGE) continue;
-        if (net.initDepth[i] > 0.0) continue;
-        if (cnt[i] > 0.0) s.newDepth[i] = acc[i] / cnt[i];
-    }
-    for (int i = 0; i < nl; i++) {                  // link_setOutfallDepth for all links
-        int k;
-        double zz;
-        if (net.nodeType[net.node2[i]] == OUTFALL) { k = net.node2[i]; zz = net.offset2[i]; }
-        else if (net.nodeType[net.node1[i]] == OUTFALL) { k = net.node1[i]; zz = net.offset1[i]; }
-        else continue;
-        Geom g = geom(i);
-        double q = fabs(s.lNewFlow[i] / net.barrels[i]);
-        double yNorm = linkYnorm(g, q, net.qMax[i], net.beta[i], ct);
-        double yCrit = getYcrit(g, q, ct);
-        // outfall_setOutletDepth (node.c:1413-1492), FREE/NORMAL/FIXED/TSERIES
-        double stage, yNew;
-        int ot = net.outfallType[k];
-        if (ot == O_FREE) { s.newDepth[k] = (zz > 0.0) ? 0.0 : gmin(yNorm, yCrit); continue; }
-        if (ot == O_NORMAL) { s.newDepth[k] = (zz > 0.0) ? 0.0 : yNorm; continue; }
-        if (ot == O_FIXED) stage = net.fixedStage[k];
-        else stage = tseriesLookup(net.outfallSeries[k], opt.startDateTime + 0.0 / kMsecPerDay, true) / ucfLength();
-        yCrit = gmin(yCrit, yNorm);
-        if (yCrit + zz + net.invertElev[k] < stage) yNew = stage - net.invertElev[k];
-        else if (zz > 0.0) {
-            if (stage < net.invertElev[k] + zz) yNew = gmax(0.0, (stage - net.invertElev[k]));
-            else yNew = zz + yCrit;
-        } else yNew = yCrit;
-        s.newDepth[k] = yNew;
-    }
-    // initLinkDepths (flowrout.c:389-421)
-    for (int i = 0; i < nl; i++) {
-        if (net.q0[i] != 0.0) continue;
-        double y1 = s.newDepth[net.node1[i]] - net.offset1[i];
-        y1 = gmax(y1, 0.0);
-        y1 = gmin(y1, net.xsect[i].yFull);
-        double y2 = s.newDepth[net.node2[i]] - net.offset2[i];
-        y2 = gmax(y2, 0.0);
-        y2 = gmin(y2, net.xsect[i].yFull);
-        double y = 0.5 * (y1 + y2);
-        y = gmax(y, kFudge);
-        s.lNewDepth[i] = y;
-    }
+    // initNodeDepths / initLinkDepths only without a hot start file (flowrout.c:89-94)
+    if (!hot) initDepths();
     // initNodes (flowrout.c:425-468)
     for (int i = 0; i < nn; i++) {
         s.inflow[i] = s.newLatFlow[i];
@@ -1361,8 +1525,8 @@ void Project::initState()
         s.lNewVolume[i] = s.a1[i] * net.length[i] * net.barrels[i];
         s.lOldVolume[i] = s.lNewVolume[i];
     }
-    // qualrout_init (qualrout.c:63-96)
-    for (int p = 0; p < P; p++) {
+    // qualrout_init (qualrout.c:63-96), skipped with a hot start file (routing.c:122)
+    for (int p = 0; p < P && !hot; p++) {
         double c0 = net.pollut[p].cInit;
         for (int i = 0; i < nn; i++) {
             double c = (s.newDepth[i] > 0.003281) ? c0 : 0.0;
@@ -1375,6 +1539,7 @@ void Project::initState()
             s.lNewQual[p * nl + i] = c;
         }
     }
+    return 0;
 }
 
 // ================================================================= inflows

@@ -36,12 +36,17 @@ public:
     State st;
     RunStats stats;                        // filled by Router::downloadStats
     std::vector<int> rptNodes, rptLinks;   // explicit [REPORT] lists
+    std::string inpDir;                    // directory of the .inp (InpDir, swmm5.c:288)
+    std::string hotstartUse, hotstartSave; // [FILES] USE / SAVE HOTSTART (iface.c:103-114)
     int errorCode = 0;
     std::string errorMsg;
     int warnings = 0;
 
     int open(const char* inpPath);          // swmm_open: read + validate
-    void initState();                       // swmm_start: project_init + routing init
+    int initState();                        // swmm_start: project_init + hot start + routing init
+    // hotstart_close / saveRouting (hotstart.c:84-92, 213-250) from the host
+    // mirror of the final state
+    int saveHotstart();
     double ucfLength() const;
     double ucfFlow() const;
     double ucfVolume() const;
@@ -69,6 +74,9 @@ private:
     int readConduit(std::vector<char*>& tok);
     int readXsect(std::vector<char*>& tok);
     int readLoss(std::vector<char*>& tok);
+    int readFiles(std::vector<char*>& tok);
+    int readHotstart();
+    void initDepths();
     int readPollutant(std::vector<char*>& tok);
     int readInflow(std::vector<char*>& tok);
     int readDwf(std::vector<char*>& tok);

@@ -56,6 +56,17 @@ public:
     int setDuration(double msec);
     // Copy device state into the host mirror (prj.st); synchronises.
     int download(Project& prj);
+    // One state value of node / link g (global index) straight from HBM;
+    // returns nonzero when the object is not held by this rank.  Synchronises.
+    enum { PK_NODE_DEPTH, PK_NODE_VOLUME, PK_NODE_LATFLOW, PK_NODE_INFLOW, PK_NODE_OVERFLOW,
+           PK_LINK_FLOW, PK_LINK_DEPTH, PK_LINK_SETTING };
+    int peek(int field, int g, double* v);
+    // swmm_setValue(NODE_HEAD) on an outfall: FIXED type with this stage (ft)
+    // (setOutfallStage, swmm5.c:1173-1188)
+    int setOutfallStage(int g, double stage);
+    // swmm_setValue(ROUTESTEP) between steps (setRoutingStep, swmm5.c:1360-
+    // 1370): fixed steps of `step` sec from now on, next step dtNext sec
+    int setRouteStep(double step, double dtNext);
     // Results of one reporting period packed on the device in the .out
     // variable order (nodes: 6 + P floats each, links: 5 + P), interpolated
     // with weight f and converted with the unit factors; pointers to pinned

@@ -248,8 +248,9 @@ LINKS ALL
 
 def write_example(path: str, *, route_step: float = 5.0,
                   variable_step: float = 0.0, end_time: str = "04:00:00",
-                  pollutants: bool = False) -> None:
-    """Write the authored Example network (see module docstring)."""
+                  pollutants: bool = False, files: str = "") -> None:
+    """Write the authored Example network (see module docstring).  `files`
+    is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf")."""
     if pollutants:
         pollut = ("TSS MG/L 0 0 0 0.5 NO * 0 20 0\n"
                   "BOD MG/L 0 0 0 0 NO * 0 10 0\n")
@@ -261,6 +262,8 @@ def write_example(path: str, *, route_step: float = 5.0,
                           end_time=end_time, pollut=pollut,
                           qual_inflow=qual_inflow, qual_dwf=qual_dwf,
                           pollut_opt="")
+    if files:
+        txt += "\n[FILES]\n" + files.rstrip("\n") + "\n"
     d = os.path.dirname(os.path.abspath(path))
     os.makedirs(d, exist_ok=True)
     with open(path, "w") as f:

@@ -2,13 +2,18 @@
 from __future__ import annotations
 
 import os
+import shutil
+import tempfile
 
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLDEN = os.path.join(HERE, "golden")
 CASES = ["grid12", "grid12_var_qual", "grid10_surcharge", "example", "example_var",
-         "example_qual"]
+         "example_qual", "example_hotsave", "example_hot", "example_api"]
+# cases whose input writes a file next to itself ([FILES] SAVE ...): they run
+# from a private copy so the fixtures directory is never written to
+SAVES = {"example_hotsave": "example_hotsave.hsf"}
 # DWF-only networks: lateral inflow is constant and pollutant loads are
 # q * concentration, so the oracle can be fed without the inflow machinery
 DWF_ONLY = {"grid12", "grid12_var_qual", "grid10_surcharge"}
@@ -21,7 +26,12 @@ def load(name: str) -> dict:
 
 
 def inp(name: str) -> str:
-    return os.path.join(GOLDEN, name + ".inp")
+    src = os.path.join(GOLDEN, name + ".inp")
+    if name not in SAVES:
+        return src
+    d = tempfile.mkdtemp(prefix="swmm_golden_")
+    shutil.copy(src, d)
+    return os.path.join(d, name + ".inp")
 
 
 def ref_out(name: str) -> bytes:
@@ -46,3 +56,28 @@ def grid_qual_loads(d: dict, lat: np.ndarray) -> np.ndarray:
         w = np.where(pos, w - q * dc, 0.0)
         out[p] = w
     return out
+
+
+# ------------------------------------------------------------------ API cases
+# swmm_setValue calls the reference run made between steps (make_golden.py
+# ACTIONS, recorded as "api.actions"): (afterStep, property, objectName, value)
+def actions(d: dict) -> list:
+    if "api.actions" not in d:
+        return []
+    out = []
+    for tok in bytes(d["api.actions"]).decode().split(";"):
+        at, prop, name, val = tok.split(":")
+        out.append((int(at), int(prop), name, float(val)))
+    return out
+
+
+def apply_actions(s, acts: list, done: int) -> None:
+    """Make the same swmm_setValue calls on engine `s` once `done` steps ran."""
+    for at, prop, name, val in acts:
+        if at != done:
+            continue
+        idx = -1
+        if name != "-":
+            idx = s.getIndex(2 if prop < 400 else 3, name)
+            assert idx >= 0, name
+        s.setValue(prop, idx, val)

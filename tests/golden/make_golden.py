@@ -12,7 +12,8 @@ swmm_start and its full-precision state after every `every`-th routing step
 (oracle/refdump.c reads them from the reference's exported globals), plus
 the run statistics (NodeStats / LinkStats / OutfallStats, "st.*") after the
 last step, the reference's binary results (<case>.ref_out.npy) and its report
-file (<case>.ref_rpt.txt).
+file (<case>.ref_rpt.txt) and, for a case that saves a hot start file, that
+file (<case>.ref.hsf).
 """
 import os
 import subprocess
@@ -43,6 +44,21 @@ CASES = {
                                                variable_step=0.75), 1),
     "example_qual": (netgen.write_example, dict(end_time="01:00:00", route_step=5.0,
                                                 pollutants=True), 1),
+    # hot start: the first run saves its final state, the second starts from
+    # the reference's saved file (kept as example_hotsave.ref.hsf)
+    "example_hotsave": (netgen.write_example, dict(end_time="01:00:00", route_step=5.0,
+                                                   pollutants=True,
+                                                   files="SAVE HOTSTART example_hotsave.hsf"), 1),
+    "example_hot": (netgen.write_example, dict(end_time="01:00:00", route_step=5.0,
+                                               pollutants=True,
+                                               files="USE HOTSTART example_hotsave.ref.hsf"), 1),
+    # swmm_setValue between steps: external inflow, outfall stage, routing step
+    "example_api": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
+                                               variable_step=0.75), 1),
+}
+# REFDUMP_ACTIONS per case: "afterStep:property:object:value" (swmm5.h codes)
+ACTIONS = {
+    "example_api": "40:306:N3:2.5;90:304:O1:104.2;150:3:-:4.0;200:306:N3:0.0;260:304:O2:104.5",
 }
 
 
@@ -56,9 +72,14 @@ def make(name):
     else:
         writer(inp, **kw)
     tmp = "/tmp/golden_" + name
+    env = dict(os.environ)
+    if name in ACTIONS:
+        env["REFDUMP_ACTIONS"] = ACTIONS[name]
     subprocess.run([REFDUMP, inp, tmp + ".rpt", tmp + ".out", tmp + ".bin", "0", str(every)],
-                   check=True, stdout=subprocess.DEVNULL)
+                   check=True, stdout=subprocess.DEVNULL, env=env)
     d = read_dump(tmp + ".bin")
+    if name in ACTIONS:
+        d["api.actions"] = np.frombuffer(ACTIONS[name].encode(), dtype=np.uint8)
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
     with open(tmp + ".out", "rb") as f:
         out = f.read()
@@ -66,6 +87,9 @@ def make(name):
     # the reference's report file (summary tables after swmm_report)
     with open(tmp + ".rpt") as f, open(os.path.join(HERE, name + ".ref_rpt.txt"), "w") as g:
         g.write(f.read())
+    saved = os.path.join(HERE, name + ".hsf")
+    if os.path.exists(saved):
+        os.replace(saved, os.path.join(HERE, name + ".ref.hsf"))
     print(name, len(d["s.dt"]), "steps", os.path.getsize(os.path.join(HERE, name + ".npz")), "bytes")
 
 

@@ -40,7 +40,9 @@ def _run(name, tmp_path):
     rec = 0
     fc_agree = fc_total = 0
     worst = 0.0
+    acts = _golden.actions(d)
     for step in range(1, total + 1):
+        _golden.apply_actions(s, acts, step - 1)
         err, t = s.step()
         assert err == 0, s.getError()
         if step % ev == 0 or step == total:

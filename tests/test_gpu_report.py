@@ -80,8 +80,11 @@ def test_report_tables_match_reference(name, tmp_path):
     s = swmm5.SWMM()
     assert s.open(_golden.inp(name), rpt, out) == 0, s.getError()
     assert s.start(True) == 0, s.getError()
+    acts, done = _golden.actions(_golden.load(name)), 0
     while True:
+        _golden.apply_actions(s, acts, done)
         err, t = s.step()
+        done += 1
         assert err == 0, s.getError()
         if t == 0.0:
             break

@@ -25,8 +25,11 @@ def _run(name, tmp_path):
     s = swmm5.SWMM()
     assert s.open(_golden.inp(name), str(tmp_path / "s.rpt"), str(tmp_path / "s.out")) == 0
     assert s.start(True) == 0, s.getError()
+    acts, done = _golden.actions(d), 0
     while True:
+        _golden.apply_actions(s, acts, done)
         err, t = s.step()
+        done += 1
         assert err == 0, s.getError()
         if t == 0.0:
             break

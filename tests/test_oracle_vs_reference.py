@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 import _golden
+import swmm5
 from _oracle import oracle_from_dump
 
 NODE_F = ["newDepth", "newVolume", "inflow", "outflow", "overflow"]
@@ -28,8 +29,27 @@ def _replay(name):
     total = int(d["s.every"][1])
     dwf = name in _golden.DWF_ONLY
     rec = 0
+    fixed = d["opt.d"][0]
+    acts = _golden.actions(d)
+    ids = {}
+    if acts:                                   # object names -> indices (host-only open)
+        s = swmm5.SWMM()
+        assert s.open(_golden.inp(name), "/tmp/_orc_api.rpt", "/tmp/_orc_api.out") == 0
+        for _, prop, nm, _ in acts:
+            if nm != "-":
+                ids[nm] = s.getIndex(swmm5.NODE if prop < 400 else swmm5.LINK, nm)
+        s.close()
     for step in range(1, total + 1):
-        dt = o.routing_step(d["opt.d"][0])
+        for at, prop, nm, val in acts:         # swmm_setValue between steps
+            if at != step - 1:
+                continue
+            if prop == swmm5.ROUTESTEP:        # setRoutingStep (swmm5.c:1360-1370)
+                o.opt("courantFactor", 0.0)
+                fixed = max(val, o.get("minRouteStep"))
+            elif prop == swmm5.NODE_HEAD:      # setOutfallStage (swmm5.c:1173-1188), CFS units
+                o.d("node.fixedStage")[ids[nm]] = val
+                o.i("node.outfallType")[ids[nm]] = 2
+        dt = o.routing_step(fixed)
         if dwf:
             lat = d["s.node.newLatFlow"][0]
         else:
