@@ -240,6 +240,9 @@ def main():
     bypass = None
     if it_n:
         bypass = 100.0 * (1.0 - tw["timed_updated"] / (it_n * tw["streaming_conduits"]))
+    regather = None
+    if tw.get("timed_gather_iters"):
+        regather = 100.0 * tw["timed_gathered"] / (tw["timed_gather_iters"] * tw["nodes"])
     traffic = args.traffic
     traffic_src = "--traffic" if traffic is not None else None
     if traffic is None:                    # PMC measurement committed for this workload
@@ -265,7 +268,8 @@ def main():
                                      "achieved_GBs": round(gbs("link_momentum_iter"), 1),
                                      "bypassed_pct": None if bypass is None else round(bypass, 2)},
             "k_node": {"avg_launch_us": round(avg_us("node_update"), 2),
-                       "achieved_GBs": round(gbs("node_update"), 1)},
+                       "achieved_GBs": round(gbs("node_update"), 1),
+                       "regathered_pct_iter_ge2": None if regather is None else round(regather, 2)},
             "k_step_end+k_finalize": {"avg_launch_us": round(avg_us("step_end"), 2),
                                       "achieved_GBs": round(gbs("step_end"), 1)},
         },

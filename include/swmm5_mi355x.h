@@ -38,7 +38,9 @@ int    DLLEXPORT swmmx_runSteps(int n, double *elapsedTime);
  * [2] non-converging steps, [3] Picard iterations of the last step,
  * [4] true conduits, [5] nodes, [6] conduits updated (not bypassed) by the
  * Picard iterations >= 1 timed since swmmx_setTiming(1), [7] conduits handled
- * by the streaming link kernel.  Synchronises with the device. */
+ * by the streaming link kernel, [8] nodes that re-gathered their conduits in
+ * the timed iterations >= 2 (the others kept their previous sums), [9] timed
+ * iterations >= 2.  Synchronises with the device. */
 int    DLLEXPORT swmmx_getCounters(long long *out, int n);
 
 /* Device kernel timing (HIP events on the routing stream; steps run as eager

@@ -919,17 +919,19 @@ int DLLEXPORT swmmx_exportState(const char* path)
 int DLLEXPORT swmmx_getCounters(long long* out, int n)
 {
     if (!G || !out) return 0;
-    long long v[8] = {G->totalStepCount, 0, 0, 0, G->prj->net.nLinks(), G->prj->net.nNodes(), 0, 0};
+    long long v[10] = {G->totalStepCount, 0, 0, 0, G->prj->net.nLinks(), G->prj->net.nNodes(), 0, 0, 0, 0};
     if (G->router && G->router->ok()) {
         int last = 0;
         G->router->counters(&v[1], &v[2], &last);
         v[3] = last;
-        double upd = 0, hot = 0;
-        G->router->timedWork(&upd, &hot);
+        double upd = 0, hot = 0, gat = 0, git = 0;
+        G->router->timedWork(&upd, &hot, &gat, &git);
         v[6] = (long long)upd;
         v[7] = (long long)hot;
+        v[8] = (long long)gat;
+        v[9] = (long long)git;
     }
-    int m = n < 8 ? n : 8;
+    int m = n < 10 ? n : 10;
     for (int i = 0; i < m; i++) out[i] = v[i];
     return m;
 }

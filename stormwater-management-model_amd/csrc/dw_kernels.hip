@@ -107,6 +107,8 @@ struct StepCtl {
     double routingDuration;           // msec
     double routeStep;                 // fixed step (sec)
     unsigned long long linkWork[kMaxTrialsCap];   // timing mode: conduits updated per iteration
+    unsigned long long nodeWork[kMaxTrialsCap];   // timing mode: nodes gathered per iteration
+    int ucount[kMaxTrialsCap];    // unconverged nodes (+ outfalls) listed by k_node at iteration k
     double stepRed[kNumPartials];     // this step's reduced block partials (k_finalize)
     // run statistics (stats.c): report-period step count / span, max system
     // outfall flow, routing time-step statistics (stats_updateTimeStepStats)
@@ -163,6 +165,17 @@ struct Params {
     double *nNewDepth, *nOldDepth, *nNewVolume, *nOldVolume, *inflow, *outflow, *overflow;
     double *newLat, *oldLat, *oldNetInflow, *oldFlowInflow, *oldSurfArea, *dYdT;
     int* conv;
+    // node sums of the last gather (surface area, sum dq/dh; inflow/outflow
+    // live in inflow/outflow) and a per-node "an incident conduit was updated
+    // in this iteration" flag: a node whose conduits were all bypassed keeps
+    // the sums of its previous gather (identical operands, identical sums)
+    double *nSurf, *nDqdh;
+    unsigned char* dirty;         // bit 0: an incident conduit was updated; bit 1: yRaw valid
+    // A clean junction whose last update was plain (not surcharged, ponded or
+    // flooded, no volume) has an unchanged unrelaxed depth yRaw = yOld + dV /
+    // surfArea, so its next update is just the relaxation 0.5 yLast + 0.5 yRaw
+    double *yRaw, *yMaxNP;        // yMaxNP = fullDepth + surDepth (non-ponding yMax)
+    int* ulist;                   // [2][nN] unconverged nodes of the last two iterations
     const double* latIn;          // lateral inflow for this step
     // quality [p][object]
     double *nOldQual, *nNewQual, *lOldQual, *lNewQual;
@@ -621,16 +634,45 @@ void k_link(Params p, int k)
     if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;     // converged: dynwave.c:249-251
     if (p.nShared && blockIdx.x == 0 && threadIdx.x == 0) p.xsend[p.xflag] = 0.0;   // k_node sets it
     __shared__ double ct[5 * SWX_CIRC_N];
-    stageTables(ct, p.gTables);
     double dt = p.ctl->dt;
     int work = 0;
-    for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nL; j += gridDim.x * kBlock) {
-        uint32_t f = p.lflags[j];
-        if (f & LF_COLD) continue;
-        int2 nn = p.lnodes[j];
-        if (k >= 2 && p.conv[nn.x] && p.conv[nn.y]) continue;   // findBypassedLinks dynwave.c:335-345
-        conduitFlow<kFirst, false, kFast>(p, j, f, nn, k, dt, ct);
-        work++;
+    if (kFirst && blockIdx.x == 0 && threadIdx.x < kMaxTrialsCap) p.ctl->ucount[threadIdx.x] = 0;
+    if (kFirst || k < 2) {
+        stageTables(ct, p.gTables);
+        for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nL; j += gridDim.x * kBlock) {
+            uint32_t f = p.lflags[j];
+            if (f & LF_COLD) continue;
+            conduitFlow<kFirst, false, kFast>(p, j, f, p.lnodes[j], k, dt, ct);
+        }
+    } else {
+        // Later iterations: a conduit is updated unless both end nodes have
+        // converged (findBypassedLinks dynwave.c:335-345), i.e. exactly the
+        // conduits incident to the nodes k_node listed as unconverged in the
+        // previous iteration (outfalls are always listed).  Four threads per
+        // listed node walk its CSR row; a conduit whose ends are both listed
+        // is taken by the lower-numbered end.
+        const int cnt = p.ctl->ucount[k - 1];
+        const int* list = p.ulist + (size_t)((k - 1) & 1) * p.nN;
+        const int slots = 4 * cnt;
+        if (blockIdx.x * kBlock < slots) {                  // uniform per block
+            stageTables(ct, p.gTables);
+            for (int t = blockIdx.x * kBlock + threadIdx.x; t < slots; t += gridDim.x * kBlock) {
+                int u = list[t >> 2];
+                int e1 = p.rowptr[u + 1];
+                for (int e = p.rowptr[u] + (t & 3); e < e1; e += 4) {
+                    int l = p.csr[e] & 0x7FFFFFFF;
+                    uint32_t f = p.lflags[l];
+                    if (f & LF_COLD) continue;                // k_link_cold's
+                    int2 nn = p.lnodes[l];
+                    int v = (nn.x == u) ? nn.y : nn.x;
+                    if (!p.conv[v] && v < u) continue;        // listed too: v takes it
+                    conduitFlow<kFirst, false, kFast>(p, l, f, nn, k, dt, ct);
+                    p.dirty[nn.x] = 1;
+                    p.dirty[nn.y] = 1;
+                    work++;
+                }
+            }
+        }
     }
     // measurement only (eager timing launches, iterations >= 2 where links can
     // be bypassed): one atomic per workgroup after an LDS reduction
@@ -689,6 +731,7 @@ __global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
         int2 nn = p.lnodes[j];
         if (k >= 2 && p.conv[nn.x] && p.conv[nn.y]) continue;
         conduitFlow<kFirst, true>(p, j, f, nn, k, dt, ct);
+        if (k >= 2) { p.dirty[nn.x] = 1; p.dirty[nn.y] = 1; }
     }
 }
 
@@ -713,9 +756,11 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
         else isSurcharged = (yCrown > 0.0 && yLast > yCrown);
     }
     double yNew, dy;
+    double yRaw = 0.0;
     if (!isSurcharged) {
         dy = dV / surfArea;
         yNew = yOld + dy;
+        yRaw = yNew;
         if (!isPonded) p.oldSurfArea[i] = surfArea;
         if (k > 0) yNew = (1.0 - omega) * yLast + omega * yNew;
         if (isPonded && yNew < fullDepth) yNew = fullDepth - 0.0001;
@@ -736,7 +781,13 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
     double yMax = fullDepth;
     if (!canPond) yMax += p.surDepth[i];
     double fullVolume = p.fullVolume[i];
-    if (yNew > yMax) {                                 // getFloodedDepth dynwave.c:766-795
+    const bool flooded = yNew > yMax;
+    if (k >= 1) {                                      // fast-path cache for the next iteration
+        bool plain = !isSurcharged && !canPond && !flooded && fullVolume == 0.0;
+        if (plain) p.yRaw[i] = yRaw;
+        p.dirty[i] = plain ? 2 : 0;
+    }
+    if (flooded) {                                     // getFloodedDepth dynwave.c:766-795
         double newVolume;
         if (!canPond) {
             overflow = dV / dt;
@@ -753,8 +804,7 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
         p.nNewVolume[i] = (fullDepth > 0.0) ? fullVolume * (yNew / fullDepth) : 0.0;
     }
     p.overflow[i] = overflow;
-    p.dYdT[i] = fabs(yNew - yOld) / dt;
-    p.nNewDepth[i] = yNew;
+    p.nNewDepth[i] = yNew;        // Xnode.dYdT = |yNew - yOld| / dt: formed at the step end
     int c = (fabs(yLast - yNew) > p.headTol) ? 0 : 1;  // dynwave.c:615-621
     p.conv[i] = c;
     return c;
@@ -785,11 +835,34 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
     }
     const double dt = p.ctl->dt;
     bool anyUnconv = false;
+    int gathered = 0;
+    int* ulist = p.ulist + (size_t)(k & 1) * p.nN;
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
         uint32_t nf = p.nflags[i];
         int type = (int)(nf & NF_TYPE);
         // an outfall's depth is written by the prologue above: not read here
         double yLast = (type == OUTFALL) ? 0.0 : p.nNewDepth[i];
+        bool listMe = (type == OUTFALL);       // unconverged after this iteration
+        bool done = false;
+        if (!kFirst && k >= 2 && type != OUTFALL && !(nf & NF_SHARED) && p.dirty[i] == 2) {
+            // plain clean junction: the relaxation step of setNodeDepth
+            // (dynwave.c:700-715) on the cached unrelaxed depth
+            double yCrown = p.yCrown[i];
+            bool sur = p.surchargeMethod == SUR_EXTRAN && yCrown > 0.0 && yLast > yCrown;
+            if (!sur) {
+                const double omega = 0.5;
+                double yNew = (1.0 - omega) * yLast + omega * p.yRaw[i];
+                if (yNew < 0) yNew = 0.0;
+                if (!(yNew > p.yMaxNP[i])) {
+                    p.nNewDepth[i] = yNew;
+                    int c = (fabs(yLast - yNew) > p.headTol) ? 0 : 1;
+                    p.conv[i] = c;
+                    if (!c) { anyUnconv = true; listMe = true; }
+                    done = true;
+                }
+            }
+        }
+        if (!done) {
         double yOld, lat;
         if (kFirst) {
             // routing.c:328-332, node.c:293-304, 325-341 -- step-begin rotation
@@ -806,58 +879,90 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
             yOld = p.nOldDepth[i];
             lat = p.newLat[i];
         }
-        // initNodeStates (dynwave.c:297-331)
-        bool canPond = (nf & NF_CANPOND) != 0;
-        double fullDepth = p.fullDepth[i];
-        double surf = 0.0;
-        if (canPond && yLast > fullDepth && !(nf & NF_REPLICA)) surf = p.pondedArea[i];  // owner adds it
-        double inflow = 0.0, outflow = 0.0;   // node losses are 0 for non-storage nodes
-        if (lat >= 0.0) inflow += lat;
-        else outflow -= lat;
-        double sumdqdh = 0.0;
-        // CSR gather in link-index order == updateNodeFlows serial order
-        int e0 = p.rowptr[i], e1 = p.rowptr[i + 1];
-        for (int e = e0; e < e1; e++) {
-            int ent = p.csr[e];
-            int l = ent & 0x7FFFFFFF;
-            bool isN2 = ent < 0;
-            double q = p.lNewFlow[l];
-            uint32_t lf = p.lflags[l];
-            double barrels = (double)((lf >> LF_BARREL_SHIFT) & 0xFF);
-            if (!isN2) {
-                if (q >= 0.0) outflow += q; else inflow -= q;
-            } else {
-                if (q >= 0.0) inflow += q; else outflow -= q;
-            }
-            if (lf & LF_SEEP) {
-                double lossRate = (p.evapLoss[l] + p.seepLoss[l]) * barrels;
-                if (lossRate > 0.0) {
-                    bool o1 = (lf & LF_N1_OUTFALL) != 0, o2 = (lf & LF_N2_OUTFALL) != 0;
-                    if (!o1 && !o2) lossRate /= 2.0;
-                    if (!isN2 && !o1) outflow += lossRate;
-                    if (isN2 && !o2) outflow += lossRate;
+        double inflow, outflow, surf, sumdqdh;
+        const bool reuse = !kFirst && k >= 2 && !(nf & (NF_CANPOND | NF_SHARED)) && !(p.dirty[i] & 1);
+        if (reuse) {
+            inflow = p.inflow[i];
+            outflow = p.outflow[i];
+            surf = p.nSurf[i];
+            sumdqdh = p.nDqdh[i];
+        } else {
+            // initNodeStates (dynwave.c:297-331)
+            bool canPond = (nf & NF_CANPOND) != 0;
+            double fullDepth = p.fullDepth[i];
+            surf = 0.0;
+            if (canPond && yLast > fullDepth && !(nf & NF_REPLICA)) surf = p.pondedArea[i];  // owner adds it
+            inflow = 0.0;
+            outflow = 0.0;                        // node losses are 0 for non-storage nodes
+            if (lat >= 0.0) inflow += lat;
+            else outflow -= lat;
+            sumdqdh = 0.0;
+            // CSR gather in link-index order == updateNodeFlows serial order
+            int e0 = p.rowptr[i], e1 = p.rowptr[i + 1];
+            for (int e = e0; e < e1; e++) {
+                int ent = p.csr[e];
+                int l = ent & 0x7FFFFFFF;
+                bool isN2 = ent < 0;
+                double q = p.lNewFlow[l];
+                uint32_t lf = p.lflags[l];
+                double barrels = (double)((lf >> LF_BARREL_SHIFT) & 0xFF);
+                if (!isN2) {
+                    if (q >= 0.0) outflow += q; else inflow -= q;
+                } else {
+                    if (q >= 0.0) inflow += q; else outflow -= q;
                 }
+                if (lf & LF_SEEP) {
+                    double lossRate = (p.evapLoss[l] + p.seepLoss[l]) * barrels;
+                    if (lossRate > 0.0) {
+                        bool o1 = (lf & LF_N1_OUTFALL) != 0, o2 = (lf & LF_N2_OUTFALL) != 0;
+                        if (!o1 && !o2) lossRate /= 2.0;
+                        if (!isN2 && !o1) outflow += lossRate;
+                        if (isN2 && !o2) outflow += lossRate;
+                    }
+                }
+                surf += (isN2 ? p.sa2[l] : p.sa1[l]) * barrels;
+                sumdqdh += p.dqdh[l];
             }
-            surf += (isN2 ? p.sa2[l] : p.sa1[l]) * barrels;
-            sumdqdh += p.dqdh[l];
+            p.inflow[i] = inflow;
+            p.outflow[i] = outflow;
+            p.nSurf[i] = surf;
+            p.nDqdh[i] = sumdqdh;
+            if (!kFirst && k >= 2) p.dirty[i] = 0;
+            gathered++;
         }
-        p.inflow[i] = inflow;
-        p.outflow[i] = outflow;
-        if (type == OUTFALL) continue;                     // depth set by the prologue
-        if (nf & NF_SHARED) {                              // multi-GPU: partial sums out
+        if (type == OUTFALL) {
+            // depth set by the prologue
+        } else if (nf & NF_SHARED) {                       // multi-GPU: partial sums out
             int s4 = 4 * p.sharedSlot[i];
             p.xsend[s4] = inflow;
             p.xsend[s4 + 1] = outflow;
             p.xsend[s4 + 2] = surf;
             p.xsend[s4 + 3] = sumdqdh;
-            continue;
+            listMe = false;                                // k_node_shared lists it
+        } else if (!nodeUpdate(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh)) {
+            anyUnconv = true;
+            listMe = true;
         }
-        if (!nodeUpdate(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh)) anyUnconv = true;
+        }
+        // list this iteration's unconverged nodes for the next k_link
+        if (!kFirst) {
+            unsigned long long m = __ballot(listMe);
+            if (m) {
+                int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1, base = 0;
+                if (lane == leader) base = atomicAdd(&p.ctl->ucount[k], __popcll(m));
+                base = __shfl(base, leader, 64);
+                if (listMe) ulist[base + __popcll(m & ((1ull << lane) - 1ull))] = i;
+            }
+        }
     }
     // one flag per iteration; any writer stores 1 (no atomics needed)
     if (__any(anyUnconv) && (threadIdx.x & 63) == 0) {
         p.ctl->unconv[k] = 1;
         if (p.nShared) p.xsend[p.xflag] = 1.0;             // tell the other ranks
+    }
+    if (!kFirst && k >= 2 && p.countWork) {                // measurement only
+        for (int off = 32; off > 0; off >>= 1) gathered += __shfl_down(gathered, off, 64);
+        if ((threadIdx.x & 63) == 0 && gathered) atomicAdd(&p.ctl->nodeWork[k], (unsigned long long)gathered);
     }
 }
 
@@ -879,7 +984,18 @@ __global__ __launch_bounds__(kBlock) void k_node_shared(Params p, int k)
         p.outflow[i] = outflow;
         if ((int)(nf & NF_TYPE) == OUTFALL) continue;
         double yLast = p.nNewDepth[i], yOld = p.nOldDepth[i];
-        if (!nodeUpdate(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh)) anyUnconv = true;
+        bool listMe = false;
+        if (!nodeUpdate(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh)) {
+            anyUnconv = true;
+            listMe = true;
+        }
+        unsigned long long m = __ballot(listMe);          // next k_link's work list
+        if (m) {
+            int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1, base = 0;
+            if (lane == leader) base = atomicAdd(&p.ctl->ucount[k], __popcll(m));
+            base = __shfl(base, leader, 64);
+            if (listMe) p.ulist[(size_t)(k & 1) * p.nN + base + __popcll(m & ((1ull << lane) - 1ull))] = i;
+        }
     }
     if (__any(anyUnconv) && (threadIdx.x & 63) == 0) p.ctl->unconv[k] = 1;
     if (blockIdx.x == 0 && threadIdx.x == 0 && p.xrecv[p.xflag] > 0.0) p.ctl->unconv[k] = 1;
@@ -1117,6 +1233,8 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
             acc[2] += -q;
         }
         double newDepth = p.nNewDepth[i];
+        if (type != OUTFALL)              // setNodeDepth's last dYdT (dynwave.c:750)
+            p.dYdT[i] = fabs(newDepth - p.nOldDepth[i]) / dt;
         if (p.varStep && type != OUTFALL) {
             double y = newDepth;
             double yc = p.crownElev[i] - p.invert[i];
@@ -1408,7 +1526,7 @@ struct Router::Impl {
     bool constantInflow = true;
     struct TimingSlot {               // one timed step's events + readback
         std::vector<hipEvent_t> ev, evHot;
-        unsigned long long* pinned = nullptr;   // [0] Picard iterations run, [1..] conduits updated
+        unsigned long long* pinned = nullptr;   // [0] iterations run, [1..] conduits updated, nodes gathered
     };
     std::vector<TimingSlot> tslots;
     int tUsed = 0;
@@ -1419,6 +1537,8 @@ struct Router::Impl {
     long long kcnt[kClasses] = {};
     double kbytes[kClasses] = {};     // byte model per launch (class 4: per updated conduit)
     double kbytesSum[kClasses] = {};  // algorithmic bytes of the timed launches
+    double nodeFix = 0, nodeGather = 0;   // node byte model at iterations >= 2
+    double gatherSum = 0, gatherCnt = 0;  // nodes gathered at iterations >= 2
     double nHot = 0, nColdD = 0;
     double workSum = 0;               // conduits updated in timed iterations >= 1
     int nE = 0;
@@ -1698,7 +1818,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         p.nCold = (int)coldLinks.size();
         UPI(cl, outLinks, outLinks.size());
         p.outLinks = cl;
-        p.nOutLinks = (int)outLinks.size();
+        p.nOutLinks = getenv("SWMM5_TIMING_NO_OUTFALL") ? 0 : (int)outLinks.size();   // timing experiment only
     }
     double* tmp;
     UPD(tmp, inv1, nL); p.inv1 = tmp;
@@ -1822,6 +1942,20 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     UPD(p.oldNetInflow, gn(st.oldNetInflow), nN);
     UPD(p.oldFlowInflow, gn(st.oldFlowInflow), nN);
     UPD(p.oldSurfArea, gn(st.oldSurfArea), nN);
+    {   // gather-reuse sums (written by every gather before any reuse) and flags
+        std::vector<double> zN(nN, 0.0);
+        UPD(p.nSurf, zN, nN);
+        UPD(p.nDqdh, zN, nN);
+        UPD(p.yRaw, zN, nN);
+        std::vector<double> ym(nN);
+        for (size_t i = 0; i < nN; i++) ym[i] = net.fullDepth[LN[i]] + net.surDepth[LN[i]];
+        UPD(p.yMaxNP, ym, nN);
+        p.ulist = devAlloc<int>(d, 2 * (size_t)nN, &e);
+        if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+        p.dirty = devAlloc<unsigned char>(d, nN, &e);
+        if (e == hipSuccess) e = hipMemset(p.dirty, 0, std::max<size_t>(nN, 1));
+        if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+    }
     UPD(p.dYdT, gn(st.dYdT), nN);
     UPI(p.conv, gni(st.converged), nN);
     // ---- inflows ----------------------------------------------------------
@@ -2031,7 +2165,13 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         //   oldDepth, oldNetInflow, newLat, oldSurfArea: 40) + writes (inflow,
         //   outflow, newDepth, newVolume, overflow, dYdT, oldSurfArea, conv:
         //   7x8+4) ; per CSR entry: index 4 + newFlow, sa, dqdh 24 + flags 4
-        d->kbytes[1] = N * (44 + 4 + 40 + 60) + E * (4 + 24 + 4);
+        // iterations >= 2 also read the node's "conduit updated" flag 1; a node
+        //   whose conduits were all bypassed reads its previous sums (inflow,
+        //   outflow, surface area, sum dq/dh: 32) instead of rowptr + CSR;
+        //   a gathering node writes those 4 sums (32), dYdT moved to step end
+        d->kbytes[1] = N * (44 + 4 + 40 + 32 + 52) + E * (4 + 24 + 4);
+        d->nodeFix = N * (44 + 40 + 52 - 16 + 1);
+        d->nodeGather = 4 + 32 + (N > 0 ? (double)E / N * 32.0 : 0.0);
         d->kbytes[2] = L * (4 + 8 + 8 + 8 + 8 + 8 + 4) + N * (4 + 8 * 6);
         d->kbytes[3] = P ? (N * (24 + 16.0 * P) + E * (4 + 8 + 8.0 * P) + L * (72 + 24.0 * P)) : 0.0;
     }
@@ -2076,7 +2216,12 @@ static void flushTiming(Router::Impl* d)
                 d->kbytesSum[4] += w * d->kbytes[4] + (d->nHot - w) * 20.0 + d->nColdD * 4.0;
             }
             d->kms[1] += ms2; d->kcnt[1]++;
-            d->kbytesSum[1] += d->kbytes[1];
+            if (k < 2) d->kbytesSum[1] += d->kbytes[1];
+            else {
+                double g = (double)work[kMaxTrialsCap + k];
+                d->kbytesSum[1] += d->nodeFix + g * d->nodeGather + ((double)p.nN - g) * 32.0;
+                d->gatherSum += g; d->gatherCnt += 1;
+            }
         }
         int base = 4 * p.maxTrials;
         float ms3 = 0, msq = 0;
@@ -2133,7 +2278,7 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
             t.evHot.resize(kMaxTrialsCap);
             for (auto& ev : t.ev) HIPCHECK(hipEventCreate(&ev));
             for (auto& ev : t.evHot) HIPCHECK(hipEventCreate(&ev));
-            HIPCHECK(hipHostMalloc((void**)&t.pinned, (1 + kMaxTrialsCap) * sizeof(unsigned long long),
+            HIPCHECK(hipHostMalloc((void**)&t.pinned, (1 + 2 * kMaxTrialsCap) * sizeof(unsigned long long),
                                    hipHostMallocDefault));
         }
         Impl::TimingSlot& t = d->tslots[d->tUsed++];
@@ -2142,9 +2287,9 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
         launchStep(d);
         HIPCHECK(hipMemcpyAsync(t.pinned, &d->ctl->lastSteps, sizeof(int), hipMemcpyDeviceToHost,
                                 d->stream));
-        HIPCHECK(hipMemcpyAsync(t.pinned + 1, d->ctl->linkWork, kMaxTrialsCap * sizeof(unsigned long long),
+        HIPCHECK(hipMemcpyAsync(t.pinned + 1, d->ctl->linkWork, 2 * kMaxTrialsCap * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, d->stream));
-        HIPCHECK(hipMemsetAsync(d->ctl->linkWork, 0, kMaxTrialsCap * sizeof(unsigned long long), d->stream));
+        HIPCHECK(hipMemsetAsync(d->ctl->linkWork, 0, 2 * kMaxTrialsCap * sizeof(unsigned long long), d->stream));
     } else if (d->useGraph) {
         HIPCHECK(hipGraphLaunch(d->graph, d->stream));
     } else {
@@ -2497,6 +2642,8 @@ void Router::setTiming(bool on)
     d_->p.countWork = on ? 1 : 0;                  // eager launches only; the graph keeps 0
     for (int k = 0; k < Impl::kClasses; k++) { d_->kms[k] = 0; d_->kcnt[k] = 0; d_->kbytesSum[k] = 0; }
     d_->workSum = 0;
+    d_->gatherSum = 0;
+    d_->gatherCnt = 0;
 }
 
 // Back-to-back replays of one kernel between two events (average duration per
@@ -2657,11 +2804,13 @@ int Router::allreduceHost(double* buf, int n, int op)
     return 0;
 }
 
-void Router::timedWork(double* updated, double* hot)
+void Router::timedWork(double* updated, double* hot, double* gathered, double* gatherIters)
 {
     flushTiming(d_);
     *updated = d_->workSum;
     *hot = d_->nHot;
+    *gathered = d_->gatherSum;
+    *gatherIters = d_->gatherCnt;
 }
 
 int Router::kernelTimes(double* out, int n)

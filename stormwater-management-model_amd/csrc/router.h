@@ -44,7 +44,7 @@ public:
     // routing time (msec) and the step length used by that step.
     int readClock(double* newRoutingTime, double* lastDt, double* nextDt);
     // conduits updated by the timed iterations >= 1, and streaming conduits
-    void timedWork(double* updated, double* hot);
+    void timedWork(double* updated, double* hot, double* gathered, double* gatherIters);
     // Sum (op 0) or min (op 1) of n host doubles over the ranks (no-op on one GPU).
     int allreduceHost(double* buf, int n, int op);
     // average duration (us) of `reps` back-to-back launches of kernel `which`

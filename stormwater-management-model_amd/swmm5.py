@@ -226,10 +226,10 @@ class SWMM:
         return err, t.value
 
     def counters(self):
-        a = (ctypes.c_longlong * 8)()
-        self.L.swmmx_getCounters(a, 8)
+        a = (ctypes.c_longlong * 10)()
+        self.L.swmmx_getCounters(a, 10)
         keys = ["steps", "iterations", "nonconverged", "last_iterations", "conduits", "nodes",
-                "timed_updated", "streaming_conduits"]
+                "timed_updated", "streaming_conduits", "timed_gathered", "timed_gather_iters"]
         return dict(zip(keys, list(a)))
 
     def set_timing(self, on: bool):
