@@ -844,21 +844,25 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
         double yLast = (type == OUTFALL) ? 0.0 : p.nNewDepth[i];
         bool listMe = (type == OUTFALL);       // unconverged after this iteration
         bool done = false;
-        if (!kFirst && k >= 2 && type != OUTFALL && !(nf & NF_SHARED) && p.dirty[i] == 2) {
-            // plain clean junction: the relaxation step of setNodeDepth
-            // (dynwave.c:700-715) on the cached unrelaxed depth
-            double yCrown = p.yCrown[i];
-            bool sur = p.surchargeMethod == SUR_EXTRAN && yCrown > 0.0 && yLast > yCrown;
-            if (!sur) {
-                const double omega = 0.5;
-                double yNew = (1.0 - omega) * yLast + omega * p.yRaw[i];
-                if (yNew < 0) yNew = 0.0;
-                if (!(yNew > p.yMaxNP[i])) {
-                    p.nNewDepth[i] = yNew;
-                    int c = (fabs(yLast - yNew) > p.headTol) ? 0 : 1;
-                    p.conv[i] = c;
-                    if (!c) { anyUnconv = true; listMe = true; }
-                    done = true;
+        if (!kFirst && k >= 2) {
+            // all fast-path operands issued at once (one memory round trip)
+            unsigned char cache = p.dirty[i];
+            double yLast2 = p.nNewDepth[i], yCrown = p.yCrown[i], yRaw = p.yRaw[i], yMax = p.yMaxNP[i];
+            if (type != OUTFALL && !(nf & NF_SHARED) && cache == 2) {
+                // plain clean junction: the relaxation step of setNodeDepth
+                // (dynwave.c:700-715) on the cached unrelaxed depth
+                bool sur = p.surchargeMethod == SUR_EXTRAN && yCrown > 0.0 && yLast2 > yCrown;
+                if (!sur) {
+                    const double omega = 0.5;
+                    double yNew = (1.0 - omega) * yLast2 + omega * yRaw;
+                    if (yNew < 0) yNew = 0.0;
+                    if (!(yNew > yMax)) {
+                        p.nNewDepth[i] = yNew;
+                        int c = (fabs(yLast2 - yNew) > p.headTol) ? 0 : 1;
+                        p.conv[i] = c;
+                        if (!c) { anyUnconv = true; listMe = true; }
+                        done = true;
+                    }
                 }
             }
         }
