@@ -690,16 +690,24 @@ void k_link(Params p, int k)
 }
 
 // link_setOutfallDepth + outfall_setOutletDepth (link.c:728-766, node.c:1413-1492)
-__device__ __forceinline__ double outfallDepth(const Params& p, int i, uint32_t nf, int j,
-                                               uint32_t f, const double* ct)
+// link_setOutfallDepth + outfall_setOutletDepth (link.c:728-766, node.c:1413-1492),
+// in two halves that can run on different waves: the normal depth (kPart 0)
+// and the critical depth (kPart 1) of the outfall conduit's flow, then the
+// outlet depth from both (outfallCombine)
+template <int kPart>
+__device__ __forceinline__ double outfallPart(const Params& p, int j, uint32_t f, const double* ct)
 {
     Geom x = loadGeom(p, j, f);
     double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
+    double q = fabs(p.lNewFlow[j] / barrels);
+    if (kPart == 0) return linkYnorm(x, q, p.qMax[j], p.beta[j], ct);
+    return getYcrit(x, q, ct);
+}
+__device__ __forceinline__ double outfallCombine(const Params& p, int i, uint32_t nf, int j,
+                                                 double yNorm, double yCrit)
+{
     int2 nn = p.lnodes[j];
     double z = (nn.y == i) ? p.off2[j] : p.off1[j];
-    double q = fabs(p.lNewFlow[j] / barrels);
-    double yNorm = linkYnorm(x, q, p.qMax[j], p.beta[j], ct);
-    double yCrit = getYcrit(x, q, ct);
     int ot = (int)((nf >> NF_OTYPE_SHIFT) & 0x7);
     double inv = p.invert[i];
     if (ot == O_FREE) return (z > 0.0) ? 0.0 : gmin(yNorm, yCrit);
@@ -821,16 +829,28 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
     // goes first because it is the long (iterative) part of the launch.  The
     // outfall is never "converged" (dynwave.c:281, 340): its link is never
     // bypassed and the depth is refreshed every iteration, as in the reference.
-    if (blockIdx.x * kBlock < p.nOutLinks) {
+    // 64 outfall conduits per block and round: wave 0 finds their normal
+    // depths while wave 1 finds their critical depths, then wave 0 combines.
+    if (blockIdx.x * 64 < p.nOutLinks) {
         __shared__ double ct[5 * SWX_CIRC_N];
+        __shared__ double yc[64];
         stageTables(ct, p.gTables);
-        for (int c = blockIdx.x * kBlock + threadIdx.x; c < p.nOutLinks; c += gridDim.x * kBlock) {
-            int j = p.outLinks[c];
-            uint32_t f = p.lflags[j];
-            int2 nn = p.lnodes[j];
-            int o = (f & LF_N2_OUTFALL) ? nn.y : nn.x;    // link.c:743-753 (node2 first)
-            if (kFirst) p.nOldDepth[o] = p.nNewDepth[o];   // node_setOldHydState before the update
-            p.nNewDepth[o] = outfallDepth(p, o, p.nflags[o], j, f, ct);
+        const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        for (int base = blockIdx.x * 64; base < p.nOutLinks; base += gridDim.x * 64) {
+            int c = base + lane;
+            int j = (c < p.nOutLinks) ? p.outLinks[c] : -1;
+            uint32_t f = (j >= 0) ? p.lflags[j] : 0u;
+            double yn = 0.0;
+            if (j >= 0 && w == 0) yn = outfallPart<0>(p, j, f, ct);
+            if (j >= 0 && w == 1) yc[lane] = outfallPart<1>(p, j, f, ct);
+            __syncthreads();
+            if (j >= 0 && w == 0) {
+                int2 nn = p.lnodes[j];
+                int o = (f & LF_N2_OUTFALL) ? nn.y : nn.x;    // link.c:743-753 (node2 first)
+                if (kFirst) p.nOldDepth[o] = p.nNewDepth[o];   // node_setOldHydState before the update
+                p.nNewDepth[o] = outfallCombine(p, o, p.nflags[o], j, yn, yc[lane]);
+            }
+            __syncthreads();
         }
     }
     const double dt = p.ctl->dt;
