@@ -117,6 +117,14 @@ static double lsd_flowTurns(int j) { return (double)LinkStats[j].flowTurns; }
 static double lsd_flowTurnSign(int j) { return (double)LinkStats[j].flowTurnSign; }
 static int StatClass = 0;
 static double lsd_timeInFlowClass(int j) { return LinkStats[j].timeInFlowClass[StatClass]; }
+extern TStorageStats* StorageStats;
+#define SSD(nm, field) static double nm(int j) { return (Node[j].type == STORAGE && StorageStats) ? StorageStats[Node[j].subIndex].field : 0.0; }
+SSD(ssd_initVol, initVol)
+SSD(ssd_avgVol, avgVol)
+SSD(ssd_maxVol, maxVol)
+SSD(ssd_maxFlow, maxFlow)
+SSD(ssd_evapLosses, evapLosses)
+SSD(ssd_maxVolDate, maxVolDate)
 static double osd_avgFlow(int j) { return Node[j].type == OUTFALL ? OutfallStats[Node[j].subIndex].avgFlow : 0.0; }
 static double osd_maxFlow(int j) { return Node[j].type == OUTFALL ? OutfallStats[Node[j].subIndex].maxFlow : 0.0; }
 static double osd_totalPeriods(int j) { return Node[j].type == OUTFALL ? OutfallStats[Node[j].subIndex].totalPeriods : 0.0; }
@@ -151,6 +159,12 @@ static void writeStats(void)
     ONE_N("st.node.maxOverflowDate", nsd_maxOverflowDate);
     ONE_N("st.node.maxPondedVol", nsd_maxPondedVol);
     ONE_N("st.node.nonConvergedCount", nsd_nonConvergedCount);
+    ONE_N("st.storage.initVol", ssd_initVol);
+    ONE_N("st.storage.avgVol", ssd_avgVol);
+    ONE_N("st.storage.maxVol", ssd_maxVol);
+    ONE_N("st.storage.maxFlow", ssd_maxFlow);
+    ONE_N("st.storage.evapLosses", ssd_evapLosses);
+    ONE_N("st.storage.maxVolDate", ssd_maxVolDate);
     ONE_N("st.outfall.avgFlow", osd_avgFlow);
     ONE_N("st.outfall.maxFlow", osd_maxFlow);
     ONE_N("st.outfall.totalPeriods", osd_totalPeriods);

@@ -148,6 +148,10 @@ int DLLEXPORT swmm_start(int saveFlag)
     for (int j = 0; j < prj.net.nNodes(); j++) s += prj.st.newVolume[j];
     for (int j = 0; j < prj.net.nLinks(); j++) s += prj.st.lNewVolume[j];
     G->initStorage = s;
+    // StorageStats.initVol (stats.c:224)
+    prj.stats.stInitVol.assign(prj.net.nNodes(), 0.0);
+    for (int j = 0; j < prj.net.nNodes(); j++)
+        if (prj.net.nodeType[j] == STORAGE) prj.stats.stInitVol[j] = prj.st.newVolume[j];
     G->router.reset(new Router());
     int dev = (gDevice >= 0) ? gDevice : defaultDevice();
     if (gPart.active() && !prj.hotstartSave.empty())
@@ -739,6 +743,9 @@ long DLLEXPORT swmmx_getArray(const char* name, double* dst, long n)
         ARR("stat.node.maxOverflowDate", R.maxOverflowDate) ARR("stat.node.maxPondedVol", R.maxPondedVol)
         ARR("stat.node.nonConvergedCount", R.nonConvergedCount)
         ARR("stat.node.inflowVolume", R.nodeInflowVol) ARR("stat.node.outflowVolume", R.nodeOutflowVol)
+        ARR("stat.storage.initVol", R.stInitVol) ARR("stat.storage.avgVol", R.stAvgVol)
+        ARR("stat.storage.maxVol", R.stMaxVol) ARR("stat.storage.maxFlow", R.stMaxFlow)
+        ARR("stat.storage.evapLosses", R.stEvapLoss) ARR("stat.storage.maxVolDate", R.stMaxVolDate)
         ARR("stat.outfall.avgFlow", R.outfallAvgFlow) ARR("stat.outfall.maxFlow", R.outfallMaxFlow)
         ARR("stat.outfall.totalPeriods", R.outfallPeriods) ARR("stat.outfall.totalLoad", R.outfallLoad)
         ARR("stat.link.maxFlow", R.lMaxFlow) ARR("stat.link.maxFlowDate", R.lMaxFlowDate)

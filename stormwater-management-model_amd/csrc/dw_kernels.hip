@@ -36,6 +36,7 @@
 
 #include "router.h"
 #include "xsect.h"
+#include "storage.h"
 
 namespace swx {
 
@@ -136,6 +137,8 @@ struct StatsDev {
     double *lTimeFullUp, *lTimeFullDn, *lTimeFullFlow, *lTimeCapLim, *lTimeClass, *lTimeCourant;
     int *lTurns, *lTurnSign;
     const double* qFull;
+    // storage units (TStorageStats, stats.c:212-228), per node
+    double *sAvgVol, *sMaxVol, *sMaxVolDate, *sMaxFlow, *sEvap;
 };
 
 struct Params {
@@ -175,6 +178,14 @@ struct Params {
     // flooded, no volume) has an unchanged unrelaxed depth yRaw = yOld + dV /
     // surfArea, so its next update is just the relaxation 0.5 yLast + 0.5 yRaw
     double *yRaw, *yMaxNP;        // yMaxNP = fullDepth + surDepth (non-ponding yMax)
+    // storage units (node.c:170-179), per node (stShape -1: not a storage unit)
+    const int* stShape;
+    const double *stA0, *stA1, *stA2, *stFEvap;
+    const int *stCOff, *stCN;     // area curve slice of curveX / curveY
+    const double *curveX, *curveY;
+    double ucfL, ucfV;            // UCF(LENGTH), UCF(VOLUME)
+    double* nLosses;              // per node: this step's loss rate (storage evaporation)
+    double* nEvapVol;             // per node: this step's evaporated volume
     int* ulist;                   // [2][nN] unconverged nodes of the last two iterations
     const double* latIn;          // lateral inflow for this step
     // quality [p][object]
@@ -743,6 +754,39 @@ __global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
     }
 }
 
+// storage unit i's area relation (node_getVolume / node_getSurfArea for
+// STORAGE); out of line: only storage nodes call them
+__device__ __forceinline__ StorageGeom devStorageGeom(const Params& p, int i)
+{
+    StorageGeom g;
+    g.shape = p.stShape[i];
+    g.a0 = p.stA0[i];
+    g.a1 = p.stA1[i];
+    g.a2 = p.stA2[i];
+    int off = p.stCOff[i];
+    g.cx = p.curveX + off;
+    g.cy = p.curveY + off;
+    g.cn = p.stCN[i];
+    g.fullDepth = p.fullDepth[i];
+    g.fullVolume = p.fullVolume[i];
+    g.ucfL = p.ucfL;
+    g.ucfV = p.ucfV;
+    return g;
+}
+__device__ __attribute__((noinline)) double devStorageVolume(const Params& p, int i, double d)
+{
+    return storageVolume(devStorageGeom(p, i), d);
+}
+__device__ __attribute__((noinline)) double devStorageArea(const Params& p, int i, double d)
+{
+    return storageSurfArea(devStorageGeom(p, i), d);
+}
+__device__ __attribute__((noinline)) double devStorageLosses(const Params& p, int i, double depth,
+                                                            double volume, double dt, double* evapVol)
+{
+    return storageLosses(devStorageGeom(p, i), p.stFEvap[i], p.evapRate, depth, volume, dt, evapVol);
+}
+
 // setNodeDepth (dynwave.c:636-762) for node i given its summed inflow,
 // outflow, surface area and dq/dh; returns 1 when converged (dynwave.c:615-621)
 __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_t nf, double dt,
@@ -758,9 +802,11 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
     double surfArea = gmax(surf, p.minSurfArea);
     double dQ = inflow - outflow;
     double dV = 0.5 * (p.oldNetInflow[i] + dQ) * dt;
+    const bool isStorage = (int)(nf & NF_TYPE) == STORAGE;
     bool isSurcharged = false;
     if (p.surchargeMethod == SUR_EXTRAN) {
         if (isPonded) isSurcharged = false;
+        else if (isStorage) isSurcharged = (p.surDepth[i] > 0.0 && yLast > fullDepth);
         else isSurcharged = (yCrown > 0.0 && yLast > yCrown);
     }
     double yNew, dy;
@@ -791,7 +837,7 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
     double fullVolume = p.fullVolume[i];
     const bool flooded = yNew > yMax;
     if (k >= 1) {                                      // fast-path cache for the next iteration
-        bool plain = !isSurcharged && !canPond && !flooded && fullVolume == 0.0;
+        bool plain = !isSurcharged && !canPond && !flooded && fullVolume == 0.0 && !isStorage;
         if (plain) p.yRaw[i] = yRaw;
         p.dirty[i] = plain ? 2 : 0;
     }
@@ -808,6 +854,8 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
         }
         if (overflow < 0.0001) overflow = 0.0;
         p.nNewVolume[i] = newVolume;
+    } else if (isStorage) {
+        p.nNewVolume[i] = devStorageVolume(p, i, yNew);
     } else {
         p.nNewVolume[i] = (fullDepth > 0.0) ? fullVolume * (yNew / fullDepth) : 0.0;
     }
@@ -899,12 +947,18 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
             p.oldLat[i] = p.newLat[i];
             lat = p.latIn[i];
             p.newLat[i] = lat;
+            if (type == STORAGE) {       // addSystemInflows: node_getLosses (routing.c:363-365)
+                double ev = 0.0;
+                p.nLosses[i] = devStorageLosses(p, i, yOld, p.nOldVolume[i], p.ctl->dt, &ev);
+                p.nEvapVol[i] = ev;
+            }
         } else {
             yOld = p.nOldDepth[i];
             lat = p.newLat[i];
         }
         double inflow, outflow, surf, sumdqdh;
-        const bool reuse = !kFirst && k >= 2 && !(nf & (NF_CANPOND | NF_SHARED)) && !(p.dirty[i] & 1);
+        const bool reuse = !kFirst && k >= 2 && !(nf & (NF_CANPOND | NF_SHARED)) && type != STORAGE &&
+                           !(p.dirty[i] & 1);
         if (reuse) {
             inflow = p.inflow[i];
             outflow = p.outflow[i];
@@ -918,6 +972,10 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
             if (canPond && yLast > fullDepth && !(nf & NF_REPLICA)) surf = p.pondedArea[i];  // owner adds it
             inflow = 0.0;
             outflow = 0.0;                        // node losses are 0 for non-storage nodes
+            if (type == STORAGE && !(nf & NF_REPLICA)) {
+                surf = devStorageArea(p, i, yLast);
+                outflow = p.nLosses[i];
+            }
             if (lat >= 0.0) inflow += lat;
             else outflow -= lat;
             sumdqdh = 0.0;
@@ -1293,6 +1351,7 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
             S.mbPendOut[i] = o1;
             S.mbPendOut[p.nN + i] = o2;
         }
+        if (type == STORAGE) acc[3] += p.nEvapVol[i] / dt;   // removeStorageLosses (routing.c:812-838)
         if (!converged && !p.conv[i]) S.nonConv[i] += 1;  // stats_updateConvergenceStats
         if (!stats) continue;
         // stats_updateNodeStats (stats.c:543-643)
@@ -1304,7 +1363,15 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
                 S.volFlooded[i] += overflow * dt;
                 if (nf & NF_CANPOND) S.maxPonded[i] = gmax(S.maxPonded[i], (newVolume - fullVolume));
             }
-            if (newDepth + p.invert[i] + 0.0001 >= p.crownElev[i]) S.timeSurch[i] += dt;
+            if ((type != STORAGE || p.surDepth[i] > 0.0) && newDepth + p.invert[i] + 0.0001 >= p.crownElev[i])
+                S.timeSurch[i] += dt;
+            if (type == STORAGE) {                         // stats.c:590-603
+                S.sAvgVol[i] += newVolume;
+                S.sEvap[i] += p.nEvapVol[i];
+                double v = gmin(newVolume, fullVolume);
+                if (v > S.sMaxVol[i]) { S.sMaxVol[i] = v; S.sMaxVolDate[i] = aDate; }
+                S.sMaxFlow[i] = gmax(S.sMaxFlow[i], outflow);
+            }
         } else {
             if (inflow >= 0.001) {
                 S.oAvgFlow[i] += inflow;
@@ -1953,6 +2020,43 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     UPD(tmp, gn(net.crownElev), nN); p.crownElev = tmp;
     UPD(tmp, gn(net.fullVolume), nN); p.fullVolume = tmp;
     UPD(tmp, gn(net.fixedStage), nN); p.fixedStage = tmp;
+    // ---- storage units -------------------------------------------------------
+    {
+        std::vector<int> shape(nN, -1), coff(nN, 0), cn(nN, 0);
+        std::vector<double> cx, cy;
+        std::vector<int> curveOff(net.curves.size(), -1);
+        for (int i = 0; i < nN; i++) {
+            const int g = LN[i];
+            if (net.nodeType[g] != STORAGE) continue;
+            shape[i] = net.stShape[g];
+            int c = net.stCurve[g];
+            if (c >= 0) {
+                if (curveOff[c] < 0) {
+                    curveOff[c] = (int)cx.size();
+                    cx.insert(cx.end(), net.curves[c].x.begin(), net.curves[c].x.end());
+                    cy.insert(cy.end(), net.curves[c].y.begin(), net.curves[c].y.end());
+                }
+                coff[i] = curveOff[c];
+                cn[i] = (int)net.curves[c].x.size();
+            }
+        }
+        if (cx.empty()) { cx.push_back(0.0); cy.push_back(0.0); }
+        int* ip;
+        UPI(ip, shape, nN); p.stShape = ip;
+        UPI(ip, coff, nN); p.stCOff = ip;
+        UPI(ip, cn, nN); p.stCN = ip;
+        UPD(tmp, gn(net.stA0), nN); p.stA0 = tmp;
+        UPD(tmp, gn(net.stA1), nN); p.stA1 = tmp;
+        UPD(tmp, gn(net.stA2), nN); p.stA2 = tmp;
+        UPD(tmp, gn(net.stFEvap), nN); p.stFEvap = tmp;
+        UPD(tmp, cx, cx.size()); p.curveX = tmp;
+        UPD(tmp, cy, cy.size()); p.curveY = tmp;
+        p.ucfL = prj.ucfLength();
+        p.ucfV = prj.ucfVolume();
+        std::vector<double> z(nN, 0.0);
+        UPD(p.nLosses, z, nN);
+        UPD(p.nEvapVol, z, nN);
+    }
     // ---- node dynamic -----------------------------------------------------
     UPD(p.nNewDepth, gn(st.newDepth), nN);
     UPD(p.nOldDepth, gn(st.oldDepth), nN);
@@ -2067,6 +2171,8 @@ int Router::init(Project& prj, int device, const Partition* partIn)
             UPD(*a, l0, nL);
         std::vector<double> cls((size_t)7 * nL, 0.0);
         UPD(S.lTimeClass, cls, cls.size());
+        for (double** a : {&S.sAvgVol, &S.sMaxVol, &S.sMaxFlow, &S.sEvap}) UPD(*a, z0, nN);
+        UPD(S.sMaxVolDate, dStart, nN);
         std::vector<double> ol((size_t)std::max(P, 1) * nN, 0.0);
         UPD(S.oLoad, ol, ol.size());
         UPD(tmp, gl(net.qFull), nL); S.qFull = tmp;
@@ -2534,6 +2640,11 @@ int Router::downloadStats(Project& prj)
     HIPCHECK(node(R.outfallAvgFlow, S.oAvgFlow));
     HIPCHECK(node(R.outfallMaxFlow, S.oMaxFlow));
     HIPCHECK(nodeI(R.outfallPeriods, S.oPeriods));
+    HIPCHECK(node(R.stAvgVol, S.sAvgVol));
+    HIPCHECK(node(R.stMaxVol, S.sMaxVol));
+    HIPCHECK(node(R.stMaxVolDate, S.sMaxVolDate));
+    HIPCHECK(node(R.stMaxFlow, S.sMaxFlow));
+    HIPCHECK(node(R.stEvapLoss, S.sEvap));
     {
         size_t P = p.P;
         R.outfallLoad.assign(P * gN, 0.0);

@@ -132,6 +132,15 @@ struct Xsect {
 };
 
 // ---- the network --------------------------------------------------------
+// [CURVES] table (table.c:67-109); type in CurveTypeWords order
+enum CurveType { CV_STORAGE = 0, CV_DIVERSION, CV_TIDAL, CV_RATING, CV_CONTROLS, CV_SHAPE, CV_WEIR,
+                 CV_PUMP1, CV_PUMP2, CV_PUMP3, CV_PUMP4, CV_PUMP5 };
+struct Curve {
+    std::string id;
+    int type = -1;
+    std::vector<double> x, y;
+};
+
 struct Network {
     // nodes
     std::vector<std::string> nodeId;
@@ -141,6 +150,12 @@ struct Network {
     // outfall parameters (indexed by node; unused for other types)
     std::vector<int> outfallType, outfallFlap, outfallSeries;
     std::vector<double> fixedStage;
+    // storage unit parameters (indexed by node; node.c:170-179): surface area
+    // relation (StorageShape), its coefficients in user units, area curve,
+    // evaporation factor
+    std::vector<int> stShape, stCurve;
+    std::vector<double> stA0, stA1, stA2, stFEvap;
+    int nStorage = 0;
     // links
     std::vector<std::string> linkId;
     std::vector<int> linkType, node1, node2, hasFlapGate, direction, barrels, hasLosses,
@@ -154,8 +169,9 @@ struct Network {
     std::vector<Pollutant> pollut;
     std::vector<Pattern> patterns;
     std::vector<Tseries> tseries;
+    std::vector<Curve> curves;
     std::unordered_map<std::string, int> nodeIndex, linkIndex, pollutIndex, patternIndex,
-        tseriesIndex;
+        tseriesIndex, curveIndex;
     std::string title;
 
     int nNodes() const { return (int)nodeId.size(); }
@@ -191,6 +207,8 @@ struct RunStats {
         timeSurcharged, timeCourantCritical, totLatFlow, maxLatFlow, maxInflow, maxInflowDate,
         maxOverflow, maxOverflowDate, maxPondedVol, nonConvergedCount;
     std::vector<double> nodeInflowVol, nodeOutflowVol;           // NodeInflow / NodeOutflow
+    // storage units (TStorageStats), node indexed; initVol = volume at stats_open
+    std::vector<double> stInitVol, stAvgVol, stMaxVol, stMaxVolDate, stMaxFlow, stEvapLoss;
     std::vector<double> outfallAvgFlow, outfallMaxFlow, outfallPeriods, outfallLoad;   // load [p][node]
     std::vector<double> lMaxFlow, lMaxFlowDate, lMaxVeloc, lMaxDepth, lTimeNormalFlow,
         lTimeSurcharged, lTimeFullUpstream, lTimeFullDnstream, lTimeFullFlow, lTimeCapacityLimited,

@@ -15,6 +15,7 @@
 // [REPORT]; map/graphics sections are skipped.  Anything else fails loudly
 // with ERR_INPUT naming the section (never silently ignored).
 #include "project.h"
+#include "storage.h"
 
 #include <cmath>
 #include <cstdlib>
@@ -207,11 +208,18 @@ static bool getDouble(const char* s, double* y)
 
 enum Sect {
     S_NONE = -1, S_TITLE, S_OPTION, S_EVAP, S_JUNC, S_OUTFALL, S_CONDUIT, S_XSECT, S_LOSS,
-    S_POLLUT, S_INFLOW, S_DWF, S_PATTERN, S_TSERIES, S_REPORT, S_FILES, S_SKIP, S_UNSUPPORTED
+    S_POLLUT, S_INFLOW, S_DWF, S_PATTERN, S_TSERIES, S_REPORT, S_FILES, S_STORAGE, S_CURVES,
+    S_SKIP, S_UNSUPPORTED
 };
 static const char* const kSectWords[] = {
     "[TITLE", "[OPTION", "[EVAP", "[JUNC", "[OUTFALL", "[CONDUIT", "[XSECT", "[LOSS",
-    "[POLLUT", "[INFLOW", "[DWF", "[PATTERN", "[TIMESERIES", "[REPORT", "[FILES", nullptr};
+    "[POLLUT", "[INFLOW", "[DWF", "[PATTERN", "[TIMESERIES", "[REPORT", "[FILES", "[STORAGE",
+    "[CURVE", nullptr};
+static const char* const kRelationWords[] = {"TABULAR", "FUNCTIONAL", "CYLINDRICAL", "CONICAL",
+                                             "PARABOLIC", "PYRAMIDAL", nullptr};
+static const char* const kCurveTypeWords[] = {"STORAGE", "DIVERSION", "TIDAL", "RATING", "CONTROL",
+                                              "SHAPE", "WEIR", "PUMP1", "PUMP2", "PUMP3", "PUMP4",
+                                              "PUMP5", nullptr};
 static const char* const kSkipWords[] = {
     "[MAP", "[COORDINATE", "[VERTICES", "[POLYGON", "[SYMBOL", "[LABEL", "[BACKDROP", "[TAG",
     "[PROFILE", nullptr};
@@ -369,6 +377,8 @@ int Project::readFile(const char* path)
             net.fullDepth.assign(nn, 0); net.surDepth.assign(nn, 0); net.pondedArea.assign(nn, 0);
             net.crownElev.assign(nn, 0); net.fullVolume.assign(nn, 0); net.outfallType.assign(nn, -1);
             net.outfallFlap.assign(nn, 0); net.outfallSeries.assign(nn, -1); net.fixedStage.assign(nn, 0);
+            net.stShape.assign(nn, -1); net.stCurve.assign(nn, -1); net.stA0.assign(nn, 0);
+            net.stA1.assign(nn, 0); net.stA2.assign(nn, 0); net.stFEvap.assign(nn, 0);
             net.linkType.assign(nl, CONDUIT); net.node1.assign(nl, 0); net.node2.assign(nl, 0);
             net.hasFlapGate.assign(nl, 0); net.direction.assign(nl, 1); net.barrels.assign(nl, 1);
             net.hasLosses.assign(nl, 0); net.superCritical.assign(nl, 0); net.linkRpt.assign(nl, 0);
@@ -406,7 +416,16 @@ int Project::parseLine(int sect, std::vector<char*>& tok, int pass)
             return readOption(tok[0], tok[1]);
         case S_JUNC:
         case S_OUTFALL:
+        case S_STORAGE:
             if (addId(net.nodeIndex, net.nodeId, tok[0]) < 0) return setError(207, std::string("ERROR 207: duplicate ID name ") + tok[0]);
+            return 0;
+        case S_CURVES:
+            if (!net.curveIndex.count(tok[0])) {
+                net.curveIndex.emplace(tok[0], (int)net.curves.size());
+                Curve c;
+                c.id = tok[0];
+                net.curves.push_back(c);
+            }
             return 0;
         case S_CONDUIT:
             if (addId(net.linkIndex, net.linkId, tok[0]) < 0) return setError(207, std::string("ERROR 207: duplicate ID name ") + tok[0]);
@@ -456,6 +475,8 @@ int Project::parseLine(int sect, std::vector<char*>& tok, int pass)
     case S_TSERIES: return readTimeseries(tok);
     case S_REPORT: return readReport(tok);
     case S_FILES: return readFiles(tok);
+    case S_STORAGE: return readStorage(tok);
+    case S_CURVES: return readCurve(tok);
     default: return 0;
     }
 }
@@ -641,6 +662,120 @@ int Project::readJunction(std::vector<char*>& tok)  // node.c:606-648, 125-196
     net.initDepth[j] = x[2] / u;
     net.surDepth[j] = x[3] / u;
     net.pondedArea[j] = x[4] / (u * u);
+    return 0;
+}
+
+// storage_readParams (node.c:654-809):
+//   id elev maxDepth initDepth shape a1 a2 a0 | TABULAR curve  [surDepth [fEvap [seepage]]]
+int Project::readStorage(std::vector<char*>& tok)
+{
+    int nt = (int)tok.size();
+    if (nt < 6) return 203;
+    int j = net.nodeIndex.at(tok[0]);
+    double x[3];
+    for (int i = 1; i <= 3; i++)
+        if (!getDouble(tok[i], &x[i - 1])) return 211;
+    int m = kfind(tok[4], kRelationWords);
+    if (m < 0) return 205;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, y[3] = {0, 0, 0};
+    int curve = -1, n;
+    if (m == ST_TABULAR) {
+        auto it = net.curveIndex.find(tok[5]);
+        if (it == net.curveIndex.end()) return 209;
+        curve = it->second;
+        n = 6;
+    } else {
+        if (nt < 8) return 203;
+        for (int i = 5; i <= 7; i++)
+            if (!getDouble(tok[i], &y[i - 5])) return 211;
+        n = 8;
+    }
+    switch (m) {
+    case ST_FUNCTIONAL:
+        if (y[2] < 0.0) return 211;
+        break;
+    case ST_CYLINDRICAL: case ST_CONICAL: case ST_PARABOLOID: case ST_PYRAMIDAL:
+        if (y[0] <= 0.0 || y[1] <= 0.0 || y[2] < 0.0) return 211;
+        break;
+    }
+    if (m == ST_PARABOLOID && y[2] == 0.0) return 211;
+    const double PI = 3.141592654;
+    double A, B, Z, L, W;
+    switch (m) {
+    case ST_FUNCTIONAL: a1 = y[0]; a2 = y[1]; a0 = y[2]; break;
+    case ST_CYLINDRICAL:
+        A = y[0] / 2.; B = y[1] / 2.;
+        a1 = 0.0; a2 = 0.0; a0 = PI * A * B;
+        break;
+    case ST_CONICAL:
+        A = y[0] / 2.; B = y[1] / 2.; Z = y[2];
+        a1 = 2.0 * PI * B * Z; a2 = PI * B / A * Z * Z; a0 = PI * A * B;
+        break;
+    case ST_PARABOLOID:
+        A = y[0] / 2.; B = y[1] / 2.; Z = y[2];
+        a1 = PI * A * B / Z; a2 = 0.0; a0 = 0.0;
+        break;
+    case ST_PYRAMIDAL:
+        L = y[0]; W = y[1]; Z = y[2];
+        a1 = 2.0 * (L + W) * Z; a2 = 4.0 * Z * Z; a0 = L * W;
+        break;
+    }
+    double surDepth = 0.0, fEvap = 0.0;
+    if (nt > n) { if (!getDouble(tok[n], &surDepth)) return 211; n++; }
+    if (nt > n) { if (!getDouble(tok[n], &fEvap)) return 211; n++; }
+    if (nt > n) {                       // exfil_readStorageParams (exfil.c:34-70)
+        double ks = 0.0;
+        if (nt == n + 1) { if (!getDouble(tok[n], &ks)) return 211; }
+        else if (nt < n + 3) return 203;
+        else {
+            double t;
+            for (int i = 0; i < 3; i++) if (!getDouble(tok[n + i], &t)) return 211;
+            getDouble(tok[n + 1], &ks);
+        }
+        if (ks != 0.0)
+            return setError(200, "ERROR 200: storage seepage (exfiltration) is not supported by the MI355X engine");
+    }
+    double u = ucfLength();
+    net.nodeType[j] = STORAGE;
+    net.invertElev[j] = x[0] / u;
+    net.crownElev[j] = net.invertElev[j];
+    net.fullDepth[j] = x[1] / u;
+    net.initDepth[j] = x[2] / u;
+    net.surDepth[j] = surDepth / u;
+    net.pondedArea[j] = 0.0;
+    net.stShape[j] = m;
+    net.stCurve[j] = curve;
+    net.stA0[j] = a0;
+    net.stA1[j] = a1;
+    net.stA2[j] = a2;
+    net.stFEvap[j] = fEvap;
+    net.nStorage++;
+    return 0;
+}
+
+// table_readCurve (table.c:67-109): first line carries the curve type
+int Project::readCurve(std::vector<char*>& tok)
+{
+    int nt = (int)tok.size();
+    if (nt < 2) return 203;
+    auto it = net.curveIndex.find(tok[0]);
+    if (it == net.curveIndex.end()) return 209;
+    Curve& c = net.curves[it->second];
+    int k1 = 1;
+    if (c.type < 0) {
+        int m = kfind(tok[1], kCurveTypeWords);
+        if (m < 0) return 205;
+        c.type = m;
+        if (nt == 2) return 0;
+        k1 = 2;
+    }
+    for (int k = k1; k < nt; k += 2) {
+        if (k + 1 >= nt) return 203;
+        double x, y;
+        if (!getDouble(tok[k], &x) || !getDouble(tok[k + 1], &y)) return 211;
+        c.x.push_back(x);
+        c.y.push_back(y);
+    }
     return 0;
 }
 
@@ -1302,16 +1437,28 @@ void Project::validate()  // project.c:186-270
         }
         validateConduit(j);
         if (errorCode) return;
-        int n = net.node1[j];                             // link.c:440-463
-        net.fullDepth[n] = gmax(net.fullDepth[n], net.offset1[j] + net.xsect[j].yFull);
+        // link.c:440-463: storage units without surcharge keep their depth
+        int n = net.node1[j];
+        if (net.nodeType[n] != STORAGE || net.surDepth[n] > 0.0)
+            net.fullDepth[n] = gmax(net.fullDepth[n], net.offset1[j] + net.xsect[j].yFull);
         n = net.node2[j];
-        net.fullDepth[n] = gmax(net.fullDepth[n], net.offset2[j] + net.xsect[j].yFull);
+        if (net.nodeType[n] != STORAGE || net.surDepth[n] > 0.0)
+            net.fullDepth[n] = gmax(net.fullDepth[n], net.offset2[j] + net.xsect[j].yFull);
     }
-    for (int j = 0; j < nn; j++)
+    for (int j = 0; j < nn; j++) {
         if (net.initDepth[j] > net.fullDepth[j] + net.surDepth[j]) {
             setError(138, "ERROR 138: initial depth greater than maximum depth for Node " + net.nodeId[j]);
             return;
         }
+        if (net.nodeType[j] == STORAGE) {                // node_validate (node.c:219-222)
+            StorageGeom g = storageGeom(j);
+            g.fullVolume = 0.0;
+            if (storageVolume(g, net.fullDepth[j]) < 0.0) {
+                setError(119, "ERROR 119: negative storage volume at full depth for Node " + net.nodeId[j]);
+                return;
+            }
+        }
+    }
     // DWF pattern ordering (inflow.c:331-354)
     for (auto& d : net.dwfInflows) {
         int tmp[4] = {-1, -1, -1, -1};
@@ -1464,14 +1611,21 @@ int Project::initState()
     z(s.nOldQual, nn * P); z(s.nNewQual, nn * P); z(s.lOldQual, nl * P); z(s.lNewQual, nl * P);
     s.variableStep = 0.0;
 
-    // node_initState (node.c:237-289): junction volume = 0 (fullVolume 0)
+    // node_initState (node.c:237-289): junction volume = 0 (fullVolume 0);
+    // storage units from their area relation
     for (int j = 0; j < nn; j++) {
         s.oldDepth[j] = net.initDepth[j];
         s.newDepth[j] = s.oldDepth[j];
         net.crownElev[j] = net.invertElev[j];
-        net.fullVolume[j] = 0.0;                    // node_getVolume(j, fullDepth) = 0
-        s.oldVolume[j] = 0.0;
-        s.newVolume[j] = 0.0;
+        if (net.nodeType[j] == STORAGE) {
+            net.fullVolume[j] = 0.0;
+            net.fullVolume[j] = storageVolume(storageGeom(j), net.fullDepth[j]);
+            s.oldVolume[j] = storageVolume(storageGeom(j), s.oldDepth[j]);
+        } else {
+            net.fullVolume[j] = 0.0;                // node_getVolume(j, fullDepth) = 0
+            s.oldVolume[j] = 0.0;
+        }
+        s.newVolume[j] = s.oldVolume[j];
     }
     // link_initState (link.c:508-539) + conduit_initState (1304-1316)
     for (int j = 0; j < nl; j++) {
@@ -1540,6 +1694,24 @@ int Project::initState()
         }
     }
     return 0;
+}
+
+StorageGeom Project::storageGeom(int j) const
+{
+    StorageGeom g;
+    g.shape = net.stShape[j];
+    g.a0 = net.stA0[j];
+    g.a1 = net.stA1[j];
+    g.a2 = net.stA2[j];
+    int c = net.stCurve[j];
+    g.cx = (c >= 0 && !net.curves[c].x.empty()) ? net.curves[c].x.data() : nullptr;
+    g.cy = (c >= 0 && !net.curves[c].y.empty()) ? net.curves[c].y.data() : nullptr;
+    g.cn = (c >= 0) ? (int)net.curves[c].x.size() : 0;
+    g.fullDepth = net.fullDepth[j];
+    g.fullVolume = net.fullVolume[j];
+    g.ucfL = ucfLength();
+    g.ucfV = ucfVolume();
+    return g;
 }
 
 // ================================================================= inflows

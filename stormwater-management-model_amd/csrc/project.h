@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "model.h"
+#include "storage.h"
 
 namespace swx {
 
@@ -61,6 +62,7 @@ public:
                      double* dwfTotal, double* extTotal, double* extOutTotal);
     bool inflowsAreConstant() const;        // no time series / patterns
     double getDateTime(double elapsedMsec) const;  // swmm5.c:1543
+    StorageGeom storageGeom(int node) const;        // storage unit j's area relation
 
     int setError(int code, const std::string& msg);
 
@@ -75,6 +77,8 @@ private:
     int readXsect(std::vector<char*>& tok);
     int readLoss(std::vector<char*>& tok);
     int readFiles(std::vector<char*>& tok);
+    int readStorage(std::vector<char*>& tok);
+    int readCurve(std::vector<char*>& tok);
     int readHotstart();
     void initDepths();
     int readPollutant(std::vector<char*>& tok);

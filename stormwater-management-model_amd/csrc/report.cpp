@@ -308,6 +308,40 @@ void writeRunReport(FILE* f, Project& prj, const ReportTotals& tot, long long no
         w.blank();
     }
 
+    // Storage Volume Summary (writeStorageVolumes, statsrpt.c:511-574)
+    if (net.nStorage > 0) {
+        w.title("Storage Volume Summary");
+        w.blank();
+        w.printf("\n  ------------------------------------------------------------------------------------------------"
+                 "\n                         Average    Avg   Evap  Exfil     Maximum    Max    Time of Max    Maximum"
+                 "\n                          Volume   Pcnt   Pcnt   Pcnt      Volume   Pcnt     Occurrence    Outflow");
+        if (o.unitSystem == 0)
+            w.printf("\n  Storage Unit          1000 ft\xB3   Full   Loss   Loss    1000 ft\xB3   Full    days hr:min        ");
+        else
+            w.printf("\n  Storage Unit           1000 m\xB3   Full   Loss   Loss     1000 m\xB3   Full    days hr:min        ");
+        w.printf("%3s", kFlowWords[o.flowUnits]);
+        w.printf("\n  ------------------------------------------------------------------------------------------------");
+        const double ucfV = prj.ucfVolume();
+        for (int j = 0; j < nN; j++) {
+            if (net.nodeType[j] != STORAGE) continue;
+            w.printf("\n  %-20s", net.nodeId[j].c_str());
+            double avgVol = R.stAvgVol[j] / steps, maxVol = R.stMaxVol[j];
+            double pctMax = 0.0, pctAvg = 0.0;
+            if (net.fullVolume[j] > 0.0) {
+                pctAvg = avgVol / net.fullVolume[j] * 100.0;
+                pctMax = maxVol / net.fullVolume[j] * 100.0;
+            }
+            double pctEvap = 0.0, pctSeep = 0.0;
+            if (R.nodeInflowVol[j] > 0.0) pctEvap = R.stEvapLoss[j] / R.nodeInflowVol[j] * 100.0;
+            w.printf("%10.3f  %5.1f  %5.1f  %5.1f  %10.3f  %5.1f", avgVol * ucfV / 1000.0, pctAvg, pctEvap, pctSeep,
+                     maxVol * ucfV / 1000.0, pctMax);
+            elapsed(R.stMaxVolDate[j], rptStart, &d, &h, &m);
+            w.printf("    %4d  %02d:%02d  ", d, h, m);
+            w.printf(flowFmt, R.stMaxFlow[j] * ucfQ);
+        }
+        w.blank();
+    }
+
     // Outfall Loading Summary
     int nOut = 0;
     for (int j = 0; j < nN; j++) nOut += net.nodeType[j] == OUTFALL;

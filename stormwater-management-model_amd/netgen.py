@@ -246,11 +246,37 @@ LINKS ALL
 """
 
 
+# storage units replacing six junctions of the Example network: every area
+# relation of node.c:654-809 (TABULAR, FUNCTIONAL, CYLINDRICAL, CONICAL,
+# PARABOLIC, PYRAMIDAL), one with surcharge depth, evaporation factors
+_STORAGE = {
+    "N3":  "N3  117.0  9   0    FUNCTIONAL  1000 0.5 200   0    0.5",
+    "N4":  "N4  115.4  9   0    TABULAR     SC1              1.0  0.8",
+    "N7":  "N7  114.0  10  0.5  CYLINDRICAL 40   30  0     0    1.0",
+    "N9":  "N9  111.0  10  0    CONICAL     30   20  2     0    1.0",
+    "N12": "N12 108.7  10  0    PYRAMIDAL   30   20  1.5",
+    "N13": "N13 109.9  6   0    PARABOLIC   30   20  6     0    0    0",
+}
+_STORAGE_EXTRA = """
+[CURVES]
+;;Name Type X Y
+SC1  Storage  0  500
+SC1           2  800
+SC1           5  1200
+SC1           9  1500
+
+[EVAPORATION]
+CONSTANT  5.0
+DRY_ONLY  NO
+"""
+
+
 def write_example(path: str, *, route_step: float = 5.0,
                   variable_step: float = 0.0, end_time: str = "04:00:00",
-                  pollutants: bool = False, files: str = "") -> None:
+                  pollutants: bool = False, files: str = "", storage: bool = False) -> None:
     """Write the authored Example network (see module docstring).  `files`
-    is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf")."""
+    is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf");
+    `storage` turns six junctions into storage units (_STORAGE)."""
     if pollutants:
         pollut = ("TSS MG/L 0 0 0 0.5 NO * 0 20 0\n"
                   "BOD MG/L 0 0 0 0 NO * 0 10 0\n")
@@ -262,6 +288,13 @@ def write_example(path: str, *, route_step: float = 5.0,
                           end_time=end_time, pollut=pollut,
                           qual_inflow=qual_inflow, qual_dwf=qual_dwf,
                           pollut_opt="")
+    if storage:
+        lines = [ln for ln in txt.split("\n") if ln.split()[:1] not in ([k] for k in _STORAGE)
+                 or not ln.split()[1:2] or not ln.split()[1].replace(".", "").isdigit()
+                 or len(ln.split()) != 6]
+        txt = "\n".join(lines)
+        txt += "\n[STORAGE]\n;;Name Elev MaxDepth InitDepth Shape Coefficients\n"
+        txt += "\n".join(_STORAGE.values()) + "\n" + _STORAGE_EXTRA
     if files:
         txt += "\n[FILES]\n" + files.rstrip("\n") + "\n"
     d = os.path.dirname(os.path.abspath(path))

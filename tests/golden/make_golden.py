@@ -52,6 +52,11 @@ CASES = {
     "example_hot": (netgen.write_example, dict(end_time="01:00:00", route_step=5.0,
                                                pollutants=True,
                                                files="USE HOTSTART example_hotsave.ref.hsf"), 1),
+    # storage units of every area relation, evaporation (node.c:654-1105)
+    "example_storage": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0,
+                                                   storage=True), 1),
+    "example_storage_var": (netgen.write_example, dict(end_time="02:00:00", route_step=10.0,
+                                                       variable_step=0.75, storage=True), 1),
     # swmm_setValue between steps: external inflow, outfall stage, routing step
     "example_api": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
                                                variable_step=0.75), 1),
@@ -85,7 +90,7 @@ def make(name):
         out = f.read()
     np.save(os.path.join(HERE, name + ".ref_out.npy"), np.frombuffer(out, dtype=np.uint8))
     # the reference's report file (summary tables after swmm_report)
-    with open(tmp + ".rpt") as f, open(os.path.join(HERE, name + ".ref_rpt.txt"), "w") as g:
+    with open(tmp + ".rpt", "rb") as f, open(os.path.join(HERE, name + ".ref_rpt.txt"), "wb") as g:
         g.write(f.read())
     saved = os.path.join(HERE, name + ".hsf")
     if os.path.exists(saved):

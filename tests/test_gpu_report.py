@@ -20,7 +20,8 @@ import swmm5
 SECTIONS = ["Highest Continuity Errors", "Time-Step Critical Elements",
             "Highest Flow Instability Indexes", "Most Frequent Nonconverging Nodes",
             "Routing Time Step Summary", "Node Depth Summary", "Node Inflow Summary",
-            "Node Surcharge Summary", "Node Flooding Summary", "Outfall Loading Summary",
+            "Node Surcharge Summary", "Node Flooding Summary", "Storage Volume Summary",
+            "Outfall Loading Summary",
             "Link Flow Summary", "Flow Classification Summary", "Conduit Surcharge Summary"]
 NUM = re.compile(r"^[-+]?(\d+\.?\d*|\.\d+)(e[-+]?\d+)?%?$", re.I)
 
@@ -91,8 +92,8 @@ def test_report_tables_match_reference(name, tmp_path):
     assert s.end() == 0
     s.report()
     s.close()
-    mine = _sections(open(rpt).read())
-    ref = _sections(open(os.path.join(_golden.GOLDEN, name + ".ref_rpt.txt")).read())
+    mine = _sections(open(rpt, encoding="latin-1").read())
+    ref = _sections(open(os.path.join(_golden.GOLDEN, name + ".ref_rpt.txt"), encoding="latin-1").read())
     checked = 0
     for title in ["Flow Routing Continuity"] + SECTIONS:
         if title not in ref:

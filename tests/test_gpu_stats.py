@@ -60,6 +60,12 @@ def test_stats_match_reference(name, tmp_path):
     for f in ("avgFlow", "maxFlow"):
         np.testing.assert_allclose(g("stat.outfall." + f), d["st.outfall." + f], rtol=RTOL, atol=ATOL,
                                    err_msg=f)
+    if "st.storage.avgVol" in d:                       # TStorageStats (stats.c:590-603)
+        for f in ("initVol", "avgVol", "maxVol", "maxFlow", "evapLosses"):
+            np.testing.assert_allclose(g("stat.storage." + f), d["st.storage." + f], rtol=RTOL, atol=ATOL,
+                                       err_msg=f)
+        st = d["st.storage.avgVol"] != 0
+        _dates_agree(g("stat.storage.maxVolDate")[st], d["st.storage.maxVolDate"][st])
     np.testing.assert_allclose(g("stat.outfall.totalPeriods"), d["st.outfall.totalPeriods"], atol=2)
     P = int(d["counts"][2])
     if P:

@@ -86,7 +86,7 @@ def _replay(name):
     return d
 
 
-@pytest.mark.parametrize("name", _golden.CASES)
+@pytest.mark.parametrize("name", [c for c in _golden.CASES if c not in _golden.BEYOND_ORACLE])
 def test_oracle_bit_identical_to_reference(name):
     _replay(name)
 
