@@ -186,6 +186,7 @@ struct Params {
     double ucfL, ucfV;            // UCF(LENGTH), UCF(VOLUME)
     double* nLosses;              // per node: this step's loss rate (storage evaporation)
     double* nEvapVol;             // per node: this step's evaporated volume
+    double* hrt;                  // per node: storage hydraulic residence time (sec)
     int* ulist;                   // [2][nN] unconverged nodes of the last two iterations
     const double* latIn;          // lateral inflow for this step
     // quality [p][object]
@@ -1111,6 +1112,16 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
         double qIn = p.inflow[i];
         double oldVol = p.nOldVolume[i];
         int e0 = p.rowptr[i], e1 = p.rowptr[i + 1];
+        const bool isStorage = (int)(p.nflags[i] & NF_TYPE) == STORAGE;
+        double fEvap = 1.0;
+        if (isStorage) {                     // findStorageQual (qualrout.c:417-436)
+            double h = p.hrt[i];             // updateHRT (qualrout.c:478-494)
+            if (oldVol < 1.E-10) h = 0.0;
+            else h = (h + dt) * oldVol / (oldVol + qIn * dt);
+            p.hrt[i] = gmax(h, 0.0);
+            double vEvap = p.nEvapVol[i];
+            if (vEvap > 0.0 && oldVol > 0.0353147) fEvap += vEvap / oldVol;
+        }
         for (int pp = 0; pp < p.P; pp++) {
             size_t ni = (size_t)pp * p.nN + i;
             double cOld = p.nNewQual[ni];           // node_setOldQualState
@@ -1125,8 +1136,8 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
                 if (down) w += fabs(ql) * p.lNewQual[(size_t)pp * p.nL + l];
             }
             double c;
-            if (oldVol > 0.0353147) {
-                double c1 = reactedQual(p.kDecay[pp], cOld, dt);
+            if (isStorage || oldVol > 0.0353147) {
+                double c1 = reactedQual(p.kDecay[pp], cOld * fEvap, dt);
                 c = mixedQual(c1, oldVol, w, qIn, dt);
                 if ((p.nNewVolume[i] <= 0.0353147 || p.nNewDepth[i] <= 0.003281) && qIn <= 1.E-10) c = 0.0;
             } else if (qIn > 1.E-10) {
@@ -2056,6 +2067,9 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         std::vector<double> z(nN, 0.0);
         UPD(p.nLosses, z, nN);
         UPD(p.nEvapVol, z, nN);
+        std::vector<double> h(nN, 0.0);
+        if (!st.hrt.empty()) h = gn(st.hrt);
+        UPD(p.hrt, h, nN);
     }
     // ---- node dynamic -----------------------------------------------------
     UPD(p.nNewDepth, gn(st.newDepth), nN);
@@ -2528,6 +2542,7 @@ int Router::download(Project& prj)
     HIPCHECK(dnN(st.oldFlowInflow, p.oldFlowInflow));
     HIPCHECK(dnN(st.oldSurfArea, p.oldSurfArea));
     HIPCHECK(dnN(st.dYdT, p.dYdT));
+    HIPCHECK(dnN(st.hrt, p.hrt));
     HIPCHECK(dnL(st.lNewFlow, p.lNewFlow));
     HIPCHECK(dnL(st.lOldFlow, p.lOldFlow));
     HIPCHECK(dnL(st.lNewDepth, p.lNewDepth));
@@ -2724,6 +2739,7 @@ int Router::upload(Project& prj)
     HIPCHECK(upN(p.inflow, st.inflow));
     HIPCHECK(upN(p.outflow, st.outflow));
     HIPCHECK(upN(p.newLat, st.newLatFlow));
+    if (st.hrt.size() == (size_t)prj.net.nNodes()) HIPCHECK(upN(p.hrt, st.hrt));
     HIPCHECK(upL(p.lNewFlow, st.lNewFlow));
     HIPCHECK(upL(p.lNewDepth, st.lNewDepth));
     HIPCHECK(upL(p.lNewVolume, st.lNewVolume));

@@ -191,6 +191,7 @@ struct State {
     std::vector<int> flowClass, fullState, normalFlow, capacityLimited;
     // Xnode (dynwave.c:72-79)
     std::vector<double> oldSurfArea, dYdT;
+    std::vector<double> hrt;              // storage hydraulic residence time (Storage.hrt)
     std::vector<int> converged;
     // quality [p][object]
     std::vector<double> nOldQual, nNewQual, lOldQual, lNewQual;

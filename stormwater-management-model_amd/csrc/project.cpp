@@ -1256,7 +1256,7 @@ int Project::readHotstart()
     double x;
     for (int i = 0; i < nn; i++) {
         if (!rdf(&s.newDepth[i]) || !rdf(&s.newLatFlow[i])) break;
-        if (version >= 4 && net.nodeType[i] == STORAGE && !rdf(&x)) break;
+        if (version >= 4 && net.nodeType[i] == STORAGE && !rdf(&s.hrt[i])) break;
         bool ok = true;
         for (int p = 0; p < P && ok; p++) ok = rdf(&s.nNewQual[(size_t)p * nn + i]);
         for (int p = 0; version <= 2 && p < P && ok; p++) ok = rdf(&x);
@@ -1288,7 +1288,7 @@ int Project::saveHotstart()   // openHotstartFile2 + saveRouting (hotstart.c:175
     for (int i = 0; i < nn; i++) {
         buf.push_back((float)s.newDepth[i]);
         buf.push_back((float)s.newLatFlow[i]);
-        if (net.nodeType[i] == STORAGE) buf.push_back(0.0f);   // storage hrt
+        if (net.nodeType[i] == STORAGE) buf.push_back((float)s.hrt[i]);
         for (int p = 0; p < P; p++) buf.push_back((float)s.nNewQual[(size_t)p * nn + i]);
     }
     for (int i = 0; i < nl; i++) {
@@ -1599,7 +1599,7 @@ int Project::initState()
     auto z = [](std::vector<double>& v, int n) { v.assign(n, 0.0); };
     for (auto* v : {&s.newDepth, &s.oldDepth, &s.newVolume, &s.oldVolume, &s.inflow, &s.outflow,
                     &s.overflow, &s.losses, &s.newLatFlow, &s.oldLatFlow, &s.oldNetInflow,
-                    &s.oldFlowInflow, &s.oldSurfArea, &s.dYdT}) z(*v, nn);
+                    &s.oldFlowInflow, &s.oldSurfArea, &s.dYdT, &s.hrt}) z(*v, nn);
     for (auto* v : {&s.lNewFlow, &s.lOldFlow, &s.lNewDepth, &s.lOldDepth, &s.lNewVolume,
                     &s.lOldVolume, &s.surfArea1, &s.surfArea2, &s.froude, &s.dqdh, &s.setting,
                     &s.a1, &s.a2, &s.q1, &s.q2, &s.evapLossRate, &s.seepLossRate}) z(*v, nl);

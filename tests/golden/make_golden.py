@@ -57,6 +57,8 @@ CASES = {
                                                    storage=True), 1),
     "example_storage_var": (netgen.write_example, dict(end_time="02:00:00", route_step=10.0,
                                                        variable_step=0.75, storage=True), 1),
+    "example_storage_qual": (netgen.write_example, dict(end_time="01:30:00", route_step=5.0,
+                                                        storage=True, pollutants=True), 1),
     # swmm_setValue between steps: external inflow, outfall stage, routing step
     "example_api": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
                                                variable_step=0.75), 1),
