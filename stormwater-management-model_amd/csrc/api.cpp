@@ -547,7 +547,7 @@ double DLLEXPORT swmm_getValue(int property, int index)   // swmm5.c:842-1213
             case swmm_LINK_TOPWIDTH: return getWofY(g, y, ct) * uL;
             case swmm_LINK_VELOCITY: {                     // link_getVelocity link.c:821-843
                 double v = 0.0;
-                if (y > 0.01) {
+                if (y > 0.01 && n.linkType[index] == CONDUIT) {
                     double fl = fabs(q) / n.barrels[index];
                     double area = getAofY(g, y, ct);
                     if (area > kFudge) v = fl / area;
@@ -567,7 +567,7 @@ double DLLEXPORT swmm_getValue(int property, int index)   // swmm5.c:842-1213
         case swmm_LINK_FULLFLOW: return n.qFull[index] * uQ;
         case swmm_LINK_FLOW: return st ? s.lNewFlow[index] * uQ * (double)n.direction[index] : 0.0;
         case swmm_LINK_VELOCITY: {
-            if (!st) return 0.0;
+            if (!st || n.linkType[index] != CONDUIT) return 0.0;   // link_getVelocity: conduits only
             double depth = s.lNewDepth[index], v = 0.0;
             if (depth > 0.01) {
                 double fl = fabs(s.lNewFlow[index]) / n.barrels[index];

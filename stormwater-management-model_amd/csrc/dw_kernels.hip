@@ -37,6 +37,7 @@
 #include "router.h"
 #include "xsect.h"
 #include "storage.h"
+#include "regulators.h"
 
 namespace swx {
 
@@ -75,6 +76,8 @@ enum : uint32_t {
     LF_QLIMIT = 1u << 20,
     LF_DIRNEG = 1u << 21,
     LF_COLD = 1u << 22,           // an invert offset: may need normal/critical depth
+    LF_NC = 1u << 23,             // pump / orifice / weir / outlet (k_nc; also LF_COLD)
+    LF_PUMP = 1u << 24,
 };
 // ---- packed per-node flags -------------------------------------------------
 enum : uint32_t {
@@ -85,6 +88,7 @@ enum : uint32_t {
     NF_SHARED = 1u << 7,          // multi-GPU: touched by conduits of several ranks
     NF_REPLICA = 1u << 8,         // multi-GPU: replica of a node another rank owns
     NF_DEG0 = 1u << 9,            // degree 0 (no outflow link; massbal.c:622)
+    NF_DEFER = 1u << 10,          // end node of a non-conduit link: updated by k_nc
 };
 // ---- packed link state word ------------------------------------------------
 // bits 0-3 flowClass, 4-7 fullState code (0 / 8 / 9 / 10), 8 normalFlow,
@@ -188,6 +192,20 @@ struct Params {
     double* nEvapVol;             // per node: this step's evaporated volume
     double* hrt;                  // per node: storage hydraulic residence time (sec)
     int* ulist;                   // [2][nN] unconverged nodes of the last two iterations
+    // non-conduit links (k_nc), in link order
+    int nNC, nDef;
+    const int* ncLinks;           // [nNC] link index
+    const NcLink* ncL;            // [nNC] static parameters
+    double* ncCoef;               // [nNC][4] cOrif, cWeir, hCrit, cSurcharge
+    double* ncTarget;             // [nNC] target setting
+    double* ncSurf;               // [nNC] orifice / weir equivalent surface area
+    double* ncQ;                  // [nNC] this iteration's raw flow (pumps)
+    int* ncBypass;                // [nNC] bypassed in this iteration
+    const int* defNodes;          // [nDef] deferred nodes (ends of non-conduit links)
+    double* nPrevDepth;           // outfalls: depth before this iteration's prologue
+    const int *qrowptr, *qcsr;    // CSR over all links (quality mass inflow, link order)
+    double *pUtil, *pAvg, *pVol, *pEnergy, *pOffLow, *pOffHigh, *pMin, *pMax;   // PumpStats, per link
+    int *pStarts, *pPeriods;
     const double* latIn;          // lateral inflow for this step
     // quality [p][object]
     double *nOldQual, *nNewQual, *lOldQual, *lNewQual;
@@ -889,14 +907,16 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
             int c = base + lane;
             int j = (c < p.nOutLinks) ? p.outLinks[c] : -1;
             uint32_t f = (j >= 0) ? p.lflags[j] : 0u;
-            double yn = 0.0;
-            if (j >= 0 && w == 0) yn = outfallPart<0>(p, j, f, ct);
-            if (j >= 0 && w == 1) yc[lane] = outfallPart<1>(p, j, f, ct);
+            double yn = 0.0;                               // non-conduits: yNorm = yCrit = 0
+            if (j >= 0 && w == 0 && !(f & LF_NC)) yn = outfallPart<0>(p, j, f, ct);
+            if (j >= 0 && w == 1) yc[lane] = (f & LF_NC) ? 0.0 : outfallPart<1>(p, j, f, ct);
             __syncthreads();
             if (j >= 0 && w == 0) {
                 int2 nn = p.lnodes[j];
                 int o = (f & LF_N2_OUTFALL) ? nn.y : nn.x;    // link.c:743-753 (node2 first)
-                if (kFirst) p.nOldDepth[o] = p.nNewDepth[o];   // node_setOldHydState before the update
+                double prev = p.nNewDepth[o];
+                if (kFirst) p.nOldDepth[o] = prev;             // node_setOldHydState before the update
+                if (p.nNC) p.nPrevDepth[o] = prev;
                 p.nNewDepth[o] = outfallCombine(p, o, p.nflags[o], j, yn, yc[lane]);
             }
             __syncthreads();
@@ -917,7 +937,7 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
             // all fast-path operands issued at once (one memory round trip)
             unsigned char cache = p.dirty[i];
             double yLast2 = p.nNewDepth[i], yCrown = p.yCrown[i], yRaw = p.yRaw[i], yMax = p.yMaxNP[i];
-            if (type != OUTFALL && !(nf & NF_SHARED) && cache == 2) {
+            if (type != OUTFALL && !(nf & (NF_SHARED | NF_DEFER)) && cache == 2) {
                 // plain clean junction: the relaxation step of setNodeDepth
                 // (dynwave.c:700-715) on the cached unrelaxed depth
                 bool sur = p.surchargeMethod == SUR_EXTRAN && yCrown > 0.0 && yLast2 > yCrown;
@@ -958,8 +978,8 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
             lat = p.newLat[i];
         }
         double inflow, outflow, surf, sumdqdh;
-        const bool reuse = !kFirst && k >= 2 && !(nf & (NF_CANPOND | NF_SHARED)) && type != STORAGE &&
-                           !(p.dirty[i] & 1);
+        const bool reuse = !kFirst && k >= 2 && !(nf & (NF_CANPOND | NF_SHARED | NF_DEFER)) &&
+                           type != STORAGE && !(p.dirty[i] & 1);
         if (reuse) {
             inflow = p.inflow[i];
             outflow = p.outflow[i];
@@ -1015,6 +1035,9 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
         }
         if (type == OUTFALL) {
             // depth set by the prologue
+        } else if (nf & NF_DEFER) {
+            // conduit sums written above; k_nc adds the non-conduit links
+            // and updates the depth
         } else if (nf & NF_SHARED) {                       // multi-GPU: partial sums out
             int s4 = 4 * p.sharedSlot[i];
             p.xsend[s4] = inflow;
@@ -1084,6 +1107,199 @@ __global__ __launch_bounds__(kBlock) void k_node_shared(Params p, int k)
     if (blockIdx.x == 0 && threadIdx.x == 0 && p.xrecv[p.xflag] > 0.0) p.ctl->unconv[k] = 1;
 }
 
+// ---------------------------------------------------------------------------
+// Non-conduit links (findLinkFlows' second loop, dynwave.c:404-412, and
+// findNonConduitFlow / getModPumpFlow / findNonConduitSurfArea /
+// updateNodeFlows, dynwave.c:423-590), then the depths of their end nodes
+// (setNodeDepth).  One workgroup: the flow of every regulator depends only on
+// last iteration's depths and runs in parallel; a pump's inlet limits and the
+// node sums need the running node totals in link order, which one thread
+// accumulates; the deferred nodes then update in parallel.
+__device__ __forceinline__ double ncDepth(const Params& p, int n)
+{
+    // an outfall's depth was refreshed by this iteration's k_node prologue;
+    // the link flows of the reference use the previous one
+    return ((int)(p.nflags[n] & NF_TYPE) == OUTFALL) ? p.nPrevDepth[n] : p.nNewDepth[n];
+}
+
+template <bool kFirst>
+__global__ __launch_bounds__(kBlock) void k_nc(Params p, int k)
+{
+    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
+    __shared__ double ct[5 * SWX_CIRC_N];
+    __shared__ int anyU;
+    stageTables(ct, p.gTables);
+    if (threadIdx.x == 0) anyU = 0;
+    const double dt = p.ctl->dt;
+    const double ucfV = p.ucfV;
+    if (kFirst) {
+        // link_setOldHydState + link_setTargetSetting / link_setSetting for
+        // pumps (routing.c:214-227, link.c:604-640), node_initFlows overflow
+        for (int c = threadIdx.x; c < p.nNC; c += kBlock) {
+            int j = p.ncLinks[c];
+            p.lOldFlow[j] = p.lNewFlow[j];
+            p.lOldDepth[j] = p.lNewDepth[j];
+            p.lOldVolume[j] = p.lNewVolume[j];
+            const NcLink& L = p.ncL[c];
+            double set = p.setting[j], ts = p.ncTarget[c];
+            if (L.type == LK_PUMP) {
+                int n1 = p.lnodes[j].x;
+                double y1 = p.nOldDepth[n1];
+                ts = set;
+                if (L.yOff > 0.0 && set > 0.0 && y1 < L.yOff) ts = 0.0;
+                if (L.yOn > 0.0 && set == 0.0 && y1 > L.yOn) ts = 1.0;
+                if (ts != set) p.setting[j] = ts;
+            }
+            p.ncTarget[c] = ts;
+        }
+        for (int d = threadIdx.x; d < p.nDef; d += kBlock) {
+            int i = p.defNodes[d];
+            if ((int)(p.nflags[i] & NF_TYPE) == OUTFALL) continue;
+            double v = p.nNewVolume[i], fv = p.fullVolume[i];
+            p.overflow[i] = (v > fv) ? (v - fv) / dt : 0.0;
+        }
+        __syncthreads();
+    }
+    // ---- phase A: regulator / pump-curve flows from last iteration's depths
+    for (int c = threadIdx.x; c < p.nNC; c += kBlock) {
+        int j = p.ncLinks[c];
+        int2 nn = p.lnodes[j];
+        int byp = (k >= 2 && p.conv[nn.x] && p.conv[nn.y]) ? 1 : 0;   // findBypassedLinks
+        p.ncBypass[c] = byp;
+        if (byp) continue;
+        const NcLink& L = p.ncL[c];
+        uint32_t f = p.lflags[j];
+        double qLast = p.lNewFlow[j];
+        NcOut o;
+        o.dqdh = 0.0;
+        o.depth = p.lNewDepth[j];
+        o.surfArea = p.ncSurf[c];
+        o.flowClass = p.lstate[j] & 0xF;
+        double set = p.setting[j], q = 0.0;
+        double y1 = ncDepth(p, nn.x), y2 = ncDepth(p, nn.y);
+        double inv1 = p.invert[nn.x], inv2 = p.invert[nn.y];
+        bool of1 = (f & LF_N1_OFLAP) != 0, of2 = (f & LF_N2_OFLAP) != 0;
+        const double* cx = p.curveX + L.cOff;
+        const double* cy = p.curveY + L.cOff;
+        NcCoef cf;
+        cf.cOrif = p.ncCoef[4 * c];
+        cf.cWeir = p.ncCoef[4 * c + 1];
+        cf.hCrit = p.ncCoef[4 * c + 2];
+        cf.cSurcharge = p.ncCoef[4 * c + 3];
+        if (set != 0.0) {                                   // link_getInflow (link.c:543-560)
+            Geom g = loadGeom<false>(p, j, f);
+            switch (L.type) {
+            case LK_ORIFICE: q = orificeInflow(L, g, cf, set, y1, y2, inv1, inv2, of1, of2, &o, ct); break;
+            case LK_WEIR: q = weirInflow(L, g, cf, cx, cy, set, y1, y2, inv1, inv2, of1, of2, &o, ct); break;
+            case LK_OUTLET: q = outletInflow(L, cx, cy, set, y1, y2, inv1, inv2, of1, of2, &o); break;
+            case LK_PUMP:
+                set = p.ncTarget[c];                        // pump_getInflow (link.c:1564-1566)
+                p.setting[j] = set;
+                o.flowClass = 0;
+                if (set != 0.0 && L.sub != PT_IDEAL)
+                    q = pumpInflow(L, cx, cy, set, y1, y2, inv1, inv2, p.nNewVolume[nn.x], ucfV, &o);
+                break;
+            }
+        }
+        // findNonConduitSurfArea (dynwave.c:510-525)
+        double sa1 = (L.type == LK_ORIFICE) ? o.surfArea / 2. : 0.0, sa2 = sa1;
+        if (L.type == LK_ORIFICE || L.type == LK_WEIR) p.ncSurf[c] = o.surfArea;
+        if (o.flowClass == FC_UP_CRITICAL || (int)(p.nflags[nn.x] & NF_TYPE) == STORAGE) sa1 = 0.0;
+        if (o.flowClass == FC_DN_CRITICAL || (int)(p.nflags[nn.y] & NF_TYPE) == STORAGE) sa2 = 0.0;
+        p.sa1[j] = sa1;
+        p.sa2[j] = sa2;
+        p.dqdh[j] = o.dqdh;
+        p.lNewDepth[j] = o.depth;
+        p.lstate[j] = (p.lstate[j] & ~0xF) | (o.flowClass & 0xF);
+        if (L.type == LK_PUMP) {
+            p.ncQ[c] = q;
+        } else {
+            if (k > 0) {                                    // under-relaxation (dynwave.c:455-461)
+                q = (1.0 - 0.5) * qLast + 0.5 * q;
+                if (q * qLast < 0.0) q = 0.001 * ((q < 0.0) ? -1.0 : 1.0);
+            }
+            p.lNewFlow[j] = q;
+        }
+    }
+    __syncthreads();
+    // ---- phase B: link-order accumulation into the end nodes (one thread)
+    if (threadIdx.x == 0) {
+        for (int c = 0; c < p.nNC; c++) {
+            int j = p.ncLinks[c];
+            int2 nn = p.lnodes[j];
+            const NcLink& L = p.ncL[c];
+            int n1 = nn.x, n2 = nn.y;
+            if (L.type == LK_PUMP && !p.ncBypass[c]) {
+                double q = p.ncQ[c];
+                double set = p.setting[j];
+                if (L.sub == PT_IDEAL && set != 0.0) {      // pump_getInflow IDEAL_PUMP
+                    q = p.inflow[n1] + p.overflow[n1];
+                    if (q < 0.0) q = 0.0;
+                    q = q * set;
+                }
+                if (q != 0.0) {                             // getModPumpFlow (dynwave.c:466-503)
+                    bool maxOut = (int)(p.nflags[n1] & NF_TYPE) == STORAGE || L.sub == PT_TYPE1;
+                    if (maxOut) {                           // node_getMaxOutflow (node.c:418-434)
+                        if (p.fullVolume[n1] > 0.0) {
+                            double qMax = p.inflow[n1] + p.nOldVolume[n1] / dt;
+                            if (q > qMax) q = qMax;
+                        }
+                        q = gmax(0.0, q);
+                    } else if (L.sub == PT_TYPE2 || L.sub == PT_TYPE3 || L.sub == PT_TYPE4) {
+                        double newNet = p.inflow[n1] - p.outflow[n1] - q;
+                        double vol = 0.5 * (p.oldNetInflow[n1] + newNet) * dt;
+                        double y = p.nOldDepth[n1] + vol / p.nSurf[n1];
+                        if (y <= 0.0) q = p.inflow[n1];
+                    }
+                }
+                p.lNewFlow[j] = q;
+            }
+            // updateNodeFlows (dynwave.c:531-590)
+            double q = p.lNewFlow[j];
+            if (q >= 0.0) { p.outflow[n1] += q; p.inflow[n2] += q; }
+            else { p.inflow[n1] -= q; p.outflow[n2] -= q; }
+            p.nSurf[n1] += p.sa1[j];
+            p.nSurf[n2] += p.sa2[j];
+            double dq = p.dqdh[j];
+            p.nDqdh[n1] += dq;
+            if (!(L.type == LK_PUMP && L.sub == PT_TYPE4)) p.nDqdh[n2] += dq;
+        }
+        __threadfence();
+    }
+    __syncthreads();
+    // ---- phase C: setNodeDepth for the deferred nodes
+    bool anyUnconv = false;
+    int* ulist = p.ulist + (size_t)(k & 1) * p.nN;
+    for (int base = 0; base < p.nDef; base += kBlock) {
+        int d = base + threadIdx.x;
+        bool listMe = false;
+        if (d < p.nDef) {
+            int i = p.defNodes[d];
+            uint32_t nf = p.nflags[i];
+            if ((int)(nf & NF_TYPE) != OUTFALL) {
+                double yLast = p.nNewDepth[i], yOld = p.nOldDepth[i];
+                if (!nodeUpdate(p, i, k, nf, dt, yLast, yOld, p.inflow[i], p.outflow[i], p.nSurf[i],
+                                p.nDqdh[i])) {
+                    anyUnconv = true;
+                    listMe = true;
+                }
+            }
+        }
+        if (!kFirst) {
+            unsigned long long m = __ballot(listMe);
+            if (m) {
+                int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1, b = 0;
+                if (lane == leader) b = atomicAdd(&p.ctl->ucount[k], __popcll(m));
+                b = __shfl(b, leader, 64);
+                if (listMe) ulist[b + __popcll(m & ((1ull << lane) - 1ull))] = p.defNodes[d];
+            }
+        }
+    }
+    if (anyUnconv) anyU = 1;
+    __syncthreads();
+    if (threadIdx.x == 0 && anyU) p.ctl->unconv[k] = 1;
+}
+
 // qualrout.c:146-174, 498-518
 __device__ __forceinline__ double mixedQual(double c, double v1, double wIn, double qIn, double tStep)
 {
@@ -1111,7 +1327,7 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
         double qIn = p.inflow[i];
         double oldVol = p.nOldVolume[i];
-        int e0 = p.rowptr[i], e1 = p.rowptr[i + 1];
+        int e0 = p.qrowptr[i], e1 = p.qrowptr[i + 1];
         const bool isStorage = (int)(p.nflags[i] & NF_TYPE) == STORAGE;
         double fEvap = 1.0;
         if (isStorage) {                     // findStorageQual (qualrout.c:417-436)
@@ -1128,7 +1344,7 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
             p.nOldQual[ni] = cOld;
             double w = p.qualIn[ni];
             for (int e = e0; e < e1; e++) {
-                int ent = p.csr[e];
+                int ent = p.qcsr[e];
                 int l = ent & 0x7FFFFFFF;
                 bool isN2 = ent < 0;
                 double ql = p.lNewFlow[l];
@@ -1159,6 +1375,14 @@ __global__ __launch_bounds__(kBlock) void k_qual_link(Params p)
         double nf = p.lNewFlow[j];
         int up = (nf < 0.0) ? nn.y : nn.x;
         uint32_t f = p.lflags[j];
+        if (f & LF_NC) {                      // non-conduit: upstream node's quality (qualrout.c:283-291)
+            for (int pp = 0; pp < p.P; pp++) {
+                size_t li = (size_t)pp * p.nL + j;
+                p.lOldQual[li] = p.lNewQual[li];
+                p.lNewQual[li] = p.nNewQual[(size_t)pp * p.nN + up];
+            }
+            continue;
+        }
         double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
         double qIn = fabs(p.q1[j]) * barrels;
         double qSeep = p.seepLoss[j] * barrels;
@@ -1246,6 +1470,42 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
     // links (fixed order within a thread: j = tid, tid + n, ...)
     for (int j = tid; j < p.nL; j += n) {
         uint32_t f = p.lflags[j];
+        if (f & LF_NC) {                                   // stats_updateLinkStats, non-conduits
+            if (!stats) continue;
+            double newFlow = p.lNewFlow[j], oldFlow = p.lOldFlow[j];
+            double dq = newFlow - oldFlow;
+            double q = fabs(newFlow);
+            if (q > S.lMaxFlow[j]) { S.lMaxFlow[j] = q; S.lMaxFlowDate[j] = aDate; }
+            double depth = p.lNewDepth[j];
+            if (depth > S.lMaxDepth[j]) S.lMaxDepth[j] = depth;
+            if (f & LF_PUMP) {
+                if (q >= S.qFull[j]) S.lTimeFullFlow[j] += dt;
+                if (q > 0.001) {
+                    int2 nn = p.lnodes[j];
+                    p.pMin[j] = gmin(p.pMin[j], q);
+                    p.pMax[j] = S.lMaxFlow[j];
+                    p.pAvg[j] += q;
+                    p.pVol[j] += q * dt;
+                    p.pUtil[j] += dt;
+                    double dh = (p.invert[nn.x] + p.nNewDepth[nn.x]) - (p.invert[nn.y] + p.nNewDepth[nn.y]);
+                    double power = fabs(dh) * q / 8.814 * 0.7457;          // link_getPower
+                    p.pEnergy[j] += power * dt / 3600.0;
+                    int fc = p.lstate[j] & 0xF;
+                    if (fc == FC_DN_DRY) p.pOffLow[j] += dt;
+                    if (fc == FC_UP_DRY) p.pOffHigh[j] += dt;
+                    if (oldFlow < 0.001) p.pStarts[j] += 1;
+                    p.pPeriods[j] += 1;
+                    S.lTimeSurch[j] += dt;
+                    S.lTimeFullUp[j] += dt;
+                    S.lTimeFullDn[j] += dt;
+                }
+            }
+            int k0 = S.lTurnSign[j];
+            int sg = (dq < 0) ? -1 : 1;
+            S.lTurnSign[j] = sg;
+            if (fabs(dq) > 0.001 && k0 * sg < 0) S.lTurns[j] += 1;
+            continue;
+        }
         double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
         int s = p.lstate[j] & ~(1 << 9);
         double a1 = p.a1[j];
@@ -1572,14 +1832,20 @@ __global__ __launch_bounds__(kBlock) void k_pack_results(Params p, double f, dou
         double q = f1 * p.lOldFlow[j] + f * p.lNewFlow[j];
         double v = f1 * p.lOldVolume[j] + f * p.lNewVolume[j];
         double u = 0.0;
-        if (y > 0.01) {                                  // link_getVelocity link.c:821-843
-            double barrels = (double)((fl >> LF_BARREL_SHIFT) & 0xFF);
-            double fq = q / barrels;
-            double area = getAofY(g, y, ct);
-            if (area > 0.0001) u = fq / area;
-        }
         double c = 0.0;
-        if (g.type != G_DUMMY) c = getAofY(g, y, ct) / g.aFull;
+        if (fl & LF_NC) {
+            c = p.setting[j];                            // link.c:699-707
+            double qo = p.lOldFlow[j], qn = p.lNewFlow[j];
+            if ((fl & LF_PUMP) && qo * qn == 0.0) q = (f >= f1) ? qn : qo;
+        } else {
+            if (y > 0.01) {                              // link_getVelocity link.c:821-843
+                double barrels = (double)((fl >> LF_BARREL_SHIFT) & 0xFF);
+                double fq = q / barrels;
+                double area = getAofY(g, y, ct);
+                if (area > 0.0001) u = fq / area;
+            }
+            if (g.type != G_DUMMY) c = getAofY(g, y, ct) / g.aFull;
+        }
         double dir = (fl & LF_DIRNEG) ? -1.0 : 1.0;
         y *= uL;
         v *= uV;
@@ -1758,6 +2024,10 @@ static void launchIteration(Router::Impl* d, int k)
         exchange(d, p.xsend, p.xrecv, (size_t)p.xflag + 1, 0);
         hipLaunchKernelGGL(k_node_shared, dim3(d->gridS), dim3(kBlock), 0, d->stream, p, k);
     }
+    if (p.nNC > 0) {                               // pumps / regulators, their end nodes
+        if (k == 0) hipLaunchKernelGGL(k_nc<true>, dim3(1), dim3(kBlock), 0, d->stream, p, k);
+        else hipLaunchKernelGGL(k_nc<false>, dim3(1), dim3(kBlock), 0, d->stream, p, k);
+    }
     if (d->timing) (void)hipEventRecord(d->curEv[4 * k + 2], d->stream);
 }
 
@@ -1878,8 +2148,15 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     std::vector<int> lflags(nL), coldLinks, outLinks;
     std::vector<double> inv1(nL), inv2(nL), xd[11];
     for (auto& v : xd) v.resize(nL);
+    if (net.nNC > 0 && part.active()) {
+        fail("pumps / regulators are not yet supported with more than one GPU");
+        return err_;
+    }
     for (int jj = 0; jj < gL; jj++)
-        if (net.linkType[jj] != CONDUIT) { fail("only conduit links are supported"); return err_; }
+        if (net.linkType[jj] == CONDUIT && net.xsect[jj].type == X_DUMMY) {
+            fail("dummy conduits are not supported yet");
+            return err_;
+        }
     for (int j = 0; j < nL; j++) {
         const int g = LL[j];                        // global link index
         int n1 = net.node1[g], n2 = net.node2[g];   // global node indices
@@ -1897,11 +2174,13 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (net.seepRate[g] > 0.0 || (prj.opt.evapRate > 0.0 && isOpen(x.type))) f |= LF_SEEP;
         if (net.qLimit[g] > 0.0) f |= LF_QLIMIT;
         if (net.direction[g] < 0) f |= LF_DIRNEG;
-        if (net.offset1[g] > 0.0 || net.offset2[g] > 0.0) {
+        if (net.linkType[g] != CONDUIT) {
+            f |= LF_NC | LF_COLD;                   // k_nc, not the conduit kernels
+            if (net.linkType[g] == PUMP) f |= LF_PUMP;
+        } else if (net.offset1[g] > 0.0 || net.offset2[g] > 0.0) {
             f |= LF_COLD;
             coldLinks.push_back(j);
         }
-        if (f & (LF_N1_OUTFALL | LF_N2_OUTFALL)) outLinks.push_back(j);
         lflags[j] = (int)f;
         xd[0][j] = x.yFull; xd[1][j] = x.wMax; xd[2][j] = x.ywMax; xd[3][j] = x.aFull;
         xd[4][j] = x.rFull; xd[5][j] = x.sFull; xd[6][j] = x.sMax; xd[7][j] = x.yBot;
@@ -1918,9 +2197,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         UPI(cl, coldLinks, coldLinks.size());
         p.coldLinks = cl;
         p.nCold = (int)coldLinks.size();
-        UPI(cl, outLinks, outLinks.size());
-        p.outLinks = cl;
-        p.nOutLinks = getenv("SWMM5_TIMING_NO_OUTFALL") ? 0 : (int)outLinks.size();   // timing experiment only
+
     }
     double* tmp;
     UPD(tmp, inv1, nL); p.inv1 = tmp;
@@ -1997,21 +2274,53 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     }
     // CSR: incident links per node, ascending link index (all links are true
     // conduits, so this is exactly the order of dynwave.c:398-401)
-    std::vector<int> rowptr(nN + 1, 0), csr;
-    for (int j = 0; j < nL; j++) { rowptr[nodes2[2 * j] + 1]++; rowptr[nodes2[2 * j + 1] + 1]++; }
-    for (int i = 0; i < nN; i++) rowptr[i + 1] += rowptr[i];
-    csr.resize(rowptr[nN]);
-    {
+    // Pumps / regulators are not in it: their flows join the node sums after
+    // all conduits (dynwave.c:398-412), in k_nc.  The quality CSR keeps every
+    // link in link order (findLinkMassFlow, qualrout.c:111).
+    auto buildCsr = [&](bool all, std::vector<int>& rowptr, std::vector<int>& csr) {
+        rowptr.assign(nN + 1, 0);
+        for (int j = 0; j < nL; j++) {
+            if (!all && (lflags[j] & LF_NC)) continue;
+            rowptr[nodes2[2 * j] + 1]++;
+            rowptr[nodes2[2 * j + 1] + 1]++;
+        }
+        for (int i = 0; i < nN; i++) rowptr[i + 1] += rowptr[i];
+        csr.resize(rowptr[nN]);
         std::vector<int> fillp(rowptr.begin(), rowptr.end() - 1);
         for (int j = 0; j < nL; j++) {
+            if (!all && (lflags[j] & LF_NC)) continue;
             int a = nodes2[2 * j], b = nodes2[2 * j + 1];
             csr[fillp[a]++] = j;
             csr[fillp[b]++] = (int)((unsigned)j | 0x80000000u);
-            // the reference's link_setOutfallDepth loop: last link touching an
-            // outfall wins (validateGeneralLayout allows only one)
-            if (net.nodeType[LN[b]] == OUTFALL) outLink[b] = j;
-            else if (net.nodeType[LN[a]] == OUTFALL) outLink[a] = j;
         }
+    };
+    std::vector<int> rowptr, csr, qrowptr, qcsr;
+    buildCsr(false, rowptr, csr);
+    if (net.nNC > 0) buildCsr(true, qrowptr, qcsr);
+    // the reference's link_setOutfallDepth loop (findNodeDepths): the last
+    // link touching an outfall sets its depth
+    for (int j = 0; j < nL; j++) {
+        int a = nodes2[2 * j], b = nodes2[2 * j + 1];
+        if (net.nodeType[LN[b]] == OUTFALL) outLink[b] = j;
+        else if (net.nodeType[LN[a]] == OUTFALL) outLink[a] = j;
+    }
+    for (int i = 0; i < nN; i++)
+        if (outLink[i] >= 0) outLinks.push_back(outLink[i]);
+    std::sort(outLinks.begin(), outLinks.end());
+    {
+        int* cl;
+        UPI(cl, outLinks, outLinks.size());
+        p.outLinks = cl;
+        p.nOutLinks = getenv("SWMM5_TIMING_NO_OUTFALL") ? 0 : (int)outLinks.size();   // timing experiment only
+    }
+    // end nodes of pumps / regulators: depth updated by k_nc
+    std::vector<int> defNodes;
+    {
+        std::vector<char> isDef(nN, 0);
+        for (int j = 0; j < nL; j++)
+            if (lflags[j] & LF_NC) { isDef[nodes2[2 * j]] = 1; isDef[nodes2[2 * j + 1]] = 1; }
+        for (int i = 0; i < nN; i++)
+            if (isDef[i]) { defNodes.push_back(i); nflags[i] = (int)((uint32_t)nflags[i] | NF_DEFER); }
     }
     d->nE = (int)csr.size();
     {
@@ -2021,6 +2330,15 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         int* rp;
         UPI(rp, rowptr, nN + 1); p.rowptr = rp;
         UPI(rp, csr, csr.size()); p.csr = rp;
+        if (net.nNC > 0) {
+            UPI(rp, qrowptr, nN + 1); p.qrowptr = rp;
+            UPI(rp, qcsr, qcsr.size()); p.qcsr = rp;
+        } else {
+            p.qrowptr = p.rowptr;
+            p.qcsr = p.csr;
+        }
+        p.nDef = (int)defNodes.size();
+        UPI(rp, defNodes, defNodes.size()); p.defNodes = rp;
         UPI(rp, outLink, nN); p.outfallLink = rp;
     }
     UPD(tmp, gn(net.invertElev), nN); p.invert = tmp;
@@ -2035,18 +2353,18 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     {
         std::vector<int> shape(nN, -1), coff(nN, 0), cn(nN, 0);
         std::vector<double> cx, cy;
-        std::vector<int> curveOff(net.curves.size(), -1);
+        std::vector<int> curveOff(net.curves.size(), 0);   // every curve, in one table
+        for (size_t c = 0; c < net.curves.size(); c++) {
+            curveOff[c] = (int)cx.size();
+            cx.insert(cx.end(), net.curves[c].x.begin(), net.curves[c].x.end());
+            cy.insert(cy.end(), net.curves[c].y.begin(), net.curves[c].y.end());
+        }
         for (int i = 0; i < nN; i++) {
             const int g = LN[i];
             if (net.nodeType[g] != STORAGE) continue;
             shape[i] = net.stShape[g];
             int c = net.stCurve[g];
             if (c >= 0) {
-                if (curveOff[c] < 0) {
-                    curveOff[c] = (int)cx.size();
-                    cx.insert(cx.end(), net.curves[c].x.begin(), net.curves[c].x.end());
-                    cy.insert(cy.end(), net.curves[c].y.begin(), net.curves[c].y.end());
-                }
                 coff[i] = curveOff[c];
                 cn[i] = (int)net.curves[c].x.size();
             }
@@ -2064,7 +2382,49 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         UPD(tmp, cy, cy.size()); p.curveY = tmp;
         p.ucfL = prj.ucfLength();
         p.ucfV = prj.ucfVolume();
+        // pumps / regulators (k_nc), link order
+        {
+            std::vector<int> ncl;
+            std::vector<NcLink> ncs;
+            std::vector<double> coef, target, zero;
+            for (int j = 0; j < nL; j++) {
+                const int g = LL[j];
+                if (net.linkType[g] == CONDUIT) continue;
+                ncl.push_back(j);
+                NcLink L = prj.ncLink(g);
+                int c = net.ncCurve[g];
+                L.cOff = c >= 0 ? curveOff[c] : 0;
+                ncs.push_back(L);
+                coef.push_back(st.ncCOrif[g]);
+                coef.push_back(st.ncCWeir[g]);
+                coef.push_back(st.ncHCrit[g]);
+                coef.push_back(st.ncCSurch[g]);
+                target.push_back(st.targetSetting[g]);
+                zero.push_back(0.0);
+            }
+            p.nNC = (int)ncl.size();
+            if (ncl.empty()) { ncl.push_back(0); ncs.push_back(NcLink{}); coef.assign(4, 0.0); target.push_back(0.0); zero.push_back(0.0); }
+            int* ip2;
+            UPI(ip2, ncl, ncl.size()); p.ncLinks = ip2;
+            NcLink* dl = devAlloc<NcLink>(d, ncs.size(), &e);
+            if (e == hipSuccess) e = hipMemcpy(dl, ncs.data(), ncs.size() * sizeof(NcLink), hipMemcpyHostToDevice);
+            if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+            p.ncL = dl;
+            UPD(p.ncCoef, coef, coef.size());
+            UPD(p.ncTarget, target, target.size());
+            UPD(p.ncSurf, zero, zero.size());
+            UPD(p.ncQ, zero, zero.size());
+            std::vector<int> zi(zero.size(), 0);
+            UPI(p.ncBypass, zi, zi.size());
+            std::vector<double> zl(nL, 0.0);
+            for (double** a : {&p.pUtil, &p.pAvg, &p.pVol, &p.pEnergy, &p.pOffLow, &p.pOffHigh, &p.pMin, &p.pMax})
+                UPD(*a, zl, nL);
+            std::vector<int> zil(nL, 0);
+            UPI(p.pStarts, zil, nL);
+            UPI(p.pPeriods, zil, nL);
+        }
         std::vector<double> z(nN, 0.0);
+        UPD(p.nPrevDepth, gn(st.newDepth), nN);
         UPD(p.nLosses, z, nN);
         UPD(p.nEvapVol, z, nN);
         std::vector<double> h(nN, 0.0);

@@ -163,6 +163,13 @@ struct Network {
     std::vector<double> offset1, offset2, q0, qLimit, cLossInlet, cLossOutlet, cLossAvg,
         seepRate, length, roughness, modLength, roughFactor, slope, beta, qMax, qFull;
     std::vector<Xsect> xsect;
+    // pumps / orifices / weirs / outlets (link.c:315-399), indexed by link:
+    // sub-type (pump type, orifice type, weir type, outlet curve type), curve
+    // (pump curve, outlet rating curve, weir Cd curve), coefficients
+    std::vector<int> ncSub, ncCurve, ncCanSurcharge;
+    std::vector<double> ncC1, ncC2, ncEndCon, ncSlope, ncLength, ncYOn, ncYOff, ncXMin, ncXMax,
+        ncInitSetting;
+    int nNC = 0, nPumps = 0;
     // inflows / quality inputs
     std::vector<ExtInflow> extInflows;
     std::vector<DwfInflow> dwfInflows;
@@ -192,6 +199,9 @@ struct State {
     // Xnode (dynwave.c:72-79)
     std::vector<double> oldSurfArea, dYdT;
     std::vector<double> hrt;              // storage hydraulic residence time (Storage.hrt)
+    // non-conduit links: target setting and setting-dependent coefficients
+    // (orifice cOrif / cWeir / hCrit, weir cSurcharge)
+    std::vector<double> targetSetting, ncCOrif, ncCWeir, ncHCrit, ncCSurch;
     std::vector<int> converged;
     // quality [p][object]
     std::vector<double> nOldQual, nNewQual, lOldQual, lNewQual;

@@ -67,12 +67,15 @@ int OutFile::open(const std::string& path, Project& prj)  // output.c:121-405
     w4(f_, 5); w4(f_, 0); w4(f_, 4); w4(f_, 4); w4(f_, 3); w4(f_, 5);   // link input codes
     for (int j = 0; j < net.nLinks(); j++) {
         if (!net.linkRpt[j]) continue;
-        float r[4];
-        r[0] = (float)(net.offset1[j] * uL);
-        r[1] = (float)(net.offset2[j] * uL);
-        if (net.direction[j] < 0) std::swap(r[0], r[1]);
-        r[2] = (float)(net.xsect[j].yFull * uL);
-        r[3] = (float)(net.length[j] * uL);
+        float r[4] = {0.0f, 0.0f, 0.0f, 0.0f};        // pumps: all zero (output.c:281-284)
+        int k = net.linkType[j];
+        if (k != PUMP) {
+            r[0] = (float)(net.offset1[j] * uL);
+            r[1] = (float)(net.offset2[j] * uL);
+            if (net.direction[j] < 0) std::swap(r[0], r[1]);
+            r[2] = (k == OUTLET) ? 0.0f : (float)(net.xsect[j].yFull * uL);
+            r[3] = (k == CONDUIT) ? (float)(net.length[j] * uL) : 0.0f;
+        }
         w4(f_, net.linkType[j]);
         fwrite(r, 4, 4, f_);
     }

@@ -16,6 +16,7 @@
 // with ERR_INPUT naming the section (never silently ignored).
 #include "project.h"
 #include "storage.h"
+#include "regulators.h"
 
 #include <cmath>
 #include <cstdlib>
@@ -209,12 +210,16 @@ static bool getDouble(const char* s, double* y)
 enum Sect {
     S_NONE = -1, S_TITLE, S_OPTION, S_EVAP, S_JUNC, S_OUTFALL, S_CONDUIT, S_XSECT, S_LOSS,
     S_POLLUT, S_INFLOW, S_DWF, S_PATTERN, S_TSERIES, S_REPORT, S_FILES, S_STORAGE, S_CURVES,
-    S_SKIP, S_UNSUPPORTED
+    S_PUMP, S_ORIFICE, S_WEIR, S_OUTLET, S_SKIP, S_UNSUPPORTED
 };
 static const char* const kSectWords[] = {
     "[TITLE", "[OPTION", "[EVAP", "[JUNC", "[OUTFALL", "[CONDUIT", "[XSECT", "[LOSS",
     "[POLLUT", "[INFLOW", "[DWF", "[PATTERN", "[TIMESERIES", "[REPORT", "[FILES", "[STORAGE",
-    "[CURVE", nullptr};
+    "[CURVE", "[PUMP", "[ORIFICE", "[WEIR", "[OUTLET", nullptr};
+static const char* const kOffOnWords[] = {"OFF", "ON", nullptr};
+static const char* const kOrificeTypeWords[] = {"SIDE", "BOTTOM", nullptr};
+static const char* const kWeirTypeWords[] = {"TRANSVERSE", "SIDEFLOW", "V-NOTCH", "TRAPEZOIDAL",
+                                             "ROADWAY", nullptr};
 static const char* const kRelationWords[] = {"TABULAR", "FUNCTIONAL", "CYLINDRICAL", "CONICAL",
                                              "PARABOLIC", "PYRAMIDAL", nullptr};
 static const char* const kCurveTypeWords[] = {"STORAGE", "DIVERSION", "TIDAL", "RATING", "CONTROL",
@@ -388,6 +393,11 @@ int Project::readFile(const char* path)
                             &net.beta, &net.qMax, &net.qFull})
                 v->assign(nl, 0.0);
             net.xsect.assign(nl, Xsect());
+            net.ncSub.assign(nl, 0); net.ncCurve.assign(nl, -1); net.ncCanSurcharge.assign(nl, 1);
+            for (auto* v : {&net.ncC1, &net.ncC2, &net.ncEndCon, &net.ncSlope, &net.ncLength,
+                            &net.ncYOn, &net.ncYOff, &net.ncXMin, &net.ncXMax})
+                v->assign(nl, 0.0);
+            net.ncInitSetting.assign(nl, 1.0);
             for (auto& ts : net.tseries) ts.lastDate = opt.startDate + opt.startTime;  // input.c:168-171
             for (auto& p : net.patterns) { p.type = -1; p.count = 0; for (double& x : p.factor) x = 1.0; }
         }
@@ -428,6 +438,10 @@ int Project::parseLine(int sect, std::vector<char*>& tok, int pass)
             }
             return 0;
         case S_CONDUIT:
+        case S_PUMP:
+        case S_ORIFICE:
+        case S_WEIR:
+        case S_OUTLET:
             if (addId(net.linkIndex, net.linkId, tok[0]) < 0) return setError(207, std::string("ERROR 207: duplicate ID name ") + tok[0]);
             return 0;
         case S_POLLUT: {
@@ -476,6 +490,7 @@ int Project::parseLine(int sect, std::vector<char*>& tok, int pass)
     case S_REPORT: return readReport(tok);
     case S_FILES: return readFiles(tok);
     case S_STORAGE: return readStorage(tok);
+    case S_PUMP: case S_ORIFICE: case S_WEIR: case S_OUTLET: return readRegulator(sect, tok);
     case S_CURVES: return readCurve(tok);
     default: return 0;
     }
@@ -856,6 +871,151 @@ int Project::readConduit(std::vector<char*>& tok)  // link.c:933-988, 315-399
     return 0;
 }
 
+// pump_readParams / orifice_readParams / weir_readParams / outlet_readParams
+// (link.c:1406-1469, 1641-1692, 2042-2097, 2520-2596) + link_setParams
+int Project::readRegulator(int sect, std::vector<char*>& tok)
+{
+    int nt = (int)tok.size();
+    if (nt < 3) return 203;
+    int j = net.linkIndex.at(tok[0]);
+    auto a = net.nodeIndex.find(tok[1]);
+    auto b = net.nodeIndex.find(tok[2]);
+    if (a == net.nodeIndex.end() || b == net.nodeIndex.end()) return 209;
+    double u = ucfLength();
+    auto curveOf = [&](const char* t) {
+        auto it = net.curveIndex.find(t);
+        return it == net.curveIndex.end() ? -2 : it->second;
+    };
+    net.node1[j] = a->second;
+    net.node2[j] = b->second;
+    net.offset1[j] = net.offset2[j] = 0.0;
+    net.q0[j] = 0.0;
+    net.qFull[j] = 0.0;
+    net.hasFlapGate[j] = 0;
+    net.qLimit[j] = 0.0;
+    net.direction[j] = 1;
+    net.barrels[j] = 0;                  // no Conduit record
+    net.nNC++;
+    switch (sect) {
+    case S_PUMP: {
+        int curve = -1;
+        if (nt >= 4 && strcmp(tok[3], "*")) {
+            curve = curveOf(tok[3]);
+            if (curve < 0) return 209;
+        }
+        double init = 1.0, yOn = 0.0, yOff = 0.0;
+        if (nt >= 5) {
+            int m = kfind(tok[4], kOffOnWords);
+            if (m < 0) return 205;
+            init = m;
+        }
+        if (nt >= 6 && (!getDouble(tok[5], &yOn) || yOn < 0.0)) return 211;
+        if (nt >= 7 && (!getDouble(tok[6], &yOff) || yOff < 0.0)) return 211;
+        net.linkType[j] = PUMP;
+        net.ncCurve[j] = curve;
+        net.ncInitSetting[j] = init;
+        net.ncYOn[j] = yOn / u;
+        net.ncYOff[j] = yOff / u;
+        net.xsect[j].type = -1;               // pumps have no cross section
+        net.xsect[j].yFull = 0.0;
+        net.nPumps++;
+        return 0;
+    }
+    case S_ORIFICE: {
+        if (nt < 6) return 203;
+        int m = kfind(tok[3], kOrificeTypeWords);
+        if (m < 0) return 205;
+        double crest, cd, orate = 0.0;
+        if (opt.linkOffsetsElev && *tok[4] == '*') crest = kMissing;
+        else if (!getDouble(tok[4], &crest)) return 211;
+        if (!getDouble(tok[5], &cd) || cd < 0.0) return 211;
+        int flap = 0;
+        if (nt >= 7) { flap = kfind(tok[6], kNoYes); if (flap < 0) return 205; }
+        if (nt >= 8 && (!getDouble(tok[7], &orate) || orate < 0.0)) return 211;
+        net.linkType[j] = ORIFICE;
+        net.ncSub[j] = m;
+        net.offset1[j] = crest <= kMissing ? crest : crest / u;
+        net.offset2[j] = net.offset1[j];
+        net.ncC1[j] = cd;
+        net.hasFlapGate[j] = flap > 0;
+        net.ncC2[j] = orate * 3600.0;
+        return 0;
+    }
+    case S_WEIR: {
+        if (nt < 6) return 203;
+        int m = kfind(tok[3], kWeirTypeWords);
+        if (m < 0) return 205;
+        if (m == WR_ROADWAY)
+            return setError(200, "ERROR 200: roadway weirs are not supported by the MI355X engine yet");
+        double crest, cd1, endCon = 0.0, cd2 = 0.0;
+        if (opt.linkOffsetsElev && *tok[4] == '*') crest = kMissing;
+        else if (!getDouble(tok[4], &crest)) return 211;
+        if (!getDouble(tok[5], &cd1) || cd1 < 0.0) return 211;
+        int flap = 0, surch = 1, cdCurve = -1;
+        if (nt >= 7 && *tok[6] != '*') { flap = kfind(tok[6], kNoYes); if (flap < 0) return 205; }
+        if (nt >= 8 && *tok[7] != '*' && (!getDouble(tok[7], &endCon) || endCon < 0.0)) return 211;
+        if (nt >= 9 && *tok[8] != '*' && (!getDouble(tok[8], &cd2) || cd2 < 0.0)) return 211;
+        if (nt >= 10 && *tok[9] != '*') { surch = kfind(tok[9], kNoYes); if (surch < 0) return 205; }
+        if (nt >= 13 && *tok[12] != '*') { cdCurve = curveOf(tok[12]); if (cdCurve < 0) return 209; }
+        net.linkType[j] = WEIR;
+        net.ncSub[j] = m;
+        net.offset1[j] = crest <= kMissing ? crest : crest / u;
+        net.offset2[j] = net.offset1[j];
+        net.ncC1[j] = cd1;
+        net.hasFlapGate[j] = flap > 0;
+        net.ncEndCon[j] = endCon;
+        net.ncC2[j] = cd2;
+        net.ncCanSurcharge[j] = surch;
+        net.ncCurve[j] = cdCurve;
+        return 0;
+    }
+    case S_OUTLET: {
+        if (nt < 6) return 203;
+        double crest;
+        if (opt.linkOffsetsElev && *tok[3] == '*') crest = kMissing;
+        else {
+            if (!getDouble(tok[3], &crest)) return 211;
+            if (!opt.linkOffsetsElev && crest < 0.0) crest = 0.0;
+        }
+        std::string rel = tok[4];
+        int m = kfind(rel.c_str(), kRelationWords);
+        if (m < 0) return 205;
+        int ctype = 0;                        // NODE_DEPTH unless "/HEAD"
+        size_t sl = rel.find('/');
+        if (sl != std::string::npos) {
+            std::string q = rel.substr(sl + 1);
+            for (auto& ch : q) ch = (char)toupper((unsigned char)ch);
+            if (q == "HEAD") ctype = 1;
+        }
+        double coeff = 0.0, expon = 0.0;
+        int curve = -1, n;
+        if (m == ST_FUNCTIONAL) {
+            if (nt < 7) return 203;
+            if (!getDouble(tok[5], &coeff) || !getDouble(tok[6], &expon)) return 211;
+            n = 7;
+        } else {
+            curve = curveOf(tok[5]);
+            if (curve < 0) return 209;
+            n = 6;
+        }
+        int flap = 0;
+        if (nt > n) { flap = kfind(tok[n], kNoYes); if (flap < 0) return 205; }
+        net.linkType[j] = OUTLET;
+        net.offset1[j] = crest <= kMissing ? crest : crest / u;
+        net.offset2[j] = net.offset1[j];
+        net.ncC1[j] = coeff;
+        net.ncC2[j] = expon;
+        net.ncCurve[j] = curve;
+        net.hasFlapGate[j] = flap > 0;
+        net.ncSub[j] = ctype;
+        double zero[4] = {0, 0, 0, 0};
+        setXsectParams(net.xsect[j], X_DUMMY, zero, u);
+        return 0;
+    }
+    }
+    return 0;
+}
+
 // xsect.c:216-634 for the supported shapes
 bool setXsectParams(Xsect& x, int type, double p[4], double ucf)
 {
@@ -941,7 +1101,7 @@ int Project::readXsect(std::vector<char*>& tok)  // link.c:162-267
     int j = it->second;
     int k = kfind(tok[1], kXsectWords);
     if (k < 0) return 205;
-    net.barrels[j] = 1;
+    if (net.linkType[j] == CONDUIT) net.barrels[j] = 1;
     net.xsect[j].culvertCode = 0;
     if (!(k == X_CIRCULAR || k == X_RECT_CLOSED || k == X_RECT_OPEN || k == X_TRAPEZOIDAL ||
           k == X_TRIANGULAR))
@@ -951,7 +1111,9 @@ int Project::readXsect(std::vector<char*>& tok)  // link.c:162-267
     double x[4];
     for (int i = 2; i <= 5; i++)
         if (!getDouble(tok[i], &x[i - 2])) return 211;
+    if (net.linkType[j] != CONDUIT && k == X_RECT_OPEN) { x[2] = 0.0; x[3] = 0.0; }
     if (!setXsectParams(net.xsect[j], k, x, ucfLength())) return 211;
+    if (net.linkType[j] != CONDUIT) return 0;
     if (nt >= 7) {
         int i = atoi(tok[6]);
         if (i <= 0) return 211;
@@ -1416,6 +1578,77 @@ void Project::validateConduit(int j)  // link.c:992-1154 (supported shapes)
                         net.cLossAvg[j] == 0.0) ? 0 : 1;
 }
 
+// pump_validate / orifice_validate / weir_validate (link.c:1473-1530,
+// 1696-1725, 2102-2152) and the crest check of link_validate (link.c:421-438)
+void Project::validateRegulator(int j)
+{
+    const double* ct = &SWX_CIRC_TABLES[0][0];
+    Xsect& xs = net.xsect[j];
+    int type = net.linkType[j];
+    if (type == PUMP) {
+        xs.yFull = 0.0;
+        int m = net.ncCurve[j];
+        if (m < 0) net.ncSub[j] = PT_IDEAL;
+        else {
+            const Curve& c = net.curves[m];
+            if (c.type < CV_PUMP1 || c.type > CV_PUMP5) {
+                setError(143, "ERROR 143: invalid pump curve for Pump " + net.linkId[j]);
+                return;
+            }
+            net.ncSub[j] = c.type - CV_PUMP1;
+            if (!c.x.empty()) {
+                double q = c.y[0];
+                net.ncXMin[j] = c.x[0];
+                net.ncXMax[j] = c.x[0];
+                for (size_t i = 1; i < c.x.size(); i++) {
+                    q = gmax(c.y[i], q);
+                    net.ncXMax[j] = c.x[i];
+                }
+                net.qFull[j] = q / ucfFlow();
+            }
+        }
+        if (net.ncYOn[j] > 0.0 && net.ncYOn[j] <= net.ncYOff[j]) {
+            setError(145, "ERROR 145: pump startup depth not higher than shutoff depth for Pump " + net.linkId[j]);
+            return;
+        }
+        if (net.ncSub[j] == PT_TYPE1) {
+            int n1 = net.node1[j];
+            if (net.nodeType[n1] != STORAGE)
+                net.fullVolume[n1] = gmax(net.fullVolume[n1], net.ncXMax[j] / ucfVolume());
+        }
+        return;
+    }
+    if (type == ORIFICE) {
+        if (xs.type != X_RECT_CLOSED && xs.type != X_CIRCULAR) {
+            setError(121, "ERROR 121: invalid cross section shape for regulator " + net.linkId[j]);
+            return;
+        }
+        if (net.offset1[j] < 0.0) net.offset1[j] = 0.0;
+        net.ncLength[j] = 2.0 * opt.routeStep * sqrt(kGravity * xs.yFull);
+        net.ncLength[j] = gmax(200.0, net.ncLength[j]);
+    } else if (type == WEIR) {
+        int w = net.ncSub[j];
+        bool ok = true;
+        if (w == WR_TRANSVERSE || w == WR_SIDEFLOW) { ok = xs.type == X_RECT_OPEN; net.ncSlope[j] = 0.0; }
+        else if (w == WR_VNOTCH) { ok = xs.type == X_TRIANGULAR; if (ok) net.ncSlope[j] = xs.sBot; }
+        else if (w == WR_TRAPEZOIDAL) { ok = xs.type == X_TRAPEZOIDAL; if (ok) net.ncSlope[j] = xs.sBot; }
+        if (!ok) {
+            setError(121, "ERROR 121: invalid cross section shape for regulator " + net.linkId[j]);
+            return;
+        }
+        if (net.offset1[j] < 0.0) net.offset1[j] = 0.0;
+        net.ncLength[j] = 2.0 * opt.routeStep * sqrt(kGravity * xs.yFull);
+        net.ncLength[j] = gmax(200.0, net.ncLength[j]);
+    }
+    // crest below the downstream invert (DW: raised, link.c:421-438)
+    int n1 = net.node1[j], n2 = net.node2[j];
+    if (net.invertElev[n1] + net.offset1[j] < net.invertElev[n2]) {
+        net.offset1[j] = net.invertElev[n2] - net.invertElev[n1];
+        warnings++;
+    }
+    (void)ct;
+}
+
 void Project::validate()  // project.c:186-270
 {
     int nn = net.nNodes(), nl = net.nLinks();
@@ -1435,14 +1668,17 @@ void Project::validate()  // project.c:186-270
                 off = 0.0;
             }
         }
-        validateConduit(j);
+        if (net.linkType[j] == CONDUIT) validateConduit(j);
+        else validateRegulator(j);
         if (errorCode) return;
-        // link.c:440-463: storage units without surcharge keep their depth
+        // link.c:440-463: not for pumps and bottom orifices; storage units
+        // without surcharge keep their depth; downstream end for conduits only
+        if (net.linkType[j] == PUMP || (net.linkType[j] == ORIFICE && net.ncSub[j] == OR_BOTTOM)) continue;
         int n = net.node1[j];
         if (net.nodeType[n] != STORAGE || net.surDepth[n] > 0.0)
             net.fullDepth[n] = gmax(net.fullDepth[n], net.offset1[j] + net.xsect[j].yFull);
         n = net.node2[j];
-        if (net.nodeType[n] != STORAGE || net.surDepth[n] > 0.0)
+        if ((net.nodeType[n] != STORAGE || net.surDepth[n] > 0.0) && net.linkType[j] == CONDUIT)
             net.fullDepth[n] = gmax(net.fullDepth[n], net.offset2[j] + net.xsect[j].yFull);
     }
     for (int j = 0; j < nn; j++) {
@@ -1543,10 +1779,13 @@ void Project::initDepths()
         if (net.nodeType[net.node2[i]] == OUTFALL) { k = net.node2[i]; zz = net.offset2[i]; }
         else if (net.nodeType[net.node1[i]] == OUTFALL) { k = net.node1[i]; zz = net.offset1[i]; }
         else continue;
-        Geom g = geom(i);
-        double q = fabs(s.lNewFlow[i] / net.barrels[i]);
-        double yNorm = linkYnorm(g, q, net.qMax[i], net.beta[i], ct);
-        double yCrit = getYcrit(g, q, ct);
+        double yNorm = 0.0, yCrit = 0.0;
+        if (net.linkType[i] == CONDUIT) {
+            Geom g = geom(i);
+            double q = fabs(s.lNewFlow[i] / net.barrels[i]);
+            yNorm = linkYnorm(g, q, net.qMax[i], net.beta[i], ct);
+            yCrit = getYcrit(g, q, ct);
+        }
         // outfall_setOutletDepth (node.c:1413-1492), FREE/NORMAL/FIXED/TSERIES
         double stage, yNew;
         int ot = net.outfallType[k];
@@ -1564,7 +1803,7 @@ void Project::initDepths()
     }
     // initLinkDepths (flowrout.c:389-421)
     for (int i = 0; i < nl; i++) {
-        if (net.q0[i] != 0.0) continue;
+        if (net.linkType[i] != CONDUIT || net.q0[i] != 0.0) continue;
         double y1 = s.newDepth[net.node1[i]] - net.offset1[i];
         y1 = gmax(y1, 0.0);
         y1 = gmin(y1, net.xsect[i].yFull);
@@ -1627,18 +1866,43 @@ int Project::initState()
         }
         s.newVolume[j] = s.oldVolume[j];
     }
-    // link_initState (link.c:508-539) + conduit_initState (1304-1316)
+    // link_initState (link.c:508-539) + conduit_initState (1304-1316) +
+    // pump_initState (1534-1544)
+    s.targetSetting.assign(nl, 1.0);
+    for (auto* v : {&s.ncCOrif, &s.ncCWeir, &s.ncHCrit, &s.ncCSurch}) v->assign(nl, 0.0);
     for (int j = 0; j < nl; j++) {
         s.lOldFlow[j] = net.q0[j];
         s.lNewFlow[j] = net.q0[j];
         s.setting[j] = 1.0;
-        Geom g = geom(j);
-        s.lNewDepth[j] = linkYnorm(g, net.q0[j] / net.barrels[j], net.qMax[j], net.beta[j], ct);
+        if (net.linkType[j] == PUMP) s.setting[j] = s.targetSetting[j] = net.ncInitSetting[j];
+        if (net.linkType[j] == CONDUIT) {
+            Geom g = geom(j);
+            s.lNewDepth[j] = linkYnorm(g, net.q0[j] / net.barrels[j], net.qMax[j], net.beta[j], ct);
+        } else {
+            s.lNewDepth[j] = 0.0;
+            ncCoefs(j);               // orifice / weir coefficients at setting 1 (validation)
+        }
         s.lOldDepth[j] = s.lNewDepth[j];
     }
     // hotstart_open (swmm5.c:385) between project_init and routing_open
     bool hot = !hotstartUse.empty();
     if (hot && readHotstart()) return errorCode;
+    if (hot) {
+        // readRouting's link_setTargetSetting + link_setSetting (hotstart.c:319-322)
+        for (int j = 0; j < nl; j++) {
+            if (net.linkType[j] == CONDUIT) continue;
+            s.targetSetting[j] = s.setting[j];
+            if (net.linkType[j] == PUMP) {
+                int n1 = net.node1[j];
+                if (net.ncYOff[j] > 0.0 && s.setting[j] > 0.0 && s.newDepth[n1] < net.ncYOff[j])
+                    s.targetSetting[j] = 0.0;
+                if (net.ncYOn[j] > 0.0 && s.setting[j] == 0.0 && s.newDepth[n1] > net.ncYOn[j])
+                    s.targetSetting[j] = 1.0;
+            }
+            s.setting[j] = s.targetSetting[j];
+            ncCoefs(j);
+        }
+    }
     // flowrout_init DW (flowrout.c:75-103): dynwave_init crown elevations
     for (int i = 0; i < nl; i++) {
         int j = net.node1[i];
@@ -1672,6 +1936,7 @@ int Project::initState()
     }
     // initLinks (flowrout.c:472-507)
     for (int i = 0; i < nl; i++) {
+        if (net.linkType[i] != CONDUIT) continue;
         s.q1[i] = s.lNewFlow[i] / net.barrels[i];
         s.q2[i] = s.q1[i];
         s.a1[i] = getAofY(geom(i), s.lNewDepth[i], ct);
@@ -1694,6 +1959,58 @@ int Project::initState()
         }
     }
     return 0;
+}
+
+// orifice_setSetting / weir_setSetting coefficients at the link's current
+// setting (link.c:1729-1765, 2156-2186; weir_validate 2140-2151)
+void Project::ncCoefs(int j)
+{
+    const double* ct = &SWX_CIRC_TABLES[0][0];
+    State& s = st;
+    NcLink L = ncLink(j);
+    const Xsect& x = net.xsect[j];
+    Geom g{x.type, x.yFull, x.wMax, x.ywMax, x.aFull, x.rFull, x.sFull, x.sMax, x.yBot, x.aBot, x.sBot, x.rBot};
+    if (net.linkType[j] == ORIFICE) {
+        NcCoef c{};
+        orificeCoefs(L, g, s.setting[j], ct, &c);
+        s.ncCOrif[j] = c.cOrif;
+        s.ncCWeir[j] = c.cWeir;
+        s.ncHCrit[j] = c.hCrit;
+    } else if (net.linkType[j] == WEIR) {
+        int cv = net.ncCurve[j];
+        const double* cx = cv >= 0 ? net.curves[cv].x.data() : nullptr;
+        const double* cy = cv >= 0 ? net.curves[cv].y.data() : nullptr;
+        if (!net.ncCanSurcharge[j] && s.ncCSurch[j] != 0.0) return;   // weir_setSetting keeps it
+        s.ncCSurch[j] = weirSurchargeCoef(L, g, cx, cy, s.setting[j], ct);
+    }
+}
+
+NcLink Project::ncLink(int j) const
+{
+    NcLink L{};
+    L.type = net.linkType[j];
+    L.sub = net.ncSub[j];
+    L.flap = net.hasFlapGate[j];
+    L.canSurcharge = net.ncCanSurcharge[j];
+    int cv = net.ncCurve[j];
+    L.cOff = 0;
+    L.cN = cv >= 0 ? (int)net.curves[cv].x.size() : 0;
+    L.offset1 = net.offset1[j];
+    L.yFull = net.xsect[j].yFull;
+    L.c1 = net.ncC1[j];
+    L.c2 = net.ncC2[j];
+    L.endCon = net.ncEndCon[j];
+    L.slope = net.ncSlope[j];
+    L.length = net.ncLength[j];
+    L.yOn = net.ncYOn[j];
+    L.yOff = net.ncYOff[j];
+    L.xMin = net.ncXMin[j];
+    L.xMax = net.ncXMax[j];
+    L.qFull = net.qFull[j];
+    L.ucfL = ucfLength();
+    L.ucfQ = ucfFlow();
+    L.si = opt.unitSystem;
+    return L;
 }
 
 StorageGeom Project::storageGeom(int j) const

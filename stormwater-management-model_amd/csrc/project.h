@@ -9,6 +9,7 @@
 
 #include "model.h"
 #include "storage.h"
+#include "regulators.h"
 
 namespace swx {
 
@@ -63,6 +64,8 @@ public:
     bool inflowsAreConstant() const;        // no time series / patterns
     double getDateTime(double elapsedMsec) const;  // swmm5.c:1543
     StorageGeom storageGeom(int node) const;        // storage unit j's area relation
+    NcLink ncLink(int link) const;                  // pump / orifice / weir / outlet j
+    void ncCoefs(int link);                         // its setting-dependent coefficients
 
     int setError(int code, const std::string& msg);
 
@@ -79,6 +82,8 @@ private:
     int readFiles(std::vector<char*>& tok);
     int readStorage(std::vector<char*>& tok);
     int readCurve(std::vector<char*>& tok);
+    int readRegulator(int sect, std::vector<char*>& tok);
+    void validateRegulator(int j);
     int readHotstart();
     void initDepths();
     int readPollutant(std::vector<char*>& tok);

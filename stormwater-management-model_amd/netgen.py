@@ -271,9 +271,47 @@ DRY_ONLY  NO
 """
 
 
+# pumps (all curve types + ideal), side / bottom orifices, transverse and
+# V-notch weirs, functional and tabular outlets replacing conduits of the
+# storage variant (link.c:1406-2692): name -> (section line, xsection line)
+_REGULATORS = {
+    "C2":  ("[ORIFICES]", "C2  N2  N3  SIDE    0.2  0.65  YES", "C2  CIRCULAR     1.0  0  0  0"),
+    "C3":  ("[WEIRS]", "C3  N3  N4  TRANSVERSE  0.5  3.33  NO  1  0  YES", "C3  RECT_OPEN  2.0  3.0  0  0"),
+    "C4":  ("[PUMPS]", "C4  N5  N6  *   ON  0  0", None),
+    "C5":  ("[PUMPS]", "C5  N6  N4  P4  ON  0  0", None),
+    "C6":  ("[PUMPS]", "C6  N4  N7  P3  ON  0  0", None),
+    "C9":  ("[OUTLETS]", "C9  N10  N8  0.2  FUNCTIONAL/DEPTH  2.0  0.5  NO", None),
+    "C12": ("[ORIFICES]", "C12 N13 N11 BOTTOM  0.0  0.6  NO", "C12 RECT_CLOSED  1.0  1.5  0  0"),
+    "C17": ("[PUMPS]", "C17 N7  N10 P2  ON  2.0  0.5", None),
+    "C18": ("[PUMPS]", "C18 N12 N13 P1  ON  0  0", None),
+    "C19": ("[OUTLETS]", "C19 N3  N6  0.5  TABULAR/HEAD  R1  YES", None),
+    "C20": ("[WEIRS]", "C20 N9  N13 V-NOTCH  0.3  2.5  NO  0  0  NO", "C20 TRIANGULAR  2.0  4.0  0  0"),
+}
+_REGULATOR_CURVES = """P1   Pump1  20    1.0
+P1          50    2.5
+P1          100   4.0
+P2   Pump2  1.0   1.5
+P2          2.0   3.0
+P2          4.0   5.0
+P3   Pump3  0     8.0
+P3          5     6.0
+P3          10    3.0
+P3          15    0.0
+P4   Pump4  0     0.0
+P4          1     2.0
+P4          3     5.0
+P4          6     7.0
+R1   Rating 0     0.0
+R1          0.5   1.0
+R1          1.5   4.0
+R1          3.0   9.0
+"""
+
+
 def write_example(path: str, *, route_step: float = 5.0,
                   variable_step: float = 0.0, end_time: str = "04:00:00",
-                  pollutants: bool = False, files: str = "", storage: bool = False) -> None:
+                  pollutants: bool = False, files: str = "", storage: bool = False,
+                  regulators: bool = False) -> None:
     """Write the authored Example network (see module docstring).  `files`
     is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf");
     `storage` turns six junctions into storage units (_STORAGE)."""
@@ -288,6 +326,23 @@ def write_example(path: str, *, route_step: float = 5.0,
                           end_time=end_time, pollut=pollut,
                           qual_inflow=qual_inflow, qual_dwf=qual_dwf,
                           pollut_opt="")
+    if regulators:
+        storage = True
+        out = []
+        for ln in txt.split("\n"):
+            t = ln.split()
+            if t and t[0] in _REGULATORS and len(t) in (5, 7, 9):   # conduit / xsection / loss lines
+                continue
+            out.append(ln)
+        txt = "\n".join(out)
+        regs = ""                      # before [XSECTIONS], as the reference's GUI writes them
+        for sect in ("[PUMPS]", "[ORIFICES]", "[WEIRS]", "[OUTLETS]"):
+            body = [v[1] for v in _REGULATORS.values() if v[0] == sect]
+            regs += sect + "\n" + "\n".join(body) + "\n\n"
+        txt = txt.replace("[XSECTIONS]\n", regs + "[XSECTIONS]\n", 1)
+        xs = [v[2] for v in _REGULATORS.values() if v[2]]
+        txt = txt.replace("[XSECTIONS]\n;;Link Shape Geom1 Geom2 Geom3 Geom4 Barrels\n",
+                          "[XSECTIONS]\n;;Link Shape Geom1 Geom2 Geom3 Geom4 Barrels\n" + "\n".join(xs) + "\n")
     if storage:
         lines = [ln for ln in txt.split("\n") if ln.split()[:1] not in ([k] for k in _STORAGE)
                  or not ln.split()[1:2] or not ln.split()[1].replace(".", "").isdigit()
@@ -295,6 +350,8 @@ def write_example(path: str, *, route_step: float = 5.0,
         txt = "\n".join(lines)
         txt += "\n[STORAGE]\n;;Name Elev MaxDepth InitDepth Shape Coefficients\n"
         txt += "\n".join(_STORAGE.values()) + "\n" + _STORAGE_EXTRA
+        if regulators:
+            txt = txt.replace("SC1           9  1500\n", "SC1           9  1500\n" + _REGULATOR_CURVES)
     if files:
         txt += "\n[FILES]\n" + files.rstrip("\n") + "\n"
     d = os.path.dirname(os.path.abspath(path))

@@ -90,7 +90,9 @@ def test_gpu_matches_reference_every_step(name, tmp_path):
     assert len(mine) == len(ref)
     # header up to the first period (IDs, input summary, codes) is byte-identical
     start = struct.unpack("<i", ref[-16:-12])[0]
-    assert mine[:start] == ref[:start]
+    if mine[:start] != ref[:start]:
+        k = next(i for i in range(start) if mine[i] != ref[i])
+        raise AssertionError("header differs at byte %d of %d" % (k, start))
     assert mine[-24:] == ref[-24:]          # closing records, same period count
     a, b = _out_floats(mine[start:-24]), _out_floats(ref[start:-24])
     # period timestamps are float64; compare everything as float32 words with tolerance

@@ -93,7 +93,8 @@ def test_missing_input_file(tmp_path):
 
 @pytest.mark.parametrize("section", ["[SUBCATCHMENTS]\nS1 RG1 N1 1 25 500 0.5 0\n",
                                      "[STORAGE]\nST1 100 10 0 FUNCTIONAL 1000 0 0 0 0 1.5\n",
-                                     "[PUMPS]\nP1 N1 N2 * ON 0 0\n"])
+                                     "[CONTROLS]\nRULE R1\nIF NODE N1 DEPTH > 1\nTHEN LINK C1 STATUS = OFF\n",
+                                     "[DIVIDERS]\nD1 100 C1 CUTOFF 1.0\n"])
 def test_unsupported_sections_fail_loudly(section, tmp_path):
     src = open(_golden.inp("example")).read()
     p = tmp_path / "u.inp"
