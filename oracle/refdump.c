@@ -118,6 +118,18 @@ static double lsd_flowTurnSign(int j) { return (double)LinkStats[j].flowTurnSign
 static int StatClass = 0;
 static double lsd_timeInFlowClass(int j) { return LinkStats[j].timeInFlowClass[StatClass]; }
 extern TStorageStats* StorageStats;
+extern TPumpStats* PumpStats;
+#define PSD(nm, field) static double nm(int j) { return (Link[j].type == PUMP && PumpStats) ? (double)PumpStats[Link[j].subIndex].field : 0.0; }
+PSD(psd_utilized, utilized)
+PSD(psd_minFlow, minFlow)
+PSD(psd_avgFlow, avgFlow)
+PSD(psd_maxFlow, maxFlow)
+PSD(psd_volume, volume)
+PSD(psd_energy, energy)
+PSD(psd_offCurveLow, offCurveLow)
+PSD(psd_offCurveHigh, offCurveHigh)
+PSD(psd_startUps, startUps)
+PSD(psd_totalPeriods, totalPeriods)
 #define SSD(nm, field) static double nm(int j) { return (Node[j].type == STORAGE && StorageStats) ? StorageStats[Node[j].subIndex].field : 0.0; }
 SSD(ssd_initVol, initVol)
 SSD(ssd_avgVol, avgVol)
@@ -159,6 +171,16 @@ static void writeStats(void)
     ONE_N("st.node.maxOverflowDate", nsd_maxOverflowDate);
     ONE_N("st.node.maxPondedVol", nsd_maxPondedVol);
     ONE_N("st.node.nonConvergedCount", nsd_nonConvergedCount);
+    ONE_L("st.pump.utilized", psd_utilized);
+    ONE_L("st.pump.minFlow", psd_minFlow);
+    ONE_L("st.pump.avgFlow", psd_avgFlow);
+    ONE_L("st.pump.maxFlow", psd_maxFlow);
+    ONE_L("st.pump.volume", psd_volume);
+    ONE_L("st.pump.energy", psd_energy);
+    ONE_L("st.pump.offCurveLow", psd_offCurveLow);
+    ONE_L("st.pump.offCurveHigh", psd_offCurveHigh);
+    ONE_L("st.pump.startUps", psd_startUps);
+    ONE_L("st.pump.totalPeriods", psd_totalPeriods);
     ONE_N("st.storage.initVol", ssd_initVol);
     ONE_N("st.storage.avgVol", ssd_avgVol);
     ONE_N("st.storage.maxVol", ssd_maxVol);

@@ -746,6 +746,11 @@ long DLLEXPORT swmmx_getArray(const char* name, double* dst, long n)
         ARR("stat.storage.initVol", R.stInitVol) ARR("stat.storage.avgVol", R.stAvgVol)
         ARR("stat.storage.maxVol", R.stMaxVol) ARR("stat.storage.maxFlow", R.stMaxFlow)
         ARR("stat.storage.evapLosses", R.stEvapLoss) ARR("stat.storage.maxVolDate", R.stMaxVolDate)
+        ARR("stat.pump.utilized", R.pUtilized) ARR("stat.pump.minFlow", R.pMinFlow)
+        ARR("stat.pump.avgFlow", R.pAvgFlow) ARR("stat.pump.maxFlow", R.pMaxFlow)
+        ARR("stat.pump.volume", R.pVolume) ARR("stat.pump.energy", R.pEnergy)
+        ARR("stat.pump.offCurveLow", R.pOffLow) ARR("stat.pump.offCurveHigh", R.pOffHigh)
+        ARR("stat.pump.startUps", R.pStartUps) ARR("stat.pump.totalPeriods", R.pPeriods)
         ARR("stat.outfall.avgFlow", R.outfallAvgFlow) ARR("stat.outfall.maxFlow", R.outfallMaxFlow)
         ARR("stat.outfall.totalPeriods", R.outfallPeriods) ARR("stat.outfall.totalLoad", R.outfallLoad)
         ARR("stat.link.maxFlow", R.lMaxFlow) ARR("stat.link.maxFlowDate", R.lMaxFlowDate)

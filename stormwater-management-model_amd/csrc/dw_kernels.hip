@@ -3044,6 +3044,16 @@ int Router::downloadStats(Project& prj)
     HIPCHECK(link(R.lTimeInFlowClass, S.lTimeClass, RunStats::kClasses));
     HIPCHECK(link(R.lTimeCourantCritical, S.lTimeCourant, 1));
     HIPCHECK(linkI(R.lFlowTurns, S.lTurns));
+    HIPCHECK(link(R.pUtilized, p.pUtil, 1));
+    HIPCHECK(link(R.pMinFlow, p.pMin, 1));
+    HIPCHECK(link(R.pAvgFlow, p.pAvg, 1));
+    HIPCHECK(link(R.pMaxFlow, p.pMax, 1));
+    HIPCHECK(link(R.pVolume, p.pVol, 1));
+    HIPCHECK(link(R.pEnergy, p.pEnergy, 1));
+    HIPCHECK(link(R.pOffLow, p.pOffLow, 1));
+    HIPCHECK(link(R.pOffHigh, p.pOffHigh, 1));
+    HIPCHECK(linkI(R.pStartUps, p.pStarts));
+    HIPCHECK(linkI(R.pPeriods, p.pPeriods));
     HIPCHECK(linkI(R.lFlowTurnSign, S.lTurnSign));
     HIPCHECK(hipMemcpy(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost));
     const StepCtl* c = d->hostCtl;

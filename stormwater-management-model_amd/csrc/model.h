@@ -220,6 +220,9 @@ struct RunStats {
     std::vector<double> nodeInflowVol, nodeOutflowVol;           // NodeInflow / NodeOutflow
     // storage units (TStorageStats), node indexed; initVol = volume at stats_open
     std::vector<double> stInitVol, stAvgVol, stMaxVol, stMaxVolDate, stMaxFlow, stEvapLoss;
+    // pumps (TPumpStats), link indexed
+    std::vector<double> pUtilized, pMinFlow, pAvgFlow, pMaxFlow, pVolume, pEnergy, pOffLow, pOffHigh,
+        pStartUps, pPeriods;
     std::vector<double> outfallAvgFlow, outfallMaxFlow, outfallPeriods, outfallLoad;   // load [p][node]
     std::vector<double> lMaxFlow, lMaxFlowDate, lMaxVeloc, lMaxDepth, lTimeNormalFlow,
         lTimeSurcharged, lTimeFullUpstream, lTimeFullDnstream, lTimeFullFlow, lTimeCapacityLimited,

@@ -5,6 +5,7 @@
 // and statsrpt_writeReport (statsrpt.c:87-865).  Each line is written as
 // "\n  <text>", the reference's report_writeLine convention.
 #include "report.h"
+#include "regulators.h"
 
 #include <cmath>
 #include <cstdarg>
@@ -420,12 +421,23 @@ void writeRunReport(FILE* f, Project& prj, const ReportTotals& tot, long long no
             elapsed(R.lMaxFlowDate[j], rptStart, &d, &h, &m);
             w.printf(flowFmt, R.lMaxFlow[j] * ucfQ);
             w.printf("  %4d  %02d:%02d", d, h, m);
-            if (net.xsect[j].type == X_DUMMY) continue;
-            double v = R.lMaxVeloc[j] * ucfL;
-            if (v > 50.0) w.printf("    >50.00");
-            else w.printf("   %7.2f", v);
-            w.printf("  %6.2f", R.lMaxFlow[j] / net.qFull[j] / (double)net.barrels[j]);
+            int lt = net.linkType[j];
+            if (lt == PUMP && net.qFull[j] > 0.0) {     // max flow / pump capacity
+                w.printf("          ");
+                w.printf("  %6.2f", R.lMaxFlow[j] / net.qFull[j]);
+                continue;
+            }
+            if (net.xsect[j].type == X_DUMMY || lt == OUTLET) continue;
+            if (lt == CONDUIT) {
+                double v = R.lMaxVeloc[j] * ucfL;
+                if (v > 50.0) w.printf("    >50.00");
+                else w.printf("   %7.2f", v);
+                w.printf("  %6.2f", R.lMaxFlow[j] / net.qFull[j] / (double)net.barrels[j]);
+            } else {
+                w.printf("                  ");
+            }
             double full = net.xsect[j].yFull;
+            if (lt == ORIFICE && net.ncSub[j] == OR_BOTTOM) full = 0.0;
             if (full > 0.0) w.printf("  %6.2f", R.lMaxDepth[j] / full);
             else w.printf("        ");
         }
@@ -473,6 +485,34 @@ void writeRunReport(FILE* f, Project& prj, const ReportTotals& tot, long long no
             w.printf("    %8.2f  %8.2f  %8.2f  %8.2f     %8.2f", t[0], t[1], t[2], t[3], t[4]);
         }
         if (n == 0) w.line("No conduits were surcharged.");
+        w.blank();
+    }
+
+    // Pumping Summary (writePumpFlows, statsrpt.c)
+    if (net.nPumps > 0) {
+        w.title("Pumping Summary");
+        w.blank();
+        w.printf("\n  ---------------------------------------------------------------------------------------------------------"
+                 "\n                                                  Min       Avg       Max     Total     Power    %% Time Off"
+                 "\n                        Percent   Number of      Flow      Flow      Flow    Volume     Usage    Pump Curve"
+                 "\n  Pump                 Utilized   Start-Ups       %3s       %3s       %3s  %8s     Kw-hr    Low   High"
+                 "\n  ---------------------------------------------------------------------------------------------------------",
+                 kFlowWords[o.flowUnits], kFlowWords[o.flowUnits], kFlowWords[o.flowUnits], kVolWords[us]);
+        for (int j = 0; j < nL; j++) {
+            if (net.linkType[j] != PUMP) continue;
+            w.printf("\n  %-20s", net.linkId[j].c_str());
+            double pctUtil = R.pUtilized[j] / R.routingTimeSpan * 100.0;
+            double avg = R.pAvgFlow[j];
+            if (R.pPeriods[j] > 0) avg /= R.pPeriods[j];
+            w.printf(" %8.2f  %10d %9.2f %9.2f %9.2f %9.3f %9.2f", pctUtil, (int)R.pStartUps[j],
+                     R.pMinFlow[j] * ucfQ, avg * ucfQ, R.pMaxFlow[j] * ucfQ, R.pVolume[j] * vcf, R.pEnergy[j]);
+            double c1 = R.pOffLow[j], c2 = R.pOffHigh[j];
+            if (R.pUtilized[j] > 0.0) {
+                c1 = c1 / R.pUtilized[j] * 100.0;
+                c2 = c2 / R.pUtilized[j] * 100.0;
+            }
+            w.printf(" %6.1f %6.1f", c1, c2);
+        }
         w.blank();
     }
 }

@@ -284,7 +284,7 @@ _REGULATORS = {
     "C12": ("[ORIFICES]", "C12 N13 N11 BOTTOM  0.0  0.6  NO", "C12 RECT_CLOSED  1.0  1.5  0  0"),
     "C17": ("[PUMPS]", "C17 N7  N10 P2  ON  2.0  0.5", None),
     "C18": ("[PUMPS]", "C18 N12 N13 P1  ON  0  0", None),
-    "C19": ("[OUTLETS]", "C19 N3  N6  0.5  TABULAR/HEAD  R1  YES", None),
+    "C19": ("[OUTLETS]", "C19 N3  N6  0.5  TABULAR/DEPTH  R1  YES", None),
     "C20": ("[WEIRS]", "C20 N9  N13 V-NOTCH  0.3  2.5  NO  0  0  NO", "C20 TRIANGULAR  2.0  4.0  0  0"),
 }
 _REGULATOR_CURVES = """P1   Pump1  20    1.0

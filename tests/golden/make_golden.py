@@ -62,6 +62,9 @@ CASES = {
     # pumps of every curve type, orifices, weirs, outlets (link.c:1406-2692)
     "example_regulators": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0,
                                                       regulators=True), 1),
+    "example_regulators_var_qual": (netgen.write_example, dict(end_time="01:30:00", route_step=10.0,
+                                                               variable_step=0.75, regulators=True,
+                                                               pollutants=True), 1),
     # swmm_setValue between steps: external inflow, outfall stage, routing step
     "example_api": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
                                                variable_step=0.75), 1),
