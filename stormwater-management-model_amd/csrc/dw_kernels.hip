@@ -808,6 +808,7 @@ __device__ __attribute__((noinline)) double devStorageLosses(const Params& p, in
 
 // setNodeDepth (dynwave.c:636-762) for node i given its summed inflow,
 // outflow, surface area and dq/dh; returns 1 when converged (dynwave.c:615-621)
+template <bool kStorage = true>
 __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_t nf, double dt,
                                           double yLast, double yOld, double inflow, double outflow,
                                           double surf, double sumdqdh)
@@ -821,7 +822,7 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
     double surfArea = gmax(surf, p.minSurfArea);
     double dQ = inflow - outflow;
     double dV = 0.5 * (p.oldNetInflow[i] + dQ) * dt;
-    const bool isStorage = (int)(nf & NF_TYPE) == STORAGE;
+    const bool isStorage = kStorage && (int)(nf & NF_TYPE) == STORAGE;
     bool isSurcharged = false;
     if (p.surchargeMethod == SUR_EXTRAN) {
         if (isPonded) isSurcharged = false;
@@ -873,7 +874,7 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
         }
         if (overflow < 0.0001) overflow = 0.0;
         p.nNewVolume[i] = newVolume;
-    } else if (isStorage) {
+    } else if (kStorage && isStorage) {
         p.nNewVolume[i] = devStorageVolume(p, i, yNew);
     } else {
         p.nNewVolume[i] = (fullDepth > 0.0) ? fullVolume * (yNew / fullDepth) : 0.0;
@@ -885,7 +886,11 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
     return c;
 }
 
-template <bool kFirst>
+// kStorage: the network has storage units.  Their area relations are out-of-
+// line calls whose stack frames would give every node update a large scratch
+// segment (and throttle its waves), so networks without them use a call-free
+// node update.
+template <bool kFirst, bool kStorage>
 __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
 {
     if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
@@ -968,7 +973,7 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
             p.oldLat[i] = p.newLat[i];
             lat = p.latIn[i];
             p.newLat[i] = lat;
-            if (type == STORAGE) {       // addSystemInflows: node_getLosses (routing.c:363-365)
+            if (kStorage && type == STORAGE) {       // addSystemInflows: node_getLosses (routing.c:363-365)
                 double ev = 0.0;
                 p.nLosses[i] = devStorageLosses(p, i, yOld, p.nOldVolume[i], p.ctl->dt, &ev);
                 p.nEvapVol[i] = ev;
@@ -993,7 +998,7 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
             if (canPond && yLast > fullDepth && !(nf & NF_REPLICA)) surf = p.pondedArea[i];  // owner adds it
             inflow = 0.0;
             outflow = 0.0;                        // node losses are 0 for non-storage nodes
-            if (type == STORAGE && !(nf & NF_REPLICA)) {
+            if (kStorage && type == STORAGE && !(nf & NF_REPLICA)) {
                 surf = devStorageArea(p, i, yLast);
                 outflow = p.nLosses[i];
             }
@@ -1045,7 +1050,7 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
             p.xsend[s4 + 2] = surf;
             p.xsend[s4 + 3] = sumdqdh;
             listMe = false;                                // k_node_shared lists it
-        } else if (!nodeUpdate(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh)) {
+        } else if (!nodeUpdate<kStorage>(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh)) {
             anyUnconv = true;
             listMe = true;
         }
@@ -1075,6 +1080,7 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
 // Multi-GPU: shared nodes after the all-reduce of their partial sums.  Every
 // replica applies the same update to the same sums (identical results on all
 // ranks), and an unconverged interior node on any rank marks the iteration.
+template <bool kStorage>
 __global__ __launch_bounds__(kBlock) void k_node_shared(Params p, int k)
 {
     if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
@@ -1091,7 +1097,7 @@ __global__ __launch_bounds__(kBlock) void k_node_shared(Params p, int k)
         if ((int)(nf & NF_TYPE) == OUTFALL) continue;
         double yLast = p.nNewDepth[i], yOld = p.nOldDepth[i];
         bool listMe = false;
-        if (!nodeUpdate(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh)) {
+        if (!nodeUpdate<kStorage>(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh)) {
             anyUnconv = true;
             listMe = true;
         }
@@ -1884,6 +1890,7 @@ struct Router::Impl {
     int gridL = 1, gridN = 1, gridEnd = 1, gridC = 1;
     int linkWaves = kLinkWavesDefault;
     bool fastLinks = false;          // all streaming conduits circular, no SLOT
+    bool hasStorage = false;         // storage units present (k_node with storage calls)
     std::vector<void*> allocs;
     double* latBase = nullptr;       // constant lateral inflows
     double* qualBase = nullptr;
@@ -1975,6 +1982,11 @@ static LinkKernelFn linkKernel(bool first, int waves, bool fast)
 {
     return fast ? linkKernelT<true>(first, waves) : linkKernelT<false>(first, waves);
 }
+static LinkKernelFn nodeKernel(bool first, bool storage)
+{
+    if (storage) return first ? k_node<true, true> : k_node<false, true>;
+    return first ? k_node<true, false> : k_node<false, false>;
+}
 
 // One Picard iteration k.  Conduits with an invert offset (k_link_cold) run on
 // a side stream, concurrently with the streaming kernel, and are joined before
@@ -2015,14 +2027,11 @@ static void launchIteration(Router::Impl* d, int k)
     if (d->timing) (void)hipEventRecord(d->curHot[k], d->stream);
     if (p.nCold) (void)hipStreamWaitEvent(d->stream, d->joinEv[k], 0);
     if (d->timing) (void)hipEventRecord(d->curEv[4 * k + 1], d->stream);
-    if (k == 0) {
-        hipLaunchKernelGGL(k_node<true>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
-    } else {
-        hipLaunchKernelGGL(k_node<false>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
-    }
+    hipLaunchKernelGGL(nodeKernel(k == 0, d->hasStorage), dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
     if (d->part.active()) {                        // interface sums + convergence flag
         exchange(d, p.xsend, p.xrecv, (size_t)p.xflag + 1, 0);
-        hipLaunchKernelGGL(k_node_shared, dim3(d->gridS), dim3(kBlock), 0, d->stream, p, k);
+        hipLaunchKernelGGL(d->hasStorage ? k_node_shared<true> : k_node_shared<false>, dim3(d->gridS),
+                           dim3(kBlock), 0, d->stream, p, k);
     }
     if (p.nNC > 0) {                               // pumps / regulators, their end nodes
         if (k == 0) hipLaunchKernelGGL(k_nc<true>, dim3(1), dim3(kBlock), 0, d->stream, p, k);
@@ -2498,6 +2507,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         UPD(tmp, t, t.size()); p.gTables = tmp;
     }
     if (const char* w = getenv("SWMM5_LINK_WAVES")) d->linkWaves = atoi(w);
+    d->hasStorage = prj.net.nStorage > 0;
     {
         bool fast = prj.opt.surchargeMethod != SUR_SLOT;
         for (int j = 0; j < nL && fast; j++)
@@ -2517,7 +2527,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         return std::max(1, std::min((n + kBlock - 1) / kBlock, std::max(cap, 1)));
     };
     d->gridL = resident((const void*)linkKernel(false, d->linkWaves, d->fastLinks), nL);
-    d->gridN = resident((const void*)k_node<false>, nN);
+    d->gridN = resident((const void*)nodeKernel(false, d->hasStorage), nN);
     d->gridC = std::max(1, std::min((p.nCold + kBlock - 1) / kBlock, maxBlocks));
     d->gridEnd = resident(d->fastLinks ? (const void*)k_step_end<true> : (const void*)k_step_end<false>,
                           std::max(nN, nL));
@@ -3186,7 +3196,7 @@ int Router::timeKernel(int which, int reps, double* avgUs)
             hipLaunchKernelGGL(linkKernel(true, d->linkWaves, d->fastLinks), dim3(d->gridL), dim3(kBlock), 0,
                                d->stream, p, 0);
         else
-            hipLaunchKernelGGL(k_node<true>, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, 0);
+            hipLaunchKernelGGL(nodeKernel(true, d->hasStorage), dim3(d->gridN), dim3(kBlock), 0, d->stream, p, 0);
     }
     HIPCHECK(hipEventRecord(b, d->stream));
     HIPCHECK(hipEventSynchronize(b));
