@@ -149,6 +149,7 @@ struct Params {
     int nN, nL, P, maxTrials;
     // options
     int surchargeMethod, inertDamping, normalFlowLtd, allowPonding, varStep;
+    int forceMainEqn;             // FM_H_W or FM_D_W (FORCE_MAIN_EQUATION)
     double crownCutoff, minSurfArea, headTol, evapRate, courantFactor, minRouteStep, routeStep;
     // link static
     const int2* lnodes;
@@ -213,6 +214,7 @@ struct Params {
     const double* kDecay;
     // misc
     const double* gTables;        // global copy of the 5x51 circular tables
+    const double* gShapeTab;      // SWX_SHAPE_TAB: tabulated shapes' geometry
     double* partials;             // [nBlocksEnd][kNumPartials]
     int nBlocksEnd;
     StatsDev st;
@@ -258,6 +260,10 @@ __device__ __forceinline__ Geom loadGeom(const Params& p, int j, uint32_t f)
     } else {
         g.yBot = g.aBot = g.sBot = g.rBot = 0.0;
     }
+    if (!kFast && !isBasicShape(g.type)) {
+        int off = shapeTabOffset(g.type);
+        g.tb = (off >= 0) ? p.gShapeTab + off : nullptr;
+    }
     return g;
 }
 
@@ -272,27 +278,31 @@ __device__ __forceinline__ double slotWidth(const Params& p, const Geom& x, doub
     return x.wMax * 0.5423 * exp(-pow(yNorm, 2.4));
 }
 // dwflow.c:592-605
-template <bool kFast = false>
+// kAll: every shape (cold conduits); streaming conduits are basic shapes
+template <bool kFast = false, bool kAll = false>
 __device__ __forceinline__ double widthAt(const Params& p, const Geom& x, double y, const double* ct)
 {
     double wSlot = slotWidth<kFast>(p, x, y);
     if (wSlot > 0.0) return wSlot;
     if (y / x.yFull >= p.crownCutoff && !isOpen(x.type)) y = p.crownCutoff * x.yFull;
-    return getWofY(x, y, ct);
+    return getWofY<kAll>(x, y, ct);
 }
 // dwflow.c:609-619, 623-633
+template <bool kAll = false>
 __device__ __forceinline__ double areaAt(const Geom& x, double y, double wSlot, const double* ct)
 {
     if (y >= x.yFull) return x.aFull + (y - x.yFull) * wSlot;
-    return getAofY(x, y, ct);
+    return getAofY<kAll>(x, y, ct);
 }
+template <bool kAll = false>
 __device__ __forceinline__ double hydRadAt(const Geom& x, double y, const double* ct)
 {
     if (y >= x.yFull) return x.rFull;
-    return getRofY(x, y, ct);
+    return getRofY<kAll>(x, y, ct);
 }
 
 // link.c:1334-1399 (DW branch); returns total loss rate, sets evap/seep
+template <bool kAll>
 __device__ double conduitLossRate(const Params& p, int j, const Geom& x, double tstep,
                                   double* evapOut, double* seepOut, const double* ct)
 {
@@ -301,7 +311,7 @@ __device__ double conduitLossRate(const Params& p, int j, const Geom& x, double 
     if (depth > 0.0001) {
         double len = p.length[j];
         if (isOpen(x.type) && p.evapRate > 0.0) {
-            double topWidth = getWofY(x, depth, ct);
+            double topWidth = getWofY<kAll>(x, depth, ct);
             evapLossRate = topWidth * len * p.evapRate;
         }
         double sr = p.seepRate[j];
@@ -310,7 +320,7 @@ __device__ double conduitLossRate(const Params& p, int j, const Geom& x, double 
             if (x.type == G_RECT_CLOSED) width = x.wMax;
             else {
                 if (depth >= x.ywMax) depth = x.ywMax;
-                width = getWofY(x, depth, ct);
+                width = getWofY<kAll>(x, depth, ct);
             }
             seepLossRate = sr * width * len;
             seepLossRate *= 1.0;
@@ -475,9 +485,9 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         } else {
             dMid = 0.5 * (d1 + d2);
             if (dMid < 0.0001) dMid = 0.0001;
-            w1 = widthAt<kFast>(p, x, d1, ct);
-            w2 = widthAt<kFast>(p, x, d2, ct);
-            wMid = widthAt<kFast>(p, x, dMid, ct);
+            w1 = widthAt<kFast, kCold>(p, x, d1, ct);
+            w2 = widthAt<kFast, kCold>(p, x, d2, ct);
+            wMid = widthAt<kFast, kCold>(p, x, dMid, ct);
             switch (fc) {
             case F_SUBCRIT:                                  // dwflow.c:460-472
                 sa1 = (w1 + wMid) * length / 4.;
@@ -506,14 +516,14 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     p.sa2[j] = sa2;
 
     double wSlot = slotWidth<kFast>(p, x, y1);
-    double a1 = areaAt(x, y1, wSlot, ct);
-    double r1 = hydRadAt(x, y1, ct);
+    double a1 = areaAt<kCold>(x, y1, wSlot, ct);
+    double r1 = hydRadAt<kCold>(x, y1, ct);
     wSlot = slotWidth<kFast>(p, x, y2);
-    double a2 = areaAt(x, y2, wSlot, ct);
+    double a2 = areaAt<kCold>(x, y2, wSlot, ct);
     double yMid = 0.5 * (y1 + y2);
     wSlot = slotWidth<kFast>(p, x, yMid);
-    double aMid = areaAt(x, yMid, wSlot, ct);
-    double rMid = hydRadAt(x, yMid, ct);
+    double aMid = areaAt<kCold>(x, yMid, wSlot, ct);
+    double rMid = hydRadAt<kCold>(x, yMid, ct);
     bool isFull = (y1 >= x.yFull && y2 >= x.yFull);
     double len0 = p.length[j];
 
@@ -535,7 +545,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
 
     double v = qLast / aMid;
     if (fabs(v) > 50.) v = 50. * gsgn(qLast);
-    double froude = linkFroude(x, v, yMid, ct);
+    double froude = linkFroude<kCold>(x, v, yMid, ct);
     p.froude[j] = froude;
     if (fc == F_SUBCRIT && froude > 1.0) fc = F_SUPCRIT;
 
@@ -553,7 +563,10 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     else if (p.inertDamping == DAMP_FULL) sigma = 0.0;
     if (isFull && !isOpen(x.type)) sigma = 0.0;
 
-    double dq1 = dt * p.roughFactor[j] / pow(rWtd, 1.33333) * fabs(v);
+    double dq1;
+    if (kCold && x.type == G_FORCE_MAIN && isFull)              // dwflow.c:212-214
+        dq1 = dt * fmFricSlope(p.forceMainEqn, x, fabs(v), rMid);
+    else dq1 = dt * p.roughFactor[j] / pow(rWtd, 1.33333) * fabs(v);
     double dq2 = dt * 32.2 * aWtd * (h2 - h1) / length;
     double dq3 = 0.0, dq4 = 0.0;
     if (sigma > 0.0) {
@@ -572,7 +585,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     if (f & LF_SEEP) {
         if (!kFirst) oldDepth = p.lOldDepth[j];
         (void)oldDepth;
-        dq6 = conduitLossRate(p, j, x, dt, &evapRate, &seepRate, ct) * 2.5 * dt * v / len0;
+        dq6 = conduitLossRate<kCold>(p, j, x, dt, &evapRate, &seepRate, ct) * 2.5 * dt * v / len0;
     } else {
         dq6 = 0.0 * 2.5 * dt * v / len0;
     }
@@ -591,7 +604,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
                 if (y1 < y2) check = true;
             if (!check && (p.normalFlowLtd == NFL_FROUDE || p.normalFlowLtd == NFL_BOTH) && !hasOutfall) {
                 if (y1 > 0.0001 && y2 > 0.0001) {
-                    double f1 = linkFroude(x, q / a1, y1, ct);
+                    double f1 = linkFroude<kCold>(x, q / a1, y1, ct);
                     if (f1 >= 1.0) check = true;
                 }
             }
@@ -719,19 +732,18 @@ void k_link(Params p, int k)
     }
 }
 
-// link_setOutfallDepth + outfall_setOutletDepth (link.c:728-766, node.c:1413-1492)
 // link_setOutfallDepth + outfall_setOutletDepth (link.c:728-766, node.c:1413-1492),
 // in two halves that can run on different waves: the normal depth (kPart 0)
 // and the critical depth (kPart 1) of the outfall conduit's flow, then the
 // outlet depth from both (outfallCombine)
-template <int kPart>
+template <int kPart, bool kAll>
 __device__ __forceinline__ double outfallPart(const Params& p, int j, uint32_t f, const double* ct)
 {
     Geom x = loadGeom(p, j, f);
     double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
     double q = fabs(p.lNewFlow[j] / barrels);
-    if (kPart == 0) return linkYnorm(x, q, p.qMax[j], p.beta[j], ct);
-    return getYcrit(x, q, ct);
+    if (kPart == 0) return linkYnorm<kAll>(x, q, p.qMax[j], p.beta[j], ct);
+    return getYcrit<kAll>(x, q, ct);
 }
 __device__ __forceinline__ double outfallCombine(const Params& p, int i, uint32_t nf, int j,
                                                  double yNorm, double yCrit)
@@ -886,13 +898,14 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
     return c;
 }
 
-// kStorage: the network has storage units.  Their area relations are out-of-
-// line calls whose stack frames would give every node update a large scratch
-// segment (and throttle its waves), so networks without them use a call-free
-// node update.
-template <bool kFirst, bool kStorage>
+// kGeneral: the network has storage units or non-basic conduit shapes.  Their
+// area relations are out-of-line calls whose stack frames and registers would
+// give every node update a large scratch segment (and throttle its waves), so
+// the other networks use a node update without them.
+template <bool kFirst, bool kGeneral>
 __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
 {
+    constexpr bool kStorage = kGeneral;
     if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
     // prologue: outfall depths (link_setOutfallDepth, findNodeDepths
     // dynwave.c:605) from this iteration's link flows.  Only the outfall's
@@ -913,8 +926,8 @@ __global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
             int j = (c < p.nOutLinks) ? p.outLinks[c] : -1;
             uint32_t f = (j >= 0) ? p.lflags[j] : 0u;
             double yn = 0.0;                               // non-conduits: yNorm = yCrit = 0
-            if (j >= 0 && w == 0 && !(f & LF_NC)) yn = outfallPart<0>(p, j, f, ct);
-            if (j >= 0 && w == 1) yc[lane] = (f & LF_NC) ? 0.0 : outfallPart<1>(p, j, f, ct);
+            if (j >= 0 && w == 0 && !(f & LF_NC)) yn = outfallPart<0, kGeneral>(p, j, f, ct);
+            if (j >= 0 && w == 1) yc[lane] = (f & LF_NC) ? 0.0 : outfallPart<1, kGeneral>(p, j, f, ct);
             __syncthreads();
             if (j >= 0 && w == 0) {
                 int2 nn = p.lnodes[j];
@@ -1428,7 +1441,7 @@ __device__ __forceinline__ void combinePartials(double* a, const double* b)
 }
 
 // link_getVelocity (link.c:809-830) for a conduit
-template <bool kFast>
+template <bool kFast, bool kAll>
 __device__ __forceinline__ double conduitVelocity(const Params& p, int j, uint32_t f, double q, double depth,
                                                   const double* ct)
 {
@@ -1436,7 +1449,7 @@ __device__ __forceinline__ double conduitVelocity(const Params& p, int j, uint32
     double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
     q /= barrels;
     Geom x = loadGeom<kFast>(p, j, f);
-    double area = getAofY(x, depth, ct);
+    double area = getAofY<kAll>(x, depth, ct);
     return (area > 0.0001) ? q / area : 0.0;
 }
 
@@ -1445,7 +1458,7 @@ __device__ __forceinline__ double conduitVelocity(const Params& p, int j, uint32
 // (dynwave.c:836-921), run statistics (stats_updateFlowStats, stats.c:449-752)
 // and the per-node volume totals (massbal_updateRoutingTotals, massbal.c:619-633).
 // Block partials: see kNumPartials.
-template <bool kFast>
+template <bool kFast, bool kAll>
 __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
 {
     __shared__ double red[kNumPartials][kBlock / 64];
@@ -1542,8 +1555,8 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
             double q = fabs(newFlow);
             if (q > S.lMaxFlow[j]) { S.lMaxFlow[j] = q; S.lMaxFlowDate[j] = aDate; }
             double depth = p.lNewDepth[j];
-            double v = (f & LF_COLD) ? conduitVelocity<false>(p, j, f, q, depth, ct)
-                                     : conduitVelocity<kFast>(p, j, f, q, depth, ct);
+            double v = (f & LF_COLD) ? conduitVelocity<false, kAll>(p, j, f, q, depth, ct)
+                                     : conduitVelocity<kFast, false>(p, j, f, q, depth, ct);
             if (v > S.lMaxVeloc[j]) S.lMaxVeloc[j] = v;
             if (depth > S.lMaxDepth[j]) S.lMaxDepth[j] = depth;
             if (s & (1 << 8)) S.lTimeNormal[j] += dt;
@@ -1890,7 +1903,8 @@ struct Router::Impl {
     int gridL = 1, gridN = 1, gridEnd = 1, gridC = 1;
     int linkWaves = kLinkWavesDefault;
     bool fastLinks = false;          // all streaming conduits circular, no SLOT
-    bool hasStorage = false;         // storage units present (k_node with storage calls)
+    bool general = false;            // storage units or non-basic shapes (k_node/k_step_end<.., true>)
+    bool allShapes = false;          // non-basic conduit shapes present
     std::vector<void*> allocs;
     double* latBase = nullptr;       // constant lateral inflows
     double* qualBase = nullptr;
@@ -1982,6 +1996,12 @@ static LinkKernelFn linkKernel(bool first, int waves, bool fast)
 {
     return fast ? linkKernelT<true>(first, waves) : linkKernelT<false>(first, waves);
 }
+typedef void (*StepEndFn)(Params);
+static StepEndFn stepEndKernel(bool fast, bool all)
+{
+    if (fast) return all ? k_step_end<true, true> : k_step_end<true, false>;
+    return all ? k_step_end<false, true> : k_step_end<false, false>;
+}
 static LinkKernelFn nodeKernel(bool first, bool storage)
 {
     if (storage) return first ? k_node<true, true> : k_node<false, true>;
@@ -2027,10 +2047,10 @@ static void launchIteration(Router::Impl* d, int k)
     if (d->timing) (void)hipEventRecord(d->curHot[k], d->stream);
     if (p.nCold) (void)hipStreamWaitEvent(d->stream, d->joinEv[k], 0);
     if (d->timing) (void)hipEventRecord(d->curEv[4 * k + 1], d->stream);
-    hipLaunchKernelGGL(nodeKernel(k == 0, d->hasStorage), dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
+    hipLaunchKernelGGL(nodeKernel(k == 0, d->general), dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
     if (d->part.active()) {                        // interface sums + convergence flag
         exchange(d, p.xsend, p.xrecv, (size_t)p.xflag + 1, 0);
-        hipLaunchKernelGGL(d->hasStorage ? k_node_shared<true> : k_node_shared<false>, dim3(d->gridS),
+        hipLaunchKernelGGL(d->general ? k_node_shared<true> : k_node_shared<false>, dim3(d->gridS),
                            dim3(kBlock), 0, d->stream, p, k);
     }
     if (p.nNC > 0) {                               // pumps / regulators, their end nodes
@@ -2051,8 +2071,7 @@ static void launchStep(Router::Impl* d)
         hipLaunchKernelGGL(k_qual_link, dim3(d->gridL), dim3(kBlock), 0, d->stream, p);
     }
     if (d->timing) (void)hipEventRecord(d->curEv[base + 1], d->stream);
-    if (d->fastLinks) hipLaunchKernelGGL(k_step_end<true>, dim3(d->gridEnd), dim3(kBlock), 0, d->stream, p);
-    else hipLaunchKernelGGL(k_step_end<false>, dim3(d->gridEnd), dim3(kBlock), 0, d->stream, p);
+    hipLaunchKernelGGL(stepEndKernel(d->fastLinks, d->allShapes), dim3(d->gridEnd), dim3(kBlock), 0, d->stream, p);
     if (d->part.active() && p.varStep) {           // global Courant limits (min over ranks)
         hipLaunchKernelGGL(k_finalize<1>, dim3(1), dim3(kBlock), 0, d->stream, p);
         exchange(d, &p.ctl->stepRed[5], &p.ctl->stepRed[5], 2, 1);
@@ -2126,6 +2145,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     p.nN = nN; p.nL = nL; p.P = P;
     p.maxTrials = std::min(prj.opt.maxTrials, kMaxTrialsCap);
     p.surchargeMethod = prj.opt.surchargeMethod;
+    p.forceMainEqn = prj.opt.forceMainEqn;
     p.inertDamping = prj.opt.inertDamping;
     p.normalFlowLtd = prj.opt.normalFlowLtd;
     p.allowPonding = prj.opt.allowPonding;
@@ -2186,7 +2206,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (net.linkType[g] != CONDUIT) {
             f |= LF_NC | LF_COLD;                   // k_nc, not the conduit kernels
             if (net.linkType[g] == PUMP) f |= LF_PUMP;
-        } else if (net.offset1[g] > 0.0 || net.offset2[g] > 0.0) {
+        } else if (net.offset1[g] > 0.0 || net.offset2[g] > 0.0 || !isBasicShape(x.type)) {
             f |= LF_COLD;
             coldLinks.push_back(j);
         }
@@ -2505,9 +2525,13 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     {
         std::vector<double> t(&SWX_CIRC_TABLES[0][0], &SWX_CIRC_TABLES[0][0] + 5 * SWX_CIRC_N);
         UPD(tmp, t, t.size()); p.gTables = tmp;
+        std::vector<double> st(SWX_SHAPE_TAB, SWX_SHAPE_TAB + SWX_SHAPE_TAB_LEN);
+        UPD(tmp, st, st.size()); p.gShapeTab = tmp;
     }
     if (const char* w = getenv("SWMM5_LINK_WAVES")) d->linkWaves = atoi(w);
-    d->hasStorage = prj.net.nStorage > 0;
+    for (int j = 0; j < nL; j++)
+        if (!isBasicShape((int)(lflags[j] & LF_XTYPE))) d->allShapes = true;
+    d->general = prj.net.nStorage > 0 || d->allShapes;
     {
         bool fast = prj.opt.surchargeMethod != SUR_SLOT;
         for (int j = 0; j < nL && fast; j++)
@@ -2527,9 +2551,9 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         return std::max(1, std::min((n + kBlock - 1) / kBlock, std::max(cap, 1)));
     };
     d->gridL = resident((const void*)linkKernel(false, d->linkWaves, d->fastLinks), nL);
-    d->gridN = resident((const void*)nodeKernel(false, d->hasStorage), nN);
+    d->gridN = resident((const void*)nodeKernel(false, d->general), nN);
     d->gridC = std::max(1, std::min((p.nCold + kBlock - 1) / kBlock, maxBlocks));
-    d->gridEnd = resident(d->fastLinks ? (const void*)k_step_end<true> : (const void*)k_step_end<false>,
+    d->gridEnd = resident((const void*)stepEndKernel(d->fastLinks, d->allShapes),
                           std::max(nN, nL));
     p.nBlocksEnd = d->gridEnd;
     p.multi = part.active() ? 1 : 0;
@@ -3196,7 +3220,7 @@ int Router::timeKernel(int which, int reps, double* avgUs)
             hipLaunchKernelGGL(linkKernel(true, d->linkWaves, d->fastLinks), dim3(d->gridL), dim3(kBlock), 0,
                                d->stream, p, 0);
         else
-            hipLaunchKernelGGL(nodeKernel(true, d->hasStorage), dim3(d->gridN), dim3(kBlock), 0, d->stream, p, 0);
+            hipLaunchKernelGGL(nodeKernel(true, d->general), dim3(d->gridN), dim3(kBlock), 0, d->stream, p, 0);
     }
     HIPCHECK(hipEventRecord(b, d->stream));
     HIPCHECK(hipEventSynchronize(b));

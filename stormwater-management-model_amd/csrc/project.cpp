@@ -1016,11 +1016,13 @@ int Project::readRegulator(int sect, std::vector<char*>& tok)
     return 0;
 }
 
-// xsect.c:216-634 for the supported shapes
+// xsect_setParams (xsect.c:216-634)
 bool setXsectParams(Xsect& x, int type, double p[4], double ucf)
 {
+    const double* ct = &SWX_CIRC_TABLES[0][0];
     if (type != X_DUMMY && p[0] <= 0.0) return false;
     x.type = type;
+    auto g = [&]() { return geomOf(x); };
     switch (type) {
     case X_DUMMY:
         x.yFull = x.wMax = x.aFull = x.rFull = x.sFull = x.sMax = 1.E-6;
@@ -1034,6 +1036,55 @@ bool setXsectParams(Xsect& x, int type, double p[4], double ucf)
         x.sMax = 1.08 * x.sFull;
         x.ywMax = 0.5 * x.yFull;
         break;
+    case X_FORCE_MAIN:
+        x.yFull = p[0] / ucf;
+        x.wMax = x.yFull;
+        x.aFull = kPi / 4.0 * x.yFull * x.yFull;
+        x.rFull = 0.2500 * x.yFull;
+        x.sFull = x.aFull * pow(x.rFull, 0.63);
+        x.sMax = 1.06949 * x.sFull;
+        x.ywMax = 0.5 * x.yFull;
+        x.rBot = p[1];                        // C-factor or roughness height
+        break;
+    case X_FILLED_CIRCULAR: {
+        if (p[1] >= p[0]) return false;
+        x.yFull = p[0] / ucf;
+        x.wMax = x.yFull;
+        x.aFull = kPi / 4.0 * x.yFull * x.yFull;
+        x.rFull = 0.2500 * x.yFull;
+        x.yBot = p[1] / ucf;
+        x.aBot = x.aFull * lookup(x.yBot / x.yFull, SWX_TA(ct), SWX_CIRC_N);
+        x.sBot = getWofY(g(), x.yBot, ct);    // the filled-circle W(y), yFull still whole
+        x.rBot = x.aBot / (x.rFull * lookup(x.yBot / x.yFull, SWX_TR(ct), SWX_CIRC_N));
+        x.aFull -= x.aBot;
+        x.rFull = x.aFull / (kPi * x.yFull - x.rBot + x.sBot);
+        x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
+        x.sMax = 1.08 * x.sFull;
+        x.yFull -= x.yBot;
+        x.ywMax = 0.5 * x.yFull;
+        break;
+    }
+    case X_EGGSHAPED: case X_HORSESHOE: case X_GOTHIC: case X_CATENARY: case X_SEMIELLIPTICAL:
+    case X_BASKETHANDLE: case X_SEMICIRCULAR: {
+        // per shape: aFull/y^2, rFull/y, sMax/sFull, wMax/y, ywMax/y (xsect.c:295-363)
+        static const double k[7][5] = {
+            {0.5105, 0.1931, 1.065, 2. / 3., 0.64},       // EGGSHAPED
+            {0.8293, 0.2538, 1.077, 1.0, 0.5},            // HORSESHOE
+            {0.6554, 0.2269, 1.065, 0.84, 0.45},          // GOTHIC
+            {0.70277, 0.23172, 1.05, 0.9, 0.25},          // CATENARY
+            {0.785, 0.242, 1.045, 1.0, 0.15},             // SEMIELLIPTICAL
+            {0.7862, 0.2464, 1.06078, 0.944, 0.2},        // BASKETHANDLE
+            {1.2697, 0.2946, 1.06637, 1.64, 0.15}};       // SEMICIRCULAR
+        int i = (type == X_EGGSHAPED) ? 0 : (type == X_HORSESHOE) ? 1 : type - X_GOTHIC + 2;
+        x.yFull = p[0] / ucf;
+        x.aFull = k[i][0] * x.yFull * x.yFull;
+        x.rFull = k[i][1] * x.yFull;
+        x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
+        x.sMax = k[i][2] * x.sFull;
+        x.wMax = (i == 0 ? 2. / 3. : k[i][3]) * x.yFull;
+        x.ywMax = k[i][4] * x.yFull;
+        break;
+    }
     case X_RECT_CLOSED: {
         if (p[1] <= 0.0) return false;
         x.yFull = p[0] / ucf;
@@ -1042,9 +1093,7 @@ bool setXsectParams(Xsect& x, int type, double p[4], double ucf)
         x.rFull = x.aFull / (2.0 * (x.yFull + x.wMax));
         x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
         double aMax = 0.97 * x.aFull;
-        Geom g{x.type, x.yFull, x.wMax, x.ywMax, x.aFull, x.rFull, x.sFull, x.sMax,
-               x.yBot, x.aBot, x.sBot, x.rBot};
-        x.sMax = aMax * pow(rectClosedRofA(g, aMax), 2. / 3.);
+        x.sMax = aMax * pow(rectClosedRofA(g(), aMax), 2. / 3.);
         x.ywMax = x.yFull;
         break;
     }
@@ -1060,6 +1109,59 @@ bool setXsectParams(Xsect& x, int type, double p[4], double ucf)
         x.sMax = x.sFull;
         x.ywMax = x.yFull;
         break;
+    case X_RECT_TRIANG: {
+        if (p[1] <= 0.0 || p[2] <= 0.0) return false;
+        x.yFull = p[0] / ucf;
+        x.wMax = p[1] / ucf;
+        x.yBot = p[2] / ucf;
+        x.ywMax = x.yFull;
+        x.aBot = x.yBot * x.wMax / 2.0;
+        x.sBot = x.wMax / x.yBot / 2.0;
+        x.rBot = sqrt(1. + x.sBot * x.sBot);
+        x.aFull = x.wMax * (x.yFull - x.yBot / 2.0);
+        x.rFull = x.aFull / (2.0 * x.yBot * x.rBot + 2.0 * (x.yFull - x.yBot) + x.wMax);
+        x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
+        double aMax = SWX_RECT_TRIANG_ALFMAX * x.aFull;
+        x.sMax = aMax * pow(rectTriangRofA(g(), aMax), 2. / 3.);
+        break;
+    }
+    case X_RECT_ROUND: {
+        if (p[1] <= 0.0) return false;
+        if (p[2] < p[1] / 2.0) p[2] = p[1] / 2.0;
+        x.yFull = p[0] / ucf;
+        x.wMax = p[1] / ucf;
+        x.rBot = p[2] / ucf;
+        double theta = 2.0 * asin(x.wMax / 2.0 / x.rBot);
+        x.aBot = x.rBot * x.rBot / 2.0 * (theta - sin(theta));
+        x.sBot = kPi * x.rBot * x.rBot * pow(x.rBot / 2.0, 2. / 3.);
+        x.yBot = x.rBot * (1.0 - cos(theta / 2.0));
+        if (x.yBot > x.yFull) return false;
+        x.ywMax = x.yFull;
+        x.aFull = x.wMax * (x.yFull - x.yBot) + x.aBot;
+        x.rFull = x.aFull / (x.rBot * theta + 2.0 * (x.yFull - x.yBot) + x.wMax);
+        x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
+        double aMax = SWX_RECT_ROUND_ALFMAX * x.aFull;
+        x.sMax = aMax * pow(rectRoundRofA(g(), aMax, ct), 2. / 3.);
+        break;
+    }
+    case X_MOD_BASKET: {
+        if (p[1] <= 0.0) return false;
+        if (p[2] < p[1] / 2.0) p[2] = p[1] / 2.0;
+        x.yFull = p[0] / ucf;
+        x.wMax = p[1] / ucf;
+        x.rBot = p[2] / ucf;
+        double theta = 2.0 * asin(x.wMax / 2.0 / x.rBot);
+        x.sBot = theta;
+        x.yBot = x.rBot * (1.0 - cos(theta / 2.0));
+        if (x.yBot > x.yFull) return false;
+        x.ywMax = x.yFull - x.yBot;
+        x.aBot = x.rBot * x.rBot / 2.0 * (theta - sin(theta));
+        x.aFull = (x.yFull - x.yBot) * x.wMax + x.aBot;
+        x.rFull = x.aFull / (x.rBot * theta + 2.0 * (x.yFull - x.yBot) + x.wMax);
+        x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
+        x.sMax = getSofA(g(), amaxRatio(X_MOD_BASKET) * x.aFull, ct);
+        break;
+    }
     case X_TRAPEZOIDAL:
         if (p[1] < 0.0 || p[2] < 0.0 || p[3] < 0.0) return false;
         x.yFull = p[0] / ucf;
@@ -1086,6 +1188,79 @@ bool setXsectParams(Xsect& x, int type, double p[4], double ucf)
         x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
         x.sMax = x.sFull;
         break;
+    case X_PARABOLIC:
+        if (p[1] <= 0.0) return false;
+        x.yFull = p[0] / ucf;
+        x.wMax = p[1] / ucf;
+        x.ywMax = x.yFull;
+        x.rBot = x.wMax / 2.0 / sqrt(x.yFull);
+        x.aFull = (2. / 3.) * x.yFull * x.wMax;
+        x.rFull = getRofY(g(), x.yFull, ct);
+        x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
+        x.sMax = x.sFull;
+        break;
+    case X_POWERFUNC:
+        if (p[1] <= 0.0 || p[2] <= 0.0) return false;
+        x.yFull = p[0] / ucf;
+        x.wMax = p[1] / ucf;
+        x.ywMax = x.yFull;
+        x.sBot = 1.0 / p[2];
+        x.rBot = x.wMax / (x.sBot + 1) / pow(x.yFull, x.sBot);
+        x.aFull = x.yFull * x.wMax / (x.sBot + 1);
+        x.rFull = getRofY(g(), x.yFull, ct);
+        x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
+        x.sMax = x.sFull;
+        break;
+    case X_HORIZ_ELLIPSE:
+    case X_VERT_ELLIPSE: {
+        bool horiz = type == X_HORIZ_ELLIPSE;
+        if (p[1] == 0.0) p[2] = p[0];
+        if (p[2] > 0.0) {                        // standard size code
+            int i = (int)floor(p[2]) - 1;
+            if (i < 0 || i >= SWX_N_ELLIPSE_MINOR) return false;
+            double minor = SWX_ELLIPSE_MINOR[i] / 12., major = SWX_ELLIPSE_MAJOR[i] / 12.;
+            x.yFull = horiz ? minor : major;
+            x.wMax = horiz ? major : minor;
+            x.aFull = SWX_ELLIPSE_AFULL[i];
+            x.rFull = SWX_ELLIPSE_RFULL[i];
+        } else if (horiz) {
+            x.yFull = p[0] / ucf;
+            if (p[1] < 0.0) return false;
+            x.wMax = p[1] / ucf;
+            x.aFull = 1.2692 * x.yFull * x.yFull;
+            x.rFull = 0.3061 * x.yFull;
+        } else {
+            if (p[1] < 0.0) return false;
+            x.yFull = p[0] / ucf;
+            x.wMax = p[1] / ucf;
+            x.aFull = 1.2692 * x.wMax * x.wMax;
+            x.rFull = 0.3061 * x.wMax;
+        }
+        x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
+        x.sMax = x.sFull;
+        x.ywMax = 0.48 * x.yFull;
+        break;
+    }
+    case X_ARCH:
+        if (p[1] == 0.0) p[2] = p[0];
+        if (p[2] > 0.0) {
+            int i = (int)floor(p[2]) - 1;
+            if (i < 0 || i >= SWX_N_ARCH_YFULL) return false;
+            x.yFull = SWX_ARCH_YFULL[i] / 12.;
+            x.wMax = SWX_ARCH_WMAX[i] / 12.;
+            x.aFull = SWX_ARCH_AFULL[i];
+            x.rFull = SWX_ARCH_RFULL[i];
+        } else {
+            if (p[1] < 0.0) return false;
+            x.yFull = p[0] / ucf;
+            x.wMax = p[1] / ucf;
+            x.aFull = 0.7879 * x.yFull * x.wMax;
+            x.rFull = 0.2991 * x.yFull;
+        }
+        x.sFull = x.aFull * pow(x.rFull, 2. / 3.);
+        x.sMax = x.sFull;
+        x.ywMax = 0.28 * x.yFull;
+        break;
     default:
         return false;
     }
@@ -1103,8 +1278,7 @@ int Project::readXsect(std::vector<char*>& tok)  // link.c:162-267
     if (k < 0) return 205;
     if (net.linkType[j] == CONDUIT) net.barrels[j] = 1;
     net.xsect[j].culvertCode = 0;
-    if (!(k == X_CIRCULAR || k == X_RECT_CLOSED || k == X_RECT_OPEN || k == X_TRAPEZOIDAL ||
-          k == X_TRIANGULAR))
+    if (k == X_IRREGULAR || k == X_CUSTOM || k == X_STREET)
         return setError(200, std::string("ERROR 200: cross-section shape ") + tok[1] +
                                  " is not supported by the MI355X engine yet");
     if (nt < 6) return 203;
@@ -1537,9 +1711,17 @@ void Project::validateConduit(int j)  // link.c:992-1154 (supported shapes)
     if (net.length[j] <= 0.0) { setError(111, "ERROR 111: invalid length for Conduit " + net.linkId[j]); return; }
     if (net.roughness[j] <= 0.0) { setError(113, "ERROR 113: invalid roughness for Conduit " + net.linkId[j]); return; }
     if (net.barrels[j] <= 0) { setError(114, "ERROR 114: invalid number of barrels for Conduit " + net.linkId[j]); return; }
+    if (xs.type == X_FORCE_MAIN) {                     // link.c:1031-1037
+        if (opt.forceMainEqn == FM_D_W) xs.rBot /= (opt.unitSystem ? 304.8 : 12.0);
+        if (xs.rBot <= 0.0) { setError(119, "ERROR 119: invalid cross section for link " + net.linkId[j]); return; }
+    }
     if (xs.aFull <= 0.0) { setError(119, "ERROR 119: invalid cross section for link " + net.linkId[j]); return; }
     if (net.offset1[j] < 0.0) { warnings++; net.offset1[j] = 0.0; }
     if (net.offset2[j] < 0.0) { warnings++; net.offset2[j] = 0.0; }
+    if (xs.type == X_FILLED_CIRCULAR) {                // link.c:1069-1074
+        net.offset1[j] += xs.yBot;
+        net.offset2[j] += xs.yBot;
+    }
     double slope = conduitSlope(net, j, opt, &warnings);
     net.slope[j] = slope;
     if (slope < 0.0 && xs.type != X_DUMMY) {           // conduit_reverse link.c:1158-1191
@@ -1551,10 +1733,17 @@ void Project::validateConduit(int j)  // link.c:992-1154 (supported shapes)
         net.q0[j] = -net.q0[j];
     }
     double roughness = net.roughness[j];
+    if (xs.type == X_FORCE_MAIN) {                     // forcemain_getEquivN forcmain.c:30-47
+        double d = xs.yFull;
+        if (opt.forceMainEqn == FM_H_W) roughness = 1.067 / xs.rBot * pow(d / net.slope[j], 0.04);
+        else {
+            double f = fmFricFactor(xs.rBot, d / 4.0, 1.0e12);
+            roughness = sqrt(f / 185.0) * pow(d, (1. / 6.));
+        }
+    }
     double lengthFactor = 1.0;
     if (opt.lengtheningStep > 0.0 && xs.type != X_DUMMY) {   // link.c:1217-1254
-        Geom g{xs.type, xs.yFull, xs.wMax, xs.ywMax, xs.aFull, xs.rFull, xs.sFull, xs.sMax,
-               xs.yBot, xs.aBot, xs.sBot, xs.rBot};
+        Geom g = geomOf(xs);
         double yFull = xs.yFull;
         if (isOpen(xs.type)) yFull = xs.aFull / getWofY(g, yFull, &SWX_CIRC_TABLES[0][0]);
         double vFull = kPhi / roughness * xs.sFull * sqrt(fabs(net.slope[j])) / xs.aFull;
@@ -1567,6 +1756,14 @@ void Project::validateConduit(int j)  // link.c:992-1154 (supported shapes)
         net.modLength[j] = lengthFactor * net.length[j];
         slope /= lengthFactor;
         roughness = roughness / sqrt(lengthFactor);
+    }
+    if (xs.type == X_FORCE_MAIN) {                     // forcemain_getRoughFactor forcmain.c:51-70
+        if (opt.forceMainEqn == FM_H_W) {
+            double r = 1.318 * xs.rBot * pow(lengthFactor, 0.54);
+            xs.sBot = kGravity / pow(r, 1.852);
+        } else {
+            xs.sBot = 1.0 / 8.0 / lengthFactor;
+        }
     }
     net.roughFactor[j] = kGravity * ((roughness / kPhi) * (roughness / kPhi));
     net.beta[j] = (xs.type == X_DUMMY) ? 0.0 : kPhi * sqrt(fabs(slope)) / roughness;
@@ -1758,8 +1955,7 @@ void Project::initDepths()
     const double* ct = &SWX_CIRC_TABLES[0][0];
     auto geom = [&](int j) {
         const Xsect& x = net.xsect[j];
-        return Geom{x.type, x.yFull, x.wMax, x.ywMax, x.aFull, x.rFull, x.sFull, x.sMax,
-                    x.yBot, x.aBot, x.sBot, x.rBot};
+        return geomOf(x);
     };
     State& s = st;
     std::vector<double> acc(nn, 0.0), cnt(nn, 0.0);
@@ -1822,8 +2018,7 @@ int Project::initState()
     const double* ct = &SWX_CIRC_TABLES[0][0];
     auto geom = [&](int j) {
         const Xsect& x = net.xsect[j];
-        return Geom{x.type, x.yFull, x.wMax, x.ywMax, x.aFull, x.rFull, x.sFull, x.sMax,
-                    x.yBot, x.aBot, x.sBot, x.rBot};
+        return geomOf(x);
     };
     // project_init runs table_tseriesInit before routing_open
     for (auto& ts : net.tseries) {            // table_tseriesInit (table.c:730-740)
@@ -1969,7 +2164,7 @@ void Project::ncCoefs(int j)
     State& s = st;
     NcLink L = ncLink(j);
     const Xsect& x = net.xsect[j];
-    Geom g{x.type, x.yFull, x.wMax, x.ywMax, x.aFull, x.rFull, x.sFull, x.sMax, x.yBot, x.aBot, x.sBot, x.rBot};
+    Geom g = geomOf(x);
     if (net.linkType[j] == ORIFICE) {
         NcCoef c{};
         orificeCoefs(L, g, s.setting[j], ct, &c);

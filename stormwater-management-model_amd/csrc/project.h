@@ -101,4 +101,15 @@ private:
 
 bool setXsectParams(Xsect& x, int type, double p[4], double ucf);
 
+// the kernels' geometry record of a cross-section (tabulated shapes point at
+// their block of SWX_SHAPE_TAB)
+inline swx::Geom geomOf(const Xsect& x)
+{
+    swx::Geom g{x.type, x.yFull, x.wMax, x.ywMax, x.aFull, x.rFull, x.sFull, x.sMax,
+                x.yBot, x.aBot, x.sBot, x.rBot};
+    int off = swx::shapeTabOffset(x.type);
+    if (off >= 0) g.tb = SWX_SHAPE_TAB + off;
+    return g;
+}
+
 }  // namespace swx

@@ -14,6 +14,7 @@
 
 #include <math.h>
 #include "xsect_tables.h"
+#include "shape_tables.h"
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -31,12 +32,28 @@ namespace swx {
 struct Geom {                 // TXsect (objects.h:581-599), packed per link
     int type;
     double yFull, wMax, ywMax, aFull, rFull, sFull, sMax, yBot, aBot, sBot, rBot;
+    // tabulated shapes: the shape's table block (SWX_SHAPE_TAB, or a
+    // transect's own tables); unused by the closed-form shapes
+    const double* tb = nullptr;
 };
 
+// xsection types in the reference's enum order (enums.h)
 enum GeomType {
-    G_DUMMY = 0, G_CIRCULAR = 1, G_RECT_CLOSED = 3, G_RECT_OPEN = 4, G_TRAPEZOIDAL = 5,
-    G_TRIANGULAR = 6, G_FORCE_MAIN = 24
+    G_DUMMY = 0, G_CIRCULAR = 1, G_FILLED_CIRCULAR = 2, G_RECT_CLOSED = 3, G_RECT_OPEN = 4,
+    G_TRAPEZOIDAL = 5, G_TRIANGULAR = 6, G_PARABOLIC = 7, G_POWERFUNC = 8, G_RECT_TRIANG = 9,
+    G_RECT_ROUND = 10, G_MOD_BASKET = 11, G_HORIZ_ELLIPSE = 12, G_VERT_ELLIPSE = 13, G_ARCH = 14,
+    G_EGGSHAPED = 15, G_HORSESHOE = 16, G_GOTHIC = 17, G_CATENARY = 18, G_SEMIELLIPTICAL = 19,
+    G_BASKETHANDLE = 20, G_SEMICIRCULAR = 21, G_IRREGULAR = 22, G_CUSTOM = 23, G_FORCE_MAIN = 24,
+    G_STREET = 25
 };
+// the shapes the streaming link kernels handle inline; every other shape
+// (tabulated, composite, transect-based, force main) is routed to the cold
+// conduit kernel, so the streaming kernels' code is unchanged by them
+SWX_HD bool isBasicShape(int t)
+{
+    return t == G_DUMMY || t == G_CIRCULAR || t == G_RECT_CLOSED || t == G_RECT_OPEN ||
+           t == G_TRAPEZOIDAL || t == G_TRIANGULAR;
+}
 
 SWX_HD double gmin(double x, double y) { return (x <= y) ? x : y; }   // macros.h:28
 SWX_HD double gmax(double x, double y) { return (x >= y) ? x : y; }   // macros.h:29
@@ -207,7 +224,270 @@ SWX_HD double trapYofA(const Geom& x, double a)
     return (sqrt(x.yBot * x.yBot + 4. * x.sBot * a) - x.yBot) / (2. * x.sBot);
 }
 
+
+// ---------------------------------------------------------------------------
+// Tabulated shapes.  The reference selects, per shape, which xsect.dat table
+// each relation interpolates (xsect_getAofY/YofA/WofY/RofY/RofA/SofA/AofS/
+// dSdA, xsect.c:714-1253): e.g. A(y) of the gothic shape is the inverse of its
+// Y(A) table, the ellipses have no S table.  TabDesc records that choice.
+struct TabDesc {
+    short a, nA, y, nY, w, nW, r, nR, s, nS;   // offset / length in the block (0 = absent)
+    bool aInv;   // A(y) = invLookup of the Y(A) table
+    bool yInv;   // Y(A) = invLookup of the A(y) table
+    bool rOfY;   // R(A) = R(Y(A)) (xsect.c:1112-1119) instead of (S(A)/A)^1.5
+};
+#define SWX_TD5(S) TabDesc{SWX_TAB_##S##_A, SWX_TAB_##S##_A_N, SWX_TAB_##S##_Y, SWX_TAB_##S##_Y_N, \
+    SWX_TAB_##S##_W, SWX_TAB_##S##_W_N, SWX_TAB_##S##_R, SWX_TAB_##S##_R_N, \
+    SWX_TAB_##S##_S, SWX_TAB_##S##_S_N, false, false, false}
+#define SWX_TD3(S) TabDesc{0, 0, SWX_TAB_##S##_Y, SWX_TAB_##S##_Y_N, SWX_TAB_##S##_W, SWX_TAB_##S##_W_N, \
+    0, 0, SWX_TAB_##S##_S, SWX_TAB_##S##_S_N, true, false, false}
+#define SWX_TDE(S) TabDesc{SWX_TAB_##S##_A, SWX_TAB_##S##_A_N, 0, 0, SWX_TAB_##S##_W, SWX_TAB_##S##_W_N, \
+    SWX_TAB_##S##_R, SWX_TAB_##S##_R_N, 0, 0, false, true, true}
+SWX_HD bool isTabShape(int t)
+{
+    return (t >= G_HORIZ_ELLIPSE && t <= G_CUSTOM) || t == G_STREET;
+}
+SWX_HD TabDesc tabDesc(const Geom& x)
+{
+    switch (x.type) {
+    case G_EGGSHAPED: return SWX_TD5(EGG);
+    case G_HORSESHOE: return SWX_TD5(HORSESHOE);
+    case G_BASKETHANDLE: return SWX_TD5(BASKETHANDLE);
+    case G_GOTHIC: return SWX_TD3(GOTHIC);
+    case G_CATENARY: return SWX_TD3(CATENARY);
+    case G_SEMIELLIPTICAL: return SWX_TD3(SEMIELLIP);
+    case G_SEMICIRCULAR: return SWX_TD3(SEMICIRC);
+    case G_HORIZ_ELLIPSE: return SWX_TDE(HORIZ_ELLIPSE);
+    case G_VERT_ELLIPSE: return SWX_TDE(VERT_ELLIPSE);
+    case G_ARCH: return SWX_TDE(ARCH);
+    default: {
+        // transect / custom-shape / street tables: [n][A n][W n][R n]
+        short n = (short)x.tb[0];
+        return TabDesc{1, n, 0, 0, (short)(1 + n), n, (short)(1 + 2 * n), n, 0, 0, false, true, true};
+    }
+    }
+}
+// block offset of a built-in tabulated shape in SWX_SHAPE_TAB (-1: none)
+SWX_HD int shapeTabOffset(int t)
+{
+    switch (t) {
+    case G_EGGSHAPED: return SWX_TAB_EGG;
+    case G_HORSESHOE: return SWX_TAB_HORSESHOE;
+    case G_GOTHIC: return SWX_TAB_GOTHIC;
+    case G_CATENARY: return SWX_TAB_CATENARY;
+    case G_SEMIELLIPTICAL: return SWX_TAB_SEMIELLIP;
+    case G_BASKETHANDLE: return SWX_TAB_BASKETHANDLE;
+    case G_SEMICIRCULAR: return SWX_TAB_SEMICIRC;
+    case G_HORIZ_ELLIPSE: return SWX_TAB_HORIZ_ELLIPSE;
+    case G_VERT_ELLIPSE: return SWX_TAB_VERT_ELLIPSE;
+    case G_ARCH: return SWX_TAB_ARCH;
+    default: return -1;
+    }
+}
+
+#define SWX_RECT_TRIANG_ALFMAX 0.98   // xsect.c:45-46
+#define SWX_RECT_ROUND_ALFMAX 0.98
+
+// xsect.c:2284-2289, 2323-2344 -- wetted perimeters
+SWX_HD double parabPofY(const Geom& x, double y)
+{
+    double xx = 2. * sqrt(y) / x.rBot;
+    double t = sqrt(1.0 + xx * xx);
+    return 0.5 * x.rBot * x.rBot * (xx * t + log(xx + t));
+}
+SWX_HD double powerPofY(const Geom& x, double y)
+{
+    double dy1 = 0.02 * x.yFull;
+    double h = (x.sBot + 1.0) * x.rBot / 2.0;
+    double m = x.sBot;
+    double p = 0.0, y1 = 0.0, x1 = 0.0, x2, y2, dx, dy;
+    #pragma unroll 1
+    do {
+        y2 = y1 + dy1;
+        if (y2 > y) y2 = y;
+        x2 = h * pow(y2, m);
+        dx = x2 - x1;
+        dy = y2 - y1;
+        p += sqrt(dx * dx + dy * dy);
+        x1 = x2;
+        y1 = y2;
+    } while (y2 < y);
+    return 2.0 * p;
+}
+// xsect.c:1837-1844, 2038-2049, 2082-2099 etc.
+SWX_HD double rectTriangYofA(const Geom& x, double a)
+{
+    if (a <= x.aBot) return sqrt(a / x.sBot);
+    return x.yBot + (a - x.aBot) / x.wMax;
+}
+SWX_HD double rectTriangRofA(const Geom& x, double a)             // xsect.c:1846-1864
+{
+    if (a <= 0.0) return 0.0;
+    double y = rectTriangYofA(x, a);
+    if (y <= x.yBot) return a / (2. * y * x.rBot);
+    double p = 2. * x.yBot * x.rBot + 2. * (y - x.yBot);
+    double alf = (a / x.aFull) - SWX_RECT_TRIANG_ALFMAX;
+    if (alf > 0.0) p += alf / (1.0 - SWX_RECT_TRIANG_ALFMAX) * x.wMax;
+    return a / p;
+}
+SWX_HD double rectRoundAofY(const Geom& x, double y)              // xsect.c:2038-2049
+{
+    if (y > x.yBot) return x.aBot + (y - x.yBot) * x.wMax;
+    double theta1 = 2.0 * acos(1.0 - y / x.rBot);
+    return 0.5 * x.rBot * x.rBot * (theta1 - sin(theta1));
+}
+SWX_HD double rectRoundYofA(const Geom& x, double a, const double* ct)   // xsect.c:1938-1950
+{
+    if (a > x.aBot) return x.yBot + (a - x.aBot) / x.wMax;
+    double alpha = a / (3.141592654 * x.rBot * x.rBot);
+    if (alpha < 0.04) return (2.0 * x.rBot) * yCircular(alpha);
+    return (2.0 * x.rBot) * lookup(alpha, SWX_TY(ct), SWX_CIRC_N);
+}
+SWX_HD double rectRoundRofA(const Geom& x, double a, const double* ct)   // xsect.c:1952-1976
+{
+    if (a <= 0.0) return 0.0;
+    if (a > x.aBot) {
+        double y1 = (a - x.aBot) / x.wMax;
+        double theta1 = 2.0 * asin(x.wMax / 2.0 / x.rBot);
+        double p = x.rBot * theta1 + 2.0 * y1;
+        double arg = (a / x.aFull) - SWX_RECT_ROUND_ALFMAX;
+        if (arg > 0.0) p += arg / (1.0 - SWX_RECT_ROUND_ALFMAX) * x.wMax;
+        return a / p;
+    }
+    double y1 = rectRoundYofA(x, a, ct);
+    double theta1 = 2.0 * acos(1.0 - y1 / x.rBot);
+    double p = x.rBot * theta1;
+    return a / p;
+}
+SWX_HD double modBasketYofA(const Geom& x, double a, const double* ct)   // xsect.c:2082-2099
+{
+    if (a <= x.aFull - x.aBot) return a / x.wMax;
+    double alpha = (x.aFull - a) / (3.141592654 * x.rBot * x.rBot);
+    double y1;
+    if (alpha < 0.04) y1 = yCircular(alpha);
+    else y1 = lookup(alpha, SWX_TY(ct), SWX_CIRC_N);
+    y1 = 2.0 * x.rBot * y1;
+    return x.yFull - y1;
+}
+SWX_HD double modBasketRofA(const Geom& x, double a, const double* ct)   // xsect.c:2101-2126
+{
+    if (a <= x.aFull - x.aBot) return a / (x.wMax + 2.0 * a / x.wMax);
+    double y1 = x.yFull - modBasketYofA(x, a, ct);
+    double theta1 = 2.0 * acos(1.0 - y1 / x.rBot);
+    double p = (x.sBot - theta1) * x.rBot;
+    y1 = x.yFull - x.yBot;
+    p = p + 2.0 * y1 + x.wMax;
+    return a / p;
+}
+// FILLED_CIRCULAR: the reference widens the section to the unfilled circle,
+// evaluates the circular relation and narrows it again (xsect.c:2462-2524)
+SWX_HD double filledCircAofY(const Geom& x, double y, const double* ct)
+{
+    double yF = x.yFull + x.yBot, aF = x.aFull + x.aBot;
+    y += x.yBot;
+    double a = aF * lookup(y / yF, SWX_TA(ct), SWX_CIRC_N);
+    return a - x.aBot;
+}
+SWX_HD double filledCircYofA(const Geom& x, double a, const double* ct)
+{
+    double yF = x.yFull + x.yBot, aF = x.aFull + x.aBot;
+    a += x.aBot;
+    double alpha = a / aF, y;
+    if (alpha < 0.04) y = yF * yCircular(alpha);
+    else y = yF * lookup(alpha, SWX_TY(ct), SWX_CIRC_N);
+    return y - x.yBot;
+}
+SWX_HD double filledCircRofY(const Geom& x, double y, const double* ct)
+{
+    double yF = x.yFull + x.yBot, aF = x.aFull + x.aBot;
+    y += x.yBot;
+    double a = aF * lookup(y / yF, SWX_TA(ct), SWX_CIRC_N);
+    double r = 0.25 * yF * lookup(y / yF, SWX_TR(ct), SWX_CIRC_N);
+    double p = (a / r);
+    a = a - x.aBot;
+    p = p - x.rBot + x.sBot;
+    return a / p;
+}
+
+// the non-basic shapes' A(y), W(y), R(y) and Y(A) (xsect.c:773-1096)
+SWX_HD double exAofY(const Geom& x, double y, const double* ct)
+{
+    switch (x.type) {
+    case G_FILLED_CIRCULAR: return filledCircAofY(x, y, ct);
+    case G_RECT_TRIANG:
+        if (y <= x.yBot) return y * y * x.sBot;
+        return x.aBot + (y - x.yBot) * x.wMax;
+    case G_RECT_ROUND: return rectRoundAofY(x, y);
+    case G_MOD_BASKET: {
+        if (y <= x.yFull - x.yBot) return y * x.wMax;
+        double y1 = x.yFull - y;
+        double theta1 = 2.0 * acos(1.0 - y1 / x.rBot);
+        double a1 = 0.5 * x.rBot * x.rBot * (theta1 - sin(theta1));
+        return x.aFull - a1;
+    }
+    case G_PARABOLIC: return (4. / 3. * x.rBot * y * sqrt(y));
+    case G_POWERFUNC: return x.rBot * pow(y, x.sBot + 1.0);
+    default: {
+        if (!isTabShape(x.type)) return 0.0;
+        TabDesc d = tabDesc(x);
+        double yNorm = y / x.yFull;
+        if (d.aInv) return x.aFull * invLookup(yNorm, x.tb + d.y, d.nY);
+        return x.aFull * lookup(yNorm, x.tb + d.a, d.nA);
+    }
+    }
+}
+SWX_HD double exWofY(const Geom& x, double y, const double* ct)
+{
+    switch (x.type) {
+    case G_FILLED_CIRCULAR: {
+        double yNorm = (y + x.yBot) / (x.yFull + x.yBot);
+        return x.wMax * lookup(yNorm, SWX_TW(ct), SWX_CIRC_N);
+    }
+    case G_RECT_TRIANG:
+        if (y <= x.yBot) return 2.0 * x.sBot * y;
+        return x.wMax;
+    case G_RECT_ROUND:
+        if (y > x.yBot) return x.wMax;
+        return 2.0 * sqrt(y * (2.0 * x.rBot - y));
+    case G_MOD_BASKET: {
+        if (y <= 0.0) return 0.0;
+        if (y <= x.yFull - x.yBot) return x.wMax;
+        double y1 = x.yFull - y;
+        return 2.0 * sqrt(y1 * (2.0 * x.rBot - y1));
+    }
+    case G_PARABOLIC: return 2.0 * x.rBot * sqrt(y);
+    case G_POWERFUNC: return (x.sBot + 1.0) * x.rBot * pow(y, x.sBot);
+    default: {
+        if (!isTabShape(x.type)) return 0.0;
+        TabDesc d = tabDesc(x);
+        return x.wMax * lookup(y / x.yFull, x.tb + d.w, d.nW);
+    }
+    }
+}
+SWX_HD double exYofA(const Geom& x, double a, const double* ct)
+{
+    switch (x.type) {
+    case G_FILLED_CIRCULAR: return filledCircYofA(x, a, ct);
+    case G_RECT_TRIANG: return rectTriangYofA(x, a);
+    case G_RECT_ROUND: return rectRoundYofA(x, a, ct);
+    case G_MOD_BASKET: return modBasketYofA(x, a, ct);
+    case G_PARABOLIC: return pow((3. / 4.) * a / x.rBot, 2. / 3.);
+    case G_POWERFUNC: return pow(a / x.rBot, 1.0 / (x.sBot + 1.0));
+    default: {
+        if (!isTabShape(x.type)) return 0.0;
+        TabDesc d = tabDesc(x);
+        double alpha = a / x.aFull;
+        if (d.yInv) return x.yFull * invLookup(alpha, x.tb + d.a, d.nA);
+        return x.yFull * lookup(alpha, x.tb + d.y, d.nY);
+    }
+    }
+}
+
+// kAll: the relations for every shape.  The streaming link kernels, which
+// only see the basic shapes, pass false so the other shapes' code is not
+// compiled into them; everything else uses the default.
 // xsect.c:857-939
+template <bool kAll = true>
 SWX_HD double getAofY(const Geom& x, double y, const double* ct)
 {
     double yNorm = y / x.yFull;
@@ -218,11 +498,14 @@ SWX_HD double getAofY(const Geom& x, double y, const double* ct)
     case G_RECT_OPEN:   return y * x.wMax;
     case G_TRAPEZOIDAL: return (x.yBot + x.sBot * y) * y;
     case G_TRIANGULAR:  return y * y * x.sBot;
-    default: return 0.0;
+    default:
+        if (kAll) return exAofY(x, y, ct);
+        return 0.0;
     }
 }
 
 // xsect.c:943-1027
+template <bool kAll = true>
 SWX_HD double getWofY(const Geom& x, double y, const double* ct)
 {
     double yNorm = y / x.yFull;
@@ -232,13 +515,52 @@ SWX_HD double getWofY(const Geom& x, double y, const double* ct)
     case G_RECT_OPEN:   return x.wMax;
     case G_TRAPEZOIDAL: return x.yBot + 2.0 * y * x.sBot;
     case G_TRIANGULAR:  return 2.0 * x.sBot * y;
-    default: return 0.0;
+    default:
+        if (kAll) return exWofY(x, y, ct);
+        return 0.0;
     }
 }
 
+template <bool kAll = true>
 SWX_HD_COLD double getSofA(const Geom& x, double a, const double* ct);
+SWX_HD_COLD double getRofYAll(const Geom& x, double y, const double* ct);
+
+// R(A) of every shape whose relation does not go through the section factor
+// (xsect.c:1112-1138); -1 for the shapes whose R(A) is (S(A)/A)^1.5.  Never
+// calls back into getSofA, so the cold call graph stays acyclic.
+template <bool kAll = true>
+SWX_HD double rOfADirect(const Geom& x, double a, const double* ct)
+{
+    switch (x.type) {
+    case G_RECT_CLOSED: return rectClosedRofA(x, a);
+    case G_RECT_OPEN:   return a / (x.wMax + (2. - x.sBot) * a / x.wMax);
+    case G_TRAPEZOIDAL: return a / (x.yBot + trapYofA(x, a) * x.rBot);
+    case G_TRIANGULAR:  return a / (2. * sqrt(a / x.sBot) * x.rBot);
+    default: break;
+    }
+    if (!kAll) return -1.0;
+    switch (x.type) {
+    case G_RECT_TRIANG: return rectTriangRofA(x, a);
+    case G_RECT_ROUND: return rectRoundRofA(x, a, ct);
+    case G_MOD_BASKET: return modBasketRofA(x, a, ct);
+    case G_PARABOLIC: return a / parabPofY(x, exYofA(x, a, ct));
+    case G_POWERFUNC: return a / powerPofY(x, exYofA(x, a, ct));
+    case G_FILLED_CIRCULAR: {                 // R(Y(A)) (xsect.c:1116, 1046-1049)
+        double y = filledCircYofA(x, a, ct);
+        if (x.yBot == 0.0) return x.rFull * lookup(y / x.yFull, SWX_TR(ct), SWX_CIRC_N);
+        return filledCircRofY(x, y, ct);
+    }
+    default:
+        if (isTabShape(x.type)) {
+            TabDesc d = tabDesc(x);
+            if (d.rOfY) return x.rFull * lookup(exYofA(x, a, ct) / x.yFull, x.tb + d.r, d.nR);
+        }
+        return -1.0;
+    }
+}
 
 // xsect.c:1100-1145
+template <bool kAll = true>
 SWX_HD double getRofA(const Geom& x, double a, const double* ct)
 {
     if (a <= 0.0) return 0.0;
@@ -248,7 +570,11 @@ SWX_HD double getRofA(const Geom& x, double a, const double* ct)
     case G_TRAPEZOIDAL: return a / (x.yBot + trapYofA(x, a) * x.rBot);
     case G_TRIANGULAR:  return a / (2. * sqrt(a / x.sBot) * x.rBot);
     default: {
-        double cathy = getSofA(x, a, ct);
+        if (kAll && !isBasicShape(x.type)) {
+            double r = rOfADirect<kAll>(x, a, ct);
+            if (r >= 0.0) return r;
+        }
+        double cathy = getSofA<kAll>(x, a, ct);
         if (cathy < 1.E-6 || a < 1.E-6) return 0.0;
         return pow(cathy / a, 3. / 2.);
     }
@@ -256,6 +582,7 @@ SWX_HD double getRofA(const Geom& x, double a, const double* ct)
 }
 
 // xsect.c:1031-1096
+template <bool kAll = true>
 SWX_HD double getRofY(const Geom& x, double y, const double* ct)
 {
     double yNorm = y / x.yFull;
@@ -265,19 +592,22 @@ SWX_HD double getRofY(const Geom& x, double y, const double* ct)
         if (y == 0.0) return 0.0;
         return ((x.yBot + x.sBot * y) * y) / (x.yBot + y * x.rBot);
     case G_TRIANGULAR: return (y * x.sBot) / (2. * x.rBot);
-    // xsect.c:1091 default branch R(A(y)); written out for the two table-free
-    // shapes that reach it so the kernels' hydraulic-radius path has no call
-    case G_RECT_CLOSED: return rectClosedRofA(x, getAofY(x, y, ct));
+    // xsect.c:1094 default branch R(A(y)); written out for the two table-free
+    // basic shapes so the streaming kernels' hydraulic-radius path has no call
+    case G_RECT_CLOSED: return rectClosedRofA(x, getAofY<false>(x, y, ct));
     case G_RECT_OPEN: {
-        double a = getAofY(x, y, ct);
+        double a = getAofY<false>(x, y, ct);
         if (a <= 0.0) return 0.0;
         return a / (x.wMax + (2. - x.sBot) * a / x.wMax);
     }
-    default: return 0.0;     // no other shape is accepted by the reader
+    default:
+        if (kAll) return getRofYAll(x, y, ct);
+        return 0.0;
     }
 }
 
 // xsect.c:773-853
+template <bool kAll = true>
 SWX_HD double getYofA(const Geom& x, double a, const double* ct)
 {
     double alpha = a / x.aFull;
@@ -289,11 +619,51 @@ SWX_HD double getYofA(const Geom& x, double a, const double* ct)
     case G_RECT_OPEN:   return a / x.wMax;
     case G_TRAPEZOIDAL: return trapYofA(x, a);
     case G_TRIANGULAR:  return sqrt(a / x.sBot);
-    default: return 0.0;
+    default:
+        if (kAll) return exYofA(x, a, ct);
+        return 0.0;
     }
 }
 
-// xsect.c:714-769 (+1755-1768, 1810-1815, 2391-2401)
+// R(y) of the non-basic shapes (xsect.c:1046-1094)
+SWX_HD_COLD double getRofYAll(const Geom& x, double y, const double* ct)
+{
+    double yNorm = y / x.yFull;
+    switch (x.type) {
+    case G_FILLED_CIRCULAR:
+        if (x.yBot == 0.0) return x.rFull * lookup(yNorm, SWX_TR(ct), SWX_CIRC_N);
+        return filledCircRofY(x, y, ct);
+    case G_RECT_TRIANG: {                                          // xsect.c:1908-1925
+        if (y <= x.yBot) return y * x.sBot / (2. * x.rBot);
+        double a = x.aBot + (y - x.yBot) * x.wMax;
+        double p = 2. * x.yBot * x.rBot + 2. * (y - x.yBot);
+        double alf = (a / x.aFull) - SWX_RECT_TRIANG_ALFMAX;
+        if (alf > 0.0) p += alf / (1.0 - SWX_RECT_TRIANG_ALFMAX) * x.wMax;
+        return a / p;
+    }
+    case G_RECT_ROUND: {                                           // xsect.c:2051-2063
+        if (y <= 0.0) return 0.0;
+        if (y > x.yBot) return rectRoundRofA(x, rectRoundAofY(x, y), ct);
+        double theta1 = 2.0 * acos(1.0 - y / x.rBot);
+        return 0.5 * x.rBot * (1.0 - sin(theta1)) / theta1;
+    }
+    case G_PARABOLIC:
+        if (y <= 0.0) return 0.0;
+        return exAofY(x, y, ct) / parabPofY(x, y);
+    case G_POWERFUNC:
+        if (y <= 0.0) return 0.0;
+        return exAofY(x, y, ct) / powerPofY(x, y);
+    default:
+        if (isTabShape(x.type)) {
+            TabDesc d = tabDesc(x);
+            if (d.nR) return x.rFull * lookup(yNorm, x.tb + d.r, d.nR);
+        }
+        return getRofA<true>(x, getAofY<true>(x, y, ct), ct);
+    }
+}
+
+// xsect.c:714-769 (+1755-1768, 1810-1815, 1866-1877, 1978-2011, 2391-2401)
+template <bool kAll>
 SWX_HD_COLD double getSofA(const Geom& x, double a, const double* ct)
 {
     double alpha = a / x.aFull;
@@ -304,32 +674,74 @@ SWX_HD_COLD double getSofA(const Geom& x, double a, const double* ct)
     case G_RECT_CLOSED:
         if (a / x.aFull > 0.97)
             return x.sMax + (x.sFull - x.sMax) * (a / x.aFull - 0.97) / (1.0 - 0.97);
-        return a * pow(getRofA(x, a, ct), 2. / 3.);
+        return a * pow(rectClosedRofA(x, a), 2. / 3.);
     case G_RECT_OPEN: {
         double y = a / x.wMax;
         double r = a / ((2.0 - x.sBot) * y + x.wMax);
         return a * pow(r, 2. / 3.);
     }
+    case G_RECT_TRIANG:
+        if (!kAll) return 0.0;
+        if (a / x.aFull > SWX_RECT_TRIANG_ALFMAX)
+            return x.sMax + (x.sFull - x.sMax) * (a / x.aFull - SWX_RECT_TRIANG_ALFMAX) /
+                                (1.0 - SWX_RECT_TRIANG_ALFMAX);
+        return a * pow(rectTriangRofA(x, a), 2. / 3.);
+    case G_RECT_ROUND: {
+        if (!kAll) return 0.0;
+        if (a / x.aFull > SWX_RECT_ROUND_ALFMAX)
+            return x.sMax + (x.sFull - x.sMax) * (a / x.aFull - SWX_RECT_ROUND_ALFMAX) /
+                                (1.0 - SWX_RECT_ROUND_ALFMAX);
+        if (a > x.aBot) return a * pow(rectRoundRofA(x, a, ct), 2. / 3.);
+        double aF = 3.141592654 * x.rBot * x.rBot;
+        double al = a / aF;
+        if (al < 0.04) return x.sBot * sCircular(al);
+        return x.sBot * lookup(al, SWX_TS(ct), SWX_CIRC_N);
+    }
     default: {
+        if (kAll && isTabShape(x.type)) {
+            TabDesc d = tabDesc(x);
+            if (d.nS) return x.sFull * lookup(alpha, x.tb + d.s, d.nS);
+        }
         if (a == 0.0) return 0.0;
-        double r = getRofA(x, a, ct);
+        if (a <= 0.0) return 0.0;                  // xsect_getRofA's a <= 0 test
+        double r = rOfADirect<kAll>(x, a, ct);     // no shape reaching here has an S table
         if (r < 1.E-6) return 0.0;
         return a * pow(r, 2. / 3.);
     }
     }
 }
 
+// xsect_getAmax (xsect.c:700-710)
+SWX_HD double areaMax(const Geom& x)
+{
+    if (x.type == G_IRREGULAR || x.type == G_CUSTOM) return x.aBot;
+    return amaxRatio(x.type) * x.aFull;
+}
+
 // xsect.c:1453-1470
+template <bool kAll = true>
 SWX_HD_COLD double genericdSdA(const Geom& x, double a, const double* ct)
 {
     double alpha = a / x.aFull, alpha1 = alpha - 0.001, alpha2 = alpha + 0.001;
     if (alpha1 < 0.0) alpha1 = 0.0;
     double a1 = alpha1 * x.aFull;
     double a2 = alpha2 * x.aFull;
-    return (getSofA(x, a2, ct) - getSofA(x, a1, ct)) / (a2 - a1);
+    return (getSofA<kAll>(x, a2, ct) - getSofA<kAll>(x, a1, ct)) / (a2 - a1);
+}
+
+// xsect.c:1424-1449
+SWX_HD double tabulardSdA(const Geom& x, double a, const double* t, int n)
+{
+    double alpha = a / x.aFull;
+    double delta = 1.0 / ((double)n - 1);
+    int i = (int)(alpha / delta);
+    if (i >= n - 1) i = n - 2;
+    double dSdA = (t[i + 1] - t[i]) / delta;
+    return dSdA * x.sFull / x.aFull;
 }
 
 // xsect.c:1194-1253 with the shape-specific derivatives
+template <bool kAll = true>
 SWX_HD_COLD double getdSdA(const Geom& x, double a, const double* ct)
 {
     double alpha, r, dPdA;
@@ -344,55 +756,84 @@ SWX_HD_COLD double getdSdA(const Geom& x, double a, const double* ct)
             dPdA = 4.0 / x.yFull / (1. - cos(theta));
             return (5. / 3. - (2. / 3.) * dPdA * r) * pow(r, 2. / 3.);
         }
-        const double* t = SWX_TS(ct);                     // xsect.c:1424-1449
-        double delta = 1.0 / ((double)SWX_CIRC_N - 1);
-        int i = (int)(alpha / delta);
-        if (i >= SWX_CIRC_N - 1) i = SWX_CIRC_N - 2;
-        double dSdA = (t[i + 1] - t[i]) / delta;
-        return dSdA * x.sFull / x.aFull;
+        return tabulardSdA(x, a, SWX_TS(ct), SWX_CIRC_N);
     }
     case G_RECT_CLOSED:                                     // xsect.c:1770-1791
         alpha = a / x.aFull;
         if (alpha > 0.97) return (x.sFull - x.sMax) / ((1.0 - 0.97) * x.aFull);
-        if (alpha <= 1.0e-30) return genericdSdA(x, a, ct);
-        r = getRofA(x, a, ct);
+        if (alpha <= 1.0e-30) return genericdSdA<kAll>(x, a, ct);
+        r = getRofA<kAll>(x, a, ct);
         return (5. / 3. - (2. / 3.) * (2.0 / x.wMax) * r) * pow(r, 2. / 3.);
     case G_RECT_OPEN:                                       // xsect.c:1818-1830
-        if (a / x.aFull <= 1.0e-30) return genericdSdA(x, a, ct);
-        r = getRofA(x, a, ct);
+        if (a / x.aFull <= 1.0e-30) return genericdSdA<kAll>(x, a, ct);
+        r = getRofA<kAll>(x, a, ct);
         dPdA = (2.0 - x.sBot) / x.wMax;
         return (5. / 3. - (2. / 3.) * dPdA * r) * pow(r, 2. / 3.);
     case G_TRAPEZOIDAL:                                     // xsect.c:2196-2208
-        if (a / x.aFull <= 1.0e-30) return genericdSdA(x, a, ct);
-        r = getRofA(x, a, ct);
+        if (a / x.aFull <= 1.0e-30) return genericdSdA<kAll>(x, a, ct);
+        r = getRofA<kAll>(x, a, ct);
         dPdA = x.rBot / sqrt(x.yBot * x.yBot + 4. * x.sBot * a);
         return (5. / 3. - (2. / 3.) * dPdA * r) * pow(r, 2. / 3.);
     case G_TRIANGULAR:                                      // xsect.c:2241-2251
-        if (a / x.aFull <= 1.0e-30) return genericdSdA(x, a, ct);
-        r = getRofA(x, a, ct);
+        if (a / x.aFull <= 1.0e-30) return genericdSdA<kAll>(x, a, ct);
+        r = getRofA<kAll>(x, a, ct);
         dPdA = x.rBot / sqrt(a * x.sBot);
         return (5. / 3. - (2. / 3.) * dPdA * r) * pow(r, 2. / 3.);
-    default: return genericdSdA(x, a, ct);
+    case G_RECT_TRIANG:                                     // xsect.c:1879-1900
+        if (!kAll) return 0.0;
+        alpha = a / x.aFull;
+        if (alpha > SWX_RECT_TRIANG_ALFMAX)
+            return (x.sFull - x.sMax) / ((1.0 - SWX_RECT_TRIANG_ALFMAX) * x.aFull);
+        if (alpha <= 1.0e-30) return genericdSdA<kAll>(x, a, ct);
+        if (a > x.aBot) dPdA = 2.0 / x.wMax;
+        else dPdA = x.rBot / sqrt(a * x.sBot);
+        r = rectTriangRofA(x, a);
+        return (5. / 3. - (2. / 3.) * dPdA * r) * pow(r, 2. / 3.);
+    case G_RECT_ROUND:                                      // xsect.c:2013-2036
+        if (!kAll) return 0.0;
+        if (a / x.aFull > SWX_RECT_ROUND_ALFMAX)
+            return (x.sFull - x.sMax) / ((1.0 - SWX_RECT_ROUND_ALFMAX) * x.aFull);
+        if (a > x.aBot) {
+            r = rectRoundRofA(x, a, ct);
+            dPdA = 2.0 / x.wMax;
+            return (5. / 3. - (2. / 3.) * dPdA * r) * pow(r, 2. / 3.);
+        }
+        return genericdSdA<kAll>(x, a, ct);
+    case G_MOD_BASKET:                                      // xsect.c:2128-2143
+        if (!kAll) return 0.0;
+        if (a <= x.aFull - x.aBot && a / x.aFull > 1.0e-30) {
+            r = a / (x.wMax + 2.0 * a / x.wMax);
+            dPdA = 2.0 / x.wMax;
+            return (5. / 3. - (2. / 3.) * dPdA * r) * pow(r, 2. / 3.);
+        }
+        return genericdSdA<kAll>(x, a, ct);
+    default:
+        if (kAll && isTabShape(x.type)) {
+            TabDesc d = tabDesc(x);
+            if (d.nS) return tabulardSdA(x, a, x.tb + d.s, d.nS);
+        }
+        return genericdSdA<kAll>(x, a, ct);
     }
 }
 
 // findroot.c:19-87 on f(a) = S(a) - s, used by generic_getAofS (xsect.c:1359-1400)
+template <bool kAll = true>
 SWX_HD_COLD double genericAofS(const Geom& x, double s, const double* ct)
 {
     if (s <= 0.0) return 0.0;
     double x1, x2;
     if ((s <= x.sMax && s >= x.sFull) && x.sMax != x.sFull) {
         x1 = x.aFull;
-        x2 = amaxRatio(x.type) * x.aFull;
+        x2 = areaMax(x);
     } else {
         x1 = 0.0;
-        x2 = amaxRatio(x.type) * x.aFull;
+        x2 = areaMax(x);
     }
     double xx = 0.5 * (x1 + x2), xacc = 0.0001 * x.aFull;
     double xlo = x1, xhi = x2;
     double dxold = fabs(x2 - x1), dx = dxold;
-    double f = getSofA(x, xx, ct) - s;
-    double df = getdSdA(x, xx, ct);
+    double f = getSofA<kAll>(x, xx, ct) - s;
+    double df = getdSdA<kAll>(x, xx, ct);
     #pragma unroll 1
     for (int j = 1; j <= 60; j++) {
         if ((((xx - xhi) * df - f) * ((xx - xlo) * df - f) >= 0.0 ||
@@ -409,50 +850,58 @@ SWX_HD_COLD double genericAofS(const Geom& x, double s, const double* ct)
             if (temp == xx) break;
         }
         if (fabs(dx) < xacc) break;
-        f = getSofA(x, xx, ct) - s;
-        df = getdSdA(x, xx, ct);
+        f = getSofA<kAll>(x, xx, ct) - s;
+        df = getdSdA<kAll>(x, xx, ct);
         if (f < 0.0) xlo = xx; else xhi = xx;
     }
     return xx;
 }
 
 // xsect.c:1149-1190 (+ circ_getAofS 2378-2389)
+template <bool kAll = true>
 SWX_HD double getAofS(const Geom& x, double s, const double* ct)
 {
+    double psi = s / x.sFull;          // of the unclamped s (xsect.c:1157)
     if (s <= 0.0) return 0.0;
     if (s > x.sMax) s = x.sMax;
     if (x.type == G_CIRCULAR || x.type == G_FORCE_MAIN) {
-        double psi = s / x.sFull;
+        psi = s / x.sFull;
         if (psi == 0.0) return 0.0;
         if (psi >= 1.0) return x.aFull;
         if (psi <= 0.015) return x.aFull * aCircular(psi);
         return x.aFull * invLookup(psi, SWX_TS(ct), SWX_CIRC_N);
     }
     if (x.type == G_DUMMY) return 0.0;
-    return genericAofS(x, s, ct);
+    if (kAll && isTabShape(x.type)) {
+        TabDesc d = tabDesc(x);
+        if (d.nS) return x.aFull * invLookup(psi, x.tb + d.s, d.nS);
+    }
+    return genericAofS<kAll>(x, s, ct);
 }
 
 // xsect.c:1612-1630
+template <bool kAll = true>
 SWX_HD double qCritical(const Geom& x, double yc, double qTarget, const double* ct)
 {
-    double a = getAofY(x, yc, ct);
-    double w = getWofY(x, yc, ct);
+    double a = getAofY<kAll>(x, yc, ct);
+    double w = getWofY<kAll>(x, yc, ct);
     double qc = -qTarget;
     if (w > 0.0) qc = a * sqrt(32.2 * a / w) - qTarget;
     return qc;
 }
 
 // xsect.c:1634-1696
+template <bool kAll = true>
 SWX_HD_COLD double yCritEnum(const Geom& x, double q, double y0, const double* ct)
 {
     double dy = x.yFull / 25., yc, qc;
     int i1 = (int)(y0 / dy);
-    double q0 = qCritical(x, i1 * dy, 0.0, ct);
+    double q0 = qCritical<kAll>(x, i1 * dy, 0.0, ct);
     if (q0 < q) {
         yc = x.yFull;
         #pragma unroll 1
         for (int i = i1 + 1; i <= 25; i++) {
-            qc = qCritical(x, i * dy, 0.0, ct);
+            qc = qCritical<kAll>(x, i * dy, 0.0, ct);
             if (qc >= q) {
                 yc = ((q - q0) / (qc - q0) + ((double)i - 1)) * dy;
                 break;
@@ -463,7 +912,7 @@ SWX_HD_COLD double yCritEnum(const Geom& x, double q, double y0, const double* c
         yc = 0.0;
         #pragma unroll 1
         for (int i = i1 - 1; i >= 0; i--) {
-            qc = qCritical(x, i * dy, 0.0, ct);
+            qc = qCritical<kAll>(x, i * dy, 0.0, ct);
             if (qc < q) {
                 yc = ((q - qc) / (q0 - qc) + (double)i) * dy;
                 break;
@@ -475,16 +924,17 @@ SWX_HD_COLD double yCritEnum(const Geom& x, double q, double y0, const double* c
 }
 
 // xsect.c:1700-1748 with findroot_Ridder (findroot.c:90-138)
+template <bool kAll = true>
 SWX_HD_COLD double yCritRidder(const Geom& x, double q, double y0, const double* ct)
 {
     double y1 = 0.0, y2 = 0.99 * x.yFull;
-    double q2 = qCritical(x, y2, 0.0, ct);
+    double q2 = qCritical<kAll>(x, y2, 0.0, ct);
     if (q2 < q) return x.yFull;
-    double q0 = qCritical(x, y0, 0.0, ct);
-    double q1 = qCritical(x, 0.5 * x.yFull, 0.0, ct);
+    double q0 = qCritical<kAll>(x, y0, 0.0, ct);
+    double q1 = qCritical<kAll>(x, 0.5 * x.yFull, 0.0, ct);
     if (q0 > q) { y2 = y0; if (q1 < q) y1 = 0.5 * x.yFull; }
     else        { y1 = y0; if (q1 > q) y2 = 0.5 * x.yFull; }
-    double flo = qCritical(x, y1, q, ct), fhi = qCritical(x, y2, q, ct);
+    double flo = qCritical<kAll>(x, y1, q, ct), fhi = qCritical<kAll>(x, y2, q, ct);
     if (flo == 0.0) return y1;
     if (fhi == 0.0) return y2;
     double ans = 0.5 * (y1 + y2);
@@ -493,13 +943,13 @@ SWX_HD_COLD double yCritRidder(const Geom& x, double q, double y0, const double*
         #pragma unroll 1
         for (int j = 1; j <= 60; j++) {
             double xm = 0.5 * (xlo + xhi);
-            double fm = qCritical(x, xm, q, ct);
+            double fm = qCritical<kAll>(x, xm, q, ct);
             double s = sqrt(fm * fm - flo * fhi);
             if (s == 0.0) return ans;
             double xnew = xm + (xm - xlo) * ((flo >= fhi ? 1.0 : -1.0) * fm / s);
             if (fabs(xnew - ans) <= 0.001) break;
             ans = xnew;
-            double fnew = qCritical(x, ans, q, ct);
+            double fnew = qCritical<kAll>(x, ans, q, ct);
             if ((fnew >= 0.0 ? fabs(fm) : -fabs(fm)) != fm) { xlo = xm; flo = fm; xhi = ans; fhi = fnew; }
             else if ((fnew >= 0.0 ? fabs(flo) : -fabs(flo)) != flo) { xhi = ans; fhi = fnew; }
             else if ((fnew >= 0.0 ? fabs(fhi) : -fabs(fhi)) != fhi) { xlo = ans; flo = fnew; }
@@ -512,6 +962,7 @@ SWX_HD_COLD double yCritRidder(const Geom& x, double q, double y0, const double*
 }
 
 // xsect.c:1257-1319
+template <bool kAll = true>
 SWX_HD_COLD double getYcrit(const Geom& x, double q, const double* ct)
 {
     double q2g = (q * q) / 32.2, y;
@@ -525,18 +976,26 @@ SWX_HD_COLD double getYcrit(const Geom& x, double q, const double* ct)
     case G_TRIANGULAR:
         y = pow(2.0 * q2g / (x.sBot * x.sBot), 1. / 5.);
         break;
+    case G_PARABOLIC:
+        y = pow(27. / 32. * q2g / (x.rBot * x.rBot), 1. / 4.);
+        break;
+    case G_POWERFUNC:
+        y = 1. / (2.0 * x.sBot + 3.0);
+        y = pow(q2g * (x.sBot + 1.0) / (x.rBot * x.rBot), y);
+        break;
     default: {
         y = 1.01 * pow(q2g / x.yFull, 1. / 4.);
         if (y >= x.yFull) y = 0.97 * x.yFull;
         double r = x.aFull / (3.141592654 / 4.0 * (x.yFull * x.yFull));
-        if (r >= 0.5 && r <= 2.0) y = yCritEnum(x, q, y, ct);
-        else y = yCritRidder(x, q, y, ct);
+        if (r >= 0.5 && r <= 2.0) y = yCritEnum<kAll>(x, q, y, ct);
+        else y = yCritRidder<kAll>(x, q, y, ct);
     }
     }
     return gmin(y, x.yFull);
 }
 
 // link.c:783-804 (conduits)
+template <bool kAll = true>
 SWX_HD_COLD double linkYnorm(const Geom& x, double q, double qMax, double beta, const double* ct)
 {
     if (x.type == G_DUMMY) return 0.0;
@@ -544,17 +1003,47 @@ SWX_HD_COLD double linkYnorm(const Geom& x, double q, double qMax, double beta, 
     if (q > qMax) q = qMax;
     if (q <= 0.0) return 0.0;
     double s = q / beta;
-    double a = getAofS(x, s, ct);
-    return getYofA(x, a, ct);
+    double a = getAofS<kAll>(x, s, ct);
+    return getYofA<kAll>(x, a, ct);
 }
 
 // link.c:847-871 (conduits)
+template <bool kAll = true>
 SWX_HD double linkFroude(const Geom& x, double v, double y, const double* ct)
 {
     if (y <= 0.0001) return 0.0;
     if (!isOpen(x.type) && x.yFull - y <= 0.0001) return 0.0;
-    y = getAofY(x, y, ct) / getWofY(x, y, ct);
+    y = getAofY<kAll>(x, y, ct) / getWofY<kAll>(x, y, ct);
     return fabs(v) / sqrt(32.2 * y);
 }
 
+
+// ---------------------------------------------------------------------------
+// Force mains (forcmain.c).  rBot holds the Hazen-Williams C-factor or the
+// Darcy-Weisbach roughness height; sBot the full-flow roughness factor.
+enum { FM_H_W = 0, FM_D_W = 1 };
+// forcemain_getFricFactor (forcmain.c:128-157), the 2000 < Re < 4000 blend's
+// recursion on Re = 4000 written out
+SWX_HD double fmFricFactor(double e, double hrad, double re)
+{
+    if (re < 10.0) re = 10.0;
+    if (re <= 2000.0) return 64.0 / re;
+    double r = (re < 4000.0) ? 4000.0 : re;
+    double f = e / 3.7 / (4.0 * hrad);
+    if (r < 1.0e10) f += 5.74 / pow(r, 0.9);
+    f = log10(f);
+    f = 0.25 / f / f;
+    if (re < 4000.0) f = 0.032 + (f - 0.032) * (re - 2000.0) / 2000.0;
+    return f;
+}
+// forcemain_getFricSlope (forcmain.c:93-115)
+SWX_HD double fmFricSlope(int eqn, const Geom& x, double v, double hrad)
+{
+    if (eqn == FM_H_W) return x.sBot * pow(v, 0.852) / pow(hrad, 1.1667);
+    double re = 4.0 * hrad * v / 1.1E-5;
+    double f = fmFricFactor(x.rBot, hrad, re);
+    return f * x.sBot * v / hrad;
+}
+
 }  // namespace swx
+

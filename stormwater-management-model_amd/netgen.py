@@ -308,10 +308,37 @@ R1          3.0   9.0
 """
 
 
+# every cross-section shape beyond the basic five, one per conduit of the
+# Example network (xsect.c:216-634): tabulated, composite, closed-form and
+# standard-size (size code in Geom1 with Geom2 = 0) sections and a force main
+_SHAPES = {
+    "C1": "EGG              1.5  0    0    0",
+    "C2": "HORSESHOE        1.5  0    0    0",
+    "C3": "GOTHIC           2.0  0    0    0",
+    "C4": "CATENARY         2.0  0    0    0",
+    "C5": "SEMIELLIPTICAL   2.0  0    0    0",
+    "C6": "BASKETHANDLE     2.5  0    0    0",
+    "C7": "SEMICIRCULAR     2.0  0    0    0",
+    "C8": "HORIZ_ELLIPSE    3.0  4.5  0    0",
+    "C9": "VERT_ELLIPSE     3.0  2.0  0    0",
+    "C10": "ARCH            5    0    0    0",
+    "C11": "FILLED_CIRCULAR 3.0  0.5  0    0",
+    "C12": "PARABOLIC       2.0  4.0  0    0",
+    "C13": "POWER           3.5  4.0  2.5  0",
+    "C14": "RECT_TRIANGULAR 4.0  4.0  1.0  0",
+    "C15": "RECT_ROUND      4.0  4.0  3.0  0",
+    "C16": "MODBASKETHANDLE 3.0  4.0  2.5  0",
+    "C17": "FORCE_MAIN      1.0  120  0    0",
+    "C18": "HORIZ_ELLIPSE   3    0    0    0",
+    "C19": "VERT_ELLIPSE    2    0    0    0",
+}
+
+
 def write_example(path: str, *, route_step: float = 5.0,
                   variable_step: float = 0.0, end_time: str = "04:00:00",
                   pollutants: bool = False, files: str = "", storage: bool = False,
-                  regulators: bool = False) -> None:
+                  regulators: bool = False, shapes: bool = False,
+                  force_main_eqn: str = "") -> None:
     """Write the authored Example network (see module docstring).  `files`
     is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf");
     `storage` turns six junctions into storage units (_STORAGE)."""
@@ -326,6 +353,19 @@ def write_example(path: str, *, route_step: float = 5.0,
                           end_time=end_time, pollut=pollut,
                           qual_inflow=qual_inflow, qual_dwf=qual_dwf,
                           pollut_opt="")
+    if shapes:
+        out = []
+        for ln in txt.split("\n"):
+            t = ln.split()
+            if len(t) == 7 and t[0] in _SHAPES and not t[1][0].isdigit() and t[1] in (
+                    "CIRCULAR", "RECT_OPEN", "RECT_CLOSED", "TRAPEZOIDAL", "TRIANGULAR"):
+                ln = "%-4s %s  %s" % (t[0], _SHAPES[t[0]], t[6])
+            out.append(ln)
+        txt = "\n".join(out)
+        if force_main_eqn:
+            txt = txt.replace("[OPTIONS]\n", "[OPTIONS]\nFORCE_MAIN_EQUATION " + force_main_eqn + "\n", 1)
+            if force_main_eqn == "D-W":          # roughness height (in) instead of a C-factor
+                txt = txt.replace("FORCE_MAIN      1.0  120", "FORCE_MAIN      1.0  0.01")
     if regulators:
         storage = True
         out = []

@@ -65,6 +65,13 @@ CASES = {
     "example_regulators_var_qual": (netgen.write_example, dict(end_time="01:30:00", route_step=10.0,
                                                                variable_step=0.75, regulators=True,
                                                                pollutants=True), 1),
+    # every non-basic cross-section shape (xsect.c:216-2618) and a force main,
+    # fixed step / variable step with Darcy-Weisbach force-main friction
+    "example_shapes": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0,
+                                                  shapes=True), 1),
+    "example_shapes_var": (netgen.write_example, dict(end_time="02:00:00", route_step=10.0,
+                                                      variable_step=0.75, shapes=True,
+                                                      force_main_eqn="D-W", pollutants=True), 1),
     # swmm_setValue between steps: external inflow, outfall stage, routing step
     "example_api": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
                                                variable_step=0.75), 1),

@@ -130,3 +130,42 @@ def test_xsect_tables_match_reference():
     for name, row in zip(["A_Circ", "R_Circ", "Y_Circ", "S_Circ", "W_Circ"], mine):
         arr = (ctypes.c_double * 51).in_dll(L, name)
         np.testing.assert_array_equal(row, np.array(arr[:]), err_msg=name)
+
+
+def test_shape_tables_match_reference():
+    """The tabulated shapes' geometry (shape_tables.h, model data) equals the
+    reference's tables value for value."""
+    ref = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "oracle", "_ref", "libswmm5_ref.so")
+    if not os.path.exists(ref):
+        pytest.skip("reference build not present")
+    L = ctypes.CDLL(ref)
+    import re
+    hdr = open(os.path.join(swmm5.PKG_DIR, "csrc", "shape_tables.h")).read()
+    defs = dict((k, int(v)) for k, v in re.findall(r"#define (SWX_\w+) (\d+)", hdr))
+    body = hdr[hdr.index("SWX_SHAPE_TAB[SWX_SHAPE_TAB_LEN] = {") + 36:]
+    body = body[:body.index("};")]
+    flat = np.array([float.fromhex(x) for x in body.replace("\n", " ").split(",") if x.strip()])
+    assert flat.size == defs["SWX_SHAPE_TAB_LEN"]
+    names = {"EGG": "Egg", "HORSESHOE": "Horseshoe", "GOTHIC": "Gothic", "CATENARY": "Catenary",
+             "SEMIELLIP": "SemiEllip", "BASKETHANDLE": "BasketHandle", "SEMICIRC": "SemiCirc",
+             "HORIZ_ELLIPSE": "HorizEllipse", "VERT_ELLIPSE": "VertEllipse", "ARCH": "Arch"}
+    checked = 0
+    for key, off in defs.items():
+        m = re.fullmatch(r"SWX_TAB_(\w+)_([AYWRS])", key)
+        if not m:
+            continue
+        shape, role = m.groups()
+        n = defs[key + "_N"]
+        base = defs["SWX_TAB_" + shape]
+        cand = [role + "_" + names[shape], role + "_" + names[shape].replace("BasketHandle", "Baskethandle")]
+        for c in cand:
+            try:
+                arr = (ctypes.c_double * n).in_dll(L, c)
+                break
+            except ValueError:
+                arr = None
+        assert arr is not None, key
+        np.testing.assert_array_equal(flat[base + off:base + off + n], np.array(arr[:]), err_msg=key)
+        checked += 1
+    assert checked == 36
