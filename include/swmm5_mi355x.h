@@ -92,6 +92,17 @@ int    DLLEXPORT swmmx_setExchange(int (*fn)(double *buf, long n, int op, void *
  * current partition; returns the object count. */
 int    DLLEXPORT swmmx_getOwner(int objType, int *out, int n);
 
+/* Cross-section known-answer evaluation (test extension; needs no project).
+ * Builds a section of reference shape code `type` from the four [XSECTIONS]
+ * parameters p[4] (user units, length factor ucf, as xsect_setParams), then
+ * fn = 0 writes its 11 parameters (yFull wMax ywMax aFull rFull sFull sMax
+ * yBot aBot sBot rBot) to y; fn = 1..9 evaluates A(y), W(y), R(y), Y(A),
+ * R(A), S(A), A(S), dS/dA, yCrit(q) at the n points x into y, on the host
+ * (device = 0) or on the GPU with the kernels' code (device = 1).
+ * Returns 0, 211 for invalid parameters, 500 when the device call fails. */
+int    DLLEXPORT swmmx_xsect(int type, const double *p, double ucf, int fn,
+                             const double *x, double *y, int n, int device);
+
 #ifdef __cplusplus
 }
 #endif

@@ -967,6 +967,24 @@ int DLLEXPORT swmmx_getKernelBytes(double* out, int n)
     return G->router->kernelBytes(out, n);
 }
 
+int DLLEXPORT swmmx_xsect(int type, const double* p, double ucf, int fn, const double* x, double* y,
+                          int n, int device)
+{
+    Xsect xs;
+    double q[4] = {p[0], p[1], p[2], p[3]};
+    if (type < 0 || type > X_STREET || !setXsectParams(xs, type, q, ucf)) return 211;
+    if (fn == 0) {
+        const double v[11] = {xs.yFull, xs.wMax, xs.ywMax, xs.aFull, xs.rFull, xs.sFull, xs.sMax,
+                              xs.yBot, xs.aBot, xs.sBot, xs.rBot};
+        for (int i = 0; i < 11 && i < n; i++) y[i] = v[i];
+        return 0;
+    }
+    Geom g = geomOf(xs);
+    if (device) return xsectEvalDevice(g, fn, x, y, n);
+    for (int i = 0; i < n; i++) y[i] = evalXsect(g, fn, x[i], &SWX_CIRC_TABLES[0][0]);
+    return 0;
+}
+
 int DLLEXPORT swmmx_getBackend(char* buf, int size)
 {
     std::string s = (G && G->router && G->router->ok()) ? G->router->deviceName() : std::string("none");

@@ -903,7 +903,7 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
 // give every node update a large scratch segment (and throttle its waves), so
 // the other networks use a node update without them.
 template <bool kFirst, bool kGeneral>
-__global__ __launch_bounds__(kBlock) void k_node(Params p, int k)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_node(Params p, int k)
 {
     constexpr bool kStorage = kGeneral;
     if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
@@ -3389,6 +3389,39 @@ int Router::kernelBytes(double* out, int n)
         out[k] = d_->kcnt[k] ? d_->kbytesSum[k] / (double)d_->kcnt[k] : model;
     }
     return m;
+}
+
+// ---------------------------------------------------------------------------
+// Known-answer evaluation of the cross-section relations on the device
+// (swmmx_xsect with device = 1): the same xsect.h code the kernels run, with
+// the device's libm
+__global__ void k_xsect_eval(Geom g, int fn, const double* x, double* y, int n, const double* circ)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = evalXsect(g, fn, x[i], circ);
+}
+
+int xsectEvalDevice(const Geom& gh, int fn, const double* x, double* y, int n)
+{
+    if (n <= 0) return 0;
+    Geom g = gh;
+    double *dx = nullptr, *dy = nullptr, *dc = nullptr, *ds = nullptr;
+    size_t nb = (size_t)n * sizeof(double);
+    bool ok = hipMalloc(&dx, nb) == hipSuccess && hipMalloc(&dy, nb) == hipSuccess &&
+              hipMalloc(&dc, sizeof(double) * 5 * SWX_CIRC_N) == hipSuccess &&
+              hipMalloc(&ds, sizeof(double) * SWX_SHAPE_TAB_LEN) == hipSuccess;
+    if (ok) {
+        (void)hipMemcpy(dx, x, nb, hipMemcpyHostToDevice);
+        (void)hipMemcpy(dc, &SWX_CIRC_TABLES[0][0], sizeof(double) * 5 * SWX_CIRC_N, hipMemcpyHostToDevice);
+        (void)hipMemcpy(ds, SWX_SHAPE_TAB, sizeof(double) * SWX_SHAPE_TAB_LEN, hipMemcpyHostToDevice);
+        int off = shapeTabOffset(g.type);
+        g.tb = (off >= 0) ? ds + off : nullptr;
+        hipLaunchKernelGGL(k_xsect_eval, dim3((n + 255) / 256), dim3(256), 0, 0, g, fn, dx, dy, n, dc);
+        ok = hipDeviceSynchronize() == hipSuccess &&
+             hipMemcpy(y, dy, nb, hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    (void)hipFree(dx); (void)hipFree(dy); (void)hipFree(dc); (void)hipFree(ds);
+    return ok ? 0 : 500;
 }
 
 }  // namespace swx

@@ -99,4 +99,7 @@ private:
     std::string errMsg_, devName_;
 };
 
+// device evaluation of a cross-section relation (swmmx_xsect); 0 or 500
+int xsectEvalDevice(const Geom& g, int fn, const double* x, double* y, int n);
+
 }  // namespace swx

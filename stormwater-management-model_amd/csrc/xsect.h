@@ -526,36 +526,36 @@ SWX_HD_COLD double getSofA(const Geom& x, double a, const double* ct);
 SWX_HD_COLD double getRofYAll(const Geom& x, double y, const double* ct);
 
 // R(A) of every shape whose relation does not go through the section factor
-// (xsect.c:1112-1138); -1 for the shapes whose R(A) is (S(A)/A)^1.5.  Never
+// (xsect.c:1112-1138); false for the shapes whose R(A) is (S(A)/A)^1.5.  Never
 // calls back into getSofA, so the cold call graph stays acyclic.
 template <bool kAll = true>
-SWX_HD double rOfADirect(const Geom& x, double a, const double* ct)
+SWX_HD bool rOfADirect(const Geom& x, double a, const double* ct, double* r)
 {
     switch (x.type) {
-    case G_RECT_CLOSED: return rectClosedRofA(x, a);
-    case G_RECT_OPEN:   return a / (x.wMax + (2. - x.sBot) * a / x.wMax);
-    case G_TRAPEZOIDAL: return a / (x.yBot + trapYofA(x, a) * x.rBot);
-    case G_TRIANGULAR:  return a / (2. * sqrt(a / x.sBot) * x.rBot);
+    case G_RECT_CLOSED: { *r = rectClosedRofA(x, a); return true; }
+    case G_RECT_OPEN:   { *r = a / (x.wMax + (2. - x.sBot) * a / x.wMax); return true; }
+    case G_TRAPEZOIDAL: { *r = a / (x.yBot + trapYofA(x, a) * x.rBot); return true; }
+    case G_TRIANGULAR:  { *r = a / (2. * sqrt(a / x.sBot) * x.rBot); return true; }
     default: break;
     }
-    if (!kAll) return -1.0;
+    if (!kAll) return false;
     switch (x.type) {
-    case G_RECT_TRIANG: return rectTriangRofA(x, a);
-    case G_RECT_ROUND: return rectRoundRofA(x, a, ct);
-    case G_MOD_BASKET: return modBasketRofA(x, a, ct);
-    case G_PARABOLIC: return a / parabPofY(x, exYofA(x, a, ct));
-    case G_POWERFUNC: return a / powerPofY(x, exYofA(x, a, ct));
+    case G_RECT_TRIANG: { *r = rectTriangRofA(x, a); return true; }
+    case G_RECT_ROUND: { *r = rectRoundRofA(x, a, ct); return true; }
+    case G_MOD_BASKET: { *r = modBasketRofA(x, a, ct); return true; }
+    case G_PARABOLIC: { *r = a / parabPofY(x, exYofA(x, a, ct)); return true; }
+    case G_POWERFUNC: { *r = a / powerPofY(x, exYofA(x, a, ct)); return true; }
     case G_FILLED_CIRCULAR: {                 // R(Y(A)) (xsect.c:1116, 1046-1049)
         double y = filledCircYofA(x, a, ct);
-        if (x.yBot == 0.0) return x.rFull * lookup(y / x.yFull, SWX_TR(ct), SWX_CIRC_N);
-        return filledCircRofY(x, y, ct);
+        if (x.yBot == 0.0) { *r = x.rFull * lookup(y / x.yFull, SWX_TR(ct), SWX_CIRC_N); return true; }
+        { *r = filledCircRofY(x, y, ct); return true; }
     }
     default:
         if (isTabShape(x.type)) {
             TabDesc d = tabDesc(x);
-            if (d.rOfY) return x.rFull * lookup(exYofA(x, a, ct) / x.yFull, x.tb + d.r, d.nR);
+            if (d.rOfY) { *r = x.rFull * lookup(exYofA(x, a, ct) / x.yFull, x.tb + d.r, d.nR); return true; }
         }
-        return -1.0;
+        return false;
     }
 }
 
@@ -571,8 +571,8 @@ SWX_HD double getRofA(const Geom& x, double a, const double* ct)
     case G_TRIANGULAR:  return a / (2. * sqrt(a / x.sBot) * x.rBot);
     default: {
         if (kAll && !isBasicShape(x.type)) {
-            double r = rOfADirect<kAll>(x, a, ct);
-            if (r >= 0.0) return r;
+            double r;
+            if (rOfADirect<kAll>(x, a, ct, &r)) return r;
         }
         double cathy = getSofA<kAll>(x, a, ct);
         if (cathy < 1.E-6 || a < 1.E-6) return 0.0;
@@ -704,7 +704,8 @@ SWX_HD_COLD double getSofA(const Geom& x, double a, const double* ct)
         }
         if (a == 0.0) return 0.0;
         if (a <= 0.0) return 0.0;                  // xsect_getRofA's a <= 0 test
-        double r = rOfADirect<kAll>(x, a, ct);     // no shape reaching here has an S table
+        double r = 0.0;                            // no shape reaching here has an S table
+        if (!rOfADirect<kAll>(x, a, ct, &r)) r = 0.0;
         if (r < 1.E-6) return 0.0;
         return a * pow(r, 2. / 3.);
     }
@@ -1043,6 +1044,25 @@ SWX_HD double fmFricSlope(int eqn, const Geom& x, double v, double hrad)
     double re = 4.0 * hrad * v / 1.1E-5;
     double f = fmFricFactor(x.rBot, hrad, re);
     return f * x.sBot * v / hrad;
+}
+
+// Geometry evaluation for the known-answer tests (swmmx_xsect): fn 1 A(y),
+// 2 W(y), 3 R(y), 4 Y(A), 5 R(A), 6 S(A), 7 A(S), 8 dS/dA, 9 critical depth
+// at flow x (xsect_getAofY ... xsect_getYcrit, xsect.c:714-1319)
+SWX_HD_COLD double evalXsect(const Geom& g, int fn, double v, const double* ct)
+{
+    switch (fn) {
+    case 1: return getAofY(g, v, ct);
+    case 2: return getWofY(g, v, ct);
+    case 3: return getRofY(g, v, ct);
+    case 4: return getYofA(g, v, ct);
+    case 5: return getRofA(g, v, ct);
+    case 6: return getSofA(g, v, ct);
+    case 7: return getAofS(g, v, ct);
+    case 8: return getdSdA(g, v, ct);
+    case 9: return getYcrit(g, v, ct);
+    default: return 0.0;
+    }
 }
 
 }  // namespace swx

@@ -91,6 +91,7 @@ def load_library(path: str | None = None):
         "swmmx_setPartition": (c_int, [c_int, c_int, ctypes.c_void_p, c_int]),
         "swmmx_setExchange": (c_int, [ctypes.c_void_p, ctypes.c_void_p]),
         "swmmx_getOwner": (c_int, [c_int, P(c_int), c_int]),
+        "swmmx_xsect": (c_int, [c_int, P(c_dbl), c_dbl, c_int, P(c_dbl), P(c_dbl), c_int, c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -99,6 +100,23 @@ def load_library(path: str | None = None):
     if path is None:
         _lib = L
     return L
+
+
+def xsect(code: int, p, fn: int, x=None, device: bool = False):
+    """Evaluate cross-section relation fn (0 = the 11 section parameters,
+    1..9 = A(y) W(y) R(y) Y(A) R(A) S(A) A(S) dS/dA yCrit(q)) of a section of
+    reference shape `code` with [XSECTIONS] parameters p (swmmx_xsect)."""
+    import numpy as np
+    L = load_library()
+    pa = (ctypes.c_double * 4)(*[float(v) for v in p])
+    xs = np.ascontiguousarray(np.zeros(11) if x is None else x, dtype=np.float64)
+    ys = np.zeros(xs.size if fn else 11)
+    P = ctypes.POINTER(ctypes.c_double)
+    err = L.swmmx_xsect(code, pa, 1.0, fn, xs.ctypes.data_as(P), ys.ctypes.data_as(P), ys.size,
+                        1 if device else 0)
+    if err:
+        raise ValueError("swmmx_xsect error %d" % err)
+    return ys
 
 
 def exported_symbols() -> list:

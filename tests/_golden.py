@@ -28,6 +28,25 @@ DWF_ONLY = {"grid12", "grid12_var_qual", "grid10_surcharge"}
 GRID_CONC = [5.0, 10.0, 15.0, 20.0, 25.0, 30.0]
 
 
+# ill-conditioned cases: the fixture carries the reference's build-to-build
+# spread ("env.*", tests/golden/make_golden.py ENVELOPE)
+ENVELOPE = {"example_shapes", "example_shapes_var"}
+
+
+def first_divergence(d, node_f, link_f, rtol, atol):
+    """First recorded step index at which the reference's two builds (plain
+    and FMA) differ by more than the tolerance in any checked state array."""
+    n = len(d["env.node.newDepth"])
+    first = n
+    for pre, fs in (("node.", node_f), ("link.", link_f)):
+        for f in fs:
+            e, ref = d["env." + pre + f], d["s." + pre + f]
+            bad = np.nonzero(e > atol + rtol * np.abs(ref).max(axis=1))[0]
+            if bad.size:
+                first = min(first, int(bad[0]))
+    return first
+
+
 def load(name: str) -> dict:
     z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     return {k: z[k] for k in z.files}
@@ -44,6 +63,16 @@ def inp(name: str) -> str:
 
 def ref_out(name: str) -> bytes:
     return np.load(os.path.join(GOLDEN, name + ".ref_out.npy"), allow_pickle=False).tobytes()
+
+
+def fma_out(name: str) -> bytes:
+    """The reference FMA build's binary results (ill-conditioned cases)."""
+    return np.load(os.path.join(GOLDEN, name + ".fma_out.npy"), allow_pickle=False).tobytes()
+
+
+def fma_rpt(name: str) -> str:
+    with open(os.path.join(GOLDEN, name + ".fma_rpt.txt")) as f:
+        return f.read()
 
 
 def every(d: dict) -> int:

@@ -10,6 +10,10 @@ in a flow class, ...) may differ by a few steps where the two builds' libm
 ulps put a state on different sides of a class boundary; dates of maxima
 must agree for >= 97 % of objects (a plateau of equal maxima can move the
 first occurrence by one step).
+
+Ill-conditioned cases (_golden.ENVELOPE, see test_gpu_parity) also allow, per
+object, twice the difference between the reference's plain and FMA builds
+("env.st.*" in the fixture).
 """
 import numpy as np
 import pytest
@@ -36,11 +40,27 @@ def _run(name, tmp_path):
     return d, s
 
 
-def _dates_agree(a, b, frac=0.97, value=None, series=None, times=None):
+def _allow(d, key):
+    """Per-object extra tolerance: twice the reference's build-to-build spread."""
+    e = d.get("env." + key)
+    return 0.0 if e is None else 2.0 * e
+
+
+def _close(actual, d, key, rtol, atol, err_msg=""):
+    ref = d[key]
+    tol = atol + rtol * np.abs(ref) + _allow(d, key)
+    bad = np.abs(np.asarray(actual, dtype=np.float64) - ref) > tol
+    assert not bad.any(), "%s %s: %s vs %s" % (err_msg or key, np.nonzero(bad)[0][:8],
+                                              np.asarray(actual)[bad][:8], ref[bad][:8])
+
+
+def _dates_agree(a, b, frac=0.97, value=None, series=None, times=None, spread=None):
     """Dates of maxima: equal, or -- where a plateau of equal maxima lets a
     last-ulp difference pick another step -- a date at which the reference's
     own series also reaches its maximum (rtol 1e-6)."""
     same = np.isclose(a, b, rtol=0, atol=1e-9)
+    if spread is not None:
+        same |= spread > 0            # the reference's own builds disagree on this date
     if same.mean() >= frac:
         return
     assert value is not None, (same.mean(), np.nonzero(~same)[0][:10])
@@ -58,33 +78,34 @@ def test_stats_match_reference(name, tmp_path):
     g = lambda k: s.get_array(k)                      # noqa: E731
     for f in ("avgDepth", "maxDepth", "totLatFlow", "maxLatFlow", "maxInflow", "maxOverflow",
               "volFlooded", "maxPondedVol"):
-        np.testing.assert_allclose(g("stat.node." + f), d["st.node." + f], rtol=RTOL, atol=ATOL,
+        _close(g("stat.node." + f), d, "st.node." + f, rtol=RTOL, atol=ATOL,
                                    err_msg=f)
     for f in ("timeFlooded", "timeSurcharged"):
-        np.testing.assert_allclose(g("stat.node." + f), d["st.node." + f], rtol=0, atol=3 * dtmax + 1e-9,
+        _close(g("stat.node." + f), d, "st.node." + f, rtol=0, atol=3 * dtmax + 1e-9,
                                    err_msg=f)
-    np.testing.assert_array_equal(g("stat.node.nonConvergedCount"), d["st.node.nonConvergedCount"])
+    _close(g("stat.node.nonConvergedCount"), d, "st.node.nonConvergedCount", 0, 0)
     # report dates of the recorded steps (getDateTime, swmm5.c:1543)
     times = None
     if _golden.every(d) == 1:
         times = s.getValue(swmm5.STARTDATE, 0) + (d["s.time"] + 1.0) / 1000.0 / 86400.0
-    _dates_agree(g("stat.node.maxDepthDate"), d["st.node.maxDepthDate"],
+    _dates_agree(g("stat.node.maxDepthDate"), d["st.node.maxDepthDate"], spread=d.get("env.st.node.maxDepthDate"),
                  value=d["st.node.maxDepth"], series=d["s.node.newDepth"], times=times)
     _dates_agree(g("stat.node.maxInflowDate"), d["st.node.maxInflowDate"],
+                 spread=d.get("env.st.node.maxInflowDate"),
                  value=d["st.node.maxInflow"], series=d["s.node.inflow"], times=times)
     for f in ("avgFlow", "maxFlow"):
-        np.testing.assert_allclose(g("stat.outfall." + f), d["st.outfall." + f], rtol=RTOL, atol=ATOL,
+        _close(g("stat.outfall." + f), d, "st.outfall." + f, rtol=RTOL, atol=ATOL,
                                    err_msg=f)
     if "st.pump.utilized" in d and d["st.pump.utilized"].any():   # TPumpStats (stats.c:683-705)
         for f in ("utilized", "minFlow", "avgFlow", "maxFlow", "volume", "energy", "offCurveLow",
                   "offCurveHigh"):
-            np.testing.assert_allclose(g("stat.pump." + f), d["st.pump." + f], rtol=RTOL, atol=3 * dtmax + 1e-9
+            _close(g("stat.pump." + f), d, "st.pump." + f, rtol=RTOL, atol=3 * dtmax + 1e-9
                                        if f in ("utilized", "offCurveLow", "offCurveHigh") else ATOL, err_msg=f)
-        np.testing.assert_array_equal(g("stat.pump.startUps"), d["st.pump.startUps"])
-        np.testing.assert_allclose(g("stat.pump.totalPeriods"), d["st.pump.totalPeriods"], atol=2)
+        _close(g("stat.pump.startUps"), d, "st.pump.startUps", 0, 0)
+        _close(g("stat.pump.totalPeriods"), d, "st.pump.totalPeriods", 0, 2)
     if "st.storage.avgVol" in d:                       # TStorageStats (stats.c:590-603)
         for f in ("initVol", "avgVol", "maxVol", "maxFlow", "evapLosses"):
-            np.testing.assert_allclose(g("stat.storage." + f), d["st.storage." + f], rtol=RTOL, atol=ATOL,
+            _close(g("stat.storage." + f), d, "st.storage." + f, rtol=RTOL, atol=ATOL,
                                        err_msg=f)
         st = d["st.storage.avgVol"] != 0
         if times is None:
@@ -94,37 +115,40 @@ def test_stats_match_reference(name, tmp_path):
             vol = np.minimum(d["s.node.newVolume"], fv[None, :])
             _dates_agree(g("stat.storage.maxVolDate")[st], d["st.storage.maxVolDate"][st],
                          value=d["st.storage.maxVol"][st], series=vol[:, st], times=times)
-    np.testing.assert_allclose(g("stat.outfall.totalPeriods"), d["st.outfall.totalPeriods"], atol=2)
+    _close(g("stat.outfall.totalPeriods"), d, "st.outfall.totalPeriods", 0, 2)
     P = int(d["counts"][2])
     if P:
         nn = int(d["counts"][0])
         load = g("stat.outfall.totalLoad").reshape(P, nn)
         for p in range(P):
-            np.testing.assert_allclose(load[p], d["st.outfall.totalLoad%d" % p], rtol=1e-6, atol=1e-6)
+            _close(load[p], d, "st.outfall.totalLoad%d" % p, 1e-6, 1e-6)
     for f in ("maxFlow", "maxVeloc", "maxDepth"):
-        np.testing.assert_allclose(g("stat.link." + f), d["st.link." + f], rtol=RTOL, atol=ATOL,
+        _close(g("stat.link." + f), d, "st.link." + f, rtol=RTOL, atol=ATOL,
                                    err_msg=f)
     _dates_agree(g("stat.link.maxFlowDate"), d["st.link.maxFlowDate"], value=d["st.link.maxFlow"],
+                 spread=d.get("env.st.link.maxFlowDate"),
                  series=np.abs(d["s.link.newFlow"]) if times is not None else None, times=times)
     for f in ("timeNormalFlow", "timeSurcharged", "timeFullUpstream", "timeFullDnstream", "timeFullFlow",
               "timeCapacityLimited"):
-        np.testing.assert_allclose(g("stat.link." + f), d["st.link." + f], rtol=0, atol=3 * dtmax + 1e-9,
+        _close(g("stat.link." + f), d, "st.link." + f, rtol=0, atol=3 * dtmax + 1e-9,
                                    err_msg=f)
     nl = int(d["counts"][1])
     cls = g("stat.link.timeInFlowClass").reshape(7, nl)
     for k in range(7):
-        np.testing.assert_allclose(cls[k], d["st.link.timeInFlowClass%d" % k], rtol=0,
-                                   atol=3 * dtmax + 1e-9, err_msg="class %d" % k)
-    np.testing.assert_allclose(g("stat.link.flowTurns"), d["st.link.flowTurns"], atol=2)
+        _close(cls[k], d, "st.link.timeInFlowClass%d" % k, 0, 3 * dtmax + 1e-9, err_msg="class %d" % k)
+    _close(g("stat.link.flowTurns"), d, "st.link.flowTurns", 0, 2)
     sysv = g("stat.sys")
-    np.testing.assert_allclose(sysv[2], d["st.sys"][0], rtol=RTOL)   # MaxOutfallFlow
+    _close(sysv[2:3], {"st.sys0": d["st.sys"][:1], "env.st.sys0": d["env.st.sys"][:1]} if "env.st.sys" in d
+           else {"st.sys0": d["st.sys"][:1]}, "st.sys0", RTOL, 0)   # MaxOutfallFlow
     np.testing.assert_allclose(sysv[1], d["st.sys"][1], rtol=1e-12)  # RoutingTimeSpan
     # Courant-critical counts (variable step only): same total, same leaders
     crit_n = g("stat.node.timeCourantCritical")
     crit_l = g("stat.link.timeCourantCritical")
     ref_n, ref_l = d["st.node.timeCourantCritical"], d["st.link.timeCourantCritical"]
-    assert abs(crit_n.sum() + crit_l.sum() - ref_n.sum() - ref_l.sum()) <= 1
-    np.testing.assert_allclose(crit_n, ref_n, atol=3)
-    np.testing.assert_allclose(crit_l, ref_l, atol=3)
+    spread = (d["env.st.node.timeCourantCritical"].sum() + d["env.st.link.timeCourantCritical"].sum()
+              if "env.st.node.timeCourantCritical" in d else 0)
+    assert abs(crit_n.sum() + crit_l.sum() - ref_n.sum() - ref_l.sum()) <= 1 + 2 * spread
+    _close(crit_n, d, "st.node.timeCourantCritical", 0, 3)
+    _close(crit_l, d, "st.link.timeCourantCritical", 0, 3)
     s.end()
     s.close()
