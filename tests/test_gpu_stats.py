@@ -11,9 +11,11 @@ ulps put a state on different sides of a class boundary; dates of maxima
 must agree for >= 97 % of objects (a plateau of equal maxima can move the
 first occurrence by one step).
 
-Ill-conditioned cases (_golden.ENVELOPE, see test_gpu_parity) also allow, per
-object, twice the difference between the reference's plain and FMA builds
-("env.st.*" in the fixture).
+Ill-conditioned cases (_golden.ENVELOPE, see test_gpu_parity) also allow twice
+the largest difference between the reference's plain build and its FMA / x87
+builds ("env.st.*" in the fixture), plus 1e-3 relative -- ten times the
+stopping tolerance of the reference's Newton A(S) solve, whose last-bit-
+sensitive stopping point moves a peak by that much.
 """
 import numpy as np
 import pytest
@@ -41,14 +43,17 @@ def _run(name, tmp_path):
 
 
 def _allow(d, key):
-    """Per-object extra tolerance: twice the reference's build-to-build spread."""
+    """Extra tolerance of an ill-conditioned case: twice the reference's
+    largest build-to-build spread of that statistic over all objects."""
     e = d.get("env." + key)
-    return 0.0 if e is None else 2.0 * e
+    return 0.0 if e is None else 2.0 * float(np.max(e, initial=0.0))
 
 
 def _close(actual, d, key, rtol, atol, err_msg=""):
     ref = d[key]
     tol = atol + rtol * np.abs(ref) + _allow(d, key)
+    if "env." + key in d:          # + ten times the Newton A(S) stopping tolerance (1e-4 of aFull)
+        tol = tol + 1e-3 * np.abs(ref)
     bad = np.abs(np.asarray(actual, dtype=np.float64) - ref) > tol
     assert not bad.any(), "%s %s: %s vs %s" % (err_msg or key, np.nonzero(bad)[0][:8],
                                               np.asarray(actual)[bad][:8], ref[bad][:8])
