@@ -526,7 +526,7 @@ double DLLEXPORT swmm_getValue(int property, int index)   // swmm5.c:842-1213
         double uL = prj.ucfLength(), uQ = prj.ucfFlow();
         bool st = !s.lNewDepth.empty();
         const Xsect& x = n.xsect[index];
-        Geom g{x.type, x.yFull, x.wMax, x.ywMax, x.aFull, x.rFull, x.sFull, x.sMax, x.yBot, x.aBot, x.sBot, x.rBot};
+        Geom g = geomOf(x, n.xTab.data());
         const double* ct = &SWX_CIRC_TABLES[0][0];
         bool dyn = (property >= swmm_LINK_FLOW && property <= swmm_LINK_TOPWIDTH) ||
                    property == swmm_LINK_SETTING;

@@ -215,6 +215,9 @@ struct Params {
     // misc
     const double* gTables;        // global copy of the 5x51 circular tables
     const double* gShapeTab;      // SWX_SHAPE_TAB: tabulated shapes' geometry
+    const double* gXTab;          // transect / custom-shape table blocks (Network::xTab)
+    const int* lTabOff;           // per link: its block in gXTab (-1: none); null without any
+    const double* lengthRaw;      // Conduit.length as input (findLimitedLinks); = length unless irregular
     double* partials;             // [nBlocksEnd][kNumPartials]
     int nBlocksEnd;
     StatsDev st;
@@ -262,7 +265,8 @@ __device__ __forceinline__ Geom loadGeom(const Params& p, int j, uint32_t f)
     }
     if (!kFast && !isBasicShape(g.type)) {
         int off = shapeTabOffset(g.type);
-        g.tb = (off >= 0) ? p.gShapeTab + off : nullptr;
+        if (off >= 0) g.tb = p.gShapeTab + off;
+        else g.tb = (p.lTabOff && p.lTabOff[j] >= 0) ? p.gXTab + p.lTabOff[j] : nullptr;
     }
     return g;
 }
@@ -1532,7 +1536,7 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
             int2 nn = p.lnodes[j];
             double h1 = p.nNewDepth[nn.x] + p.inv1[j];
             double h2 = p.nNewDepth[nn.y] + p.inv2[j];
-            if ((h1 - h2) > fabs(p.slope[j]) * p.length[j]) s |= (1 << 9);
+            if ((h1 - h2) > fabs(p.slope[j]) * p.lengthRaw[j]) s |= (1 << 9);
         }
         p.lstate[j] = s;
         if (f & LF_SEEP) {
@@ -2244,7 +2248,9 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     UPD(tmp, xd[8], nL); p.aBot = tmp;
     UPD(tmp, xd[9], nL); p.sBot = tmp;
     UPD(tmp, xd[10], nL); p.rBot = tmp;
-    UPD(tmp, gl(net.length), nL); p.length = tmp;
+    UPD(tmp, gl(net.lengthT), nL); p.length = tmp;
+    p.lengthRaw = p.length;
+    if (net.length != net.lengthT) { UPD(tmp, gl(net.length), nL); p.lengthRaw = tmp; }
     UPD(tmp, gl(net.modLength), nL); p.modLength = tmp;
     UPD(tmp, gl(net.roughFactor), nL); p.roughFactor = tmp;
     UPD(tmp, gl(net.beta), nL); p.beta = tmp;
@@ -2527,6 +2533,16 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         UPD(tmp, t, t.size()); p.gTables = tmp;
         std::vector<double> st(SWX_SHAPE_TAB, SWX_SHAPE_TAB + SWX_SHAPE_TAB_LEN);
         UPD(tmp, st, st.size()); p.gShapeTab = tmp;
+        p.gXTab = nullptr;
+        p.lTabOff = nullptr;
+        if (!prj.net.xTab.empty()) {
+            UPD(tmp, prj.net.xTab, prj.net.xTab.size()); p.gXTab = tmp;
+            std::vector<int> off(nL, -1);
+            for (int j = 0; j < nL; j++) off[j] = prj.net.xsect[LL[j]].tabOff;
+            int* o;
+            UPI(o, off, nL);
+            p.lTabOff = o;
+        }
     }
     if (const char* w = getenv("SWMM5_LINK_WAVES")) d->linkWaves = atoi(w);
     for (int j = 0; j < nL; j++)

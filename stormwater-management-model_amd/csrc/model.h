@@ -129,6 +129,22 @@ struct Xsect {
     int type = -1, culvertCode = 0;
     double yFull = 0, wMax = 0, ywMax = 0, aFull = 0, rFull = 0, sFull = 0, sMax = 0;
     double yBot = 0, aBot = 0, sBot = 0, rBot = 0;
+    int transect = -1;     // IRREGULAR: transect, CUSTOM: shape curve, STREET: street
+    int tabOff = -1;       // its table block in Network::xTab (set at validation)
+};
+
+// Geometry tables of an irregular-channel transect (TTransect, objects.h:
+// 602-622), a custom shape curve (TShape, objects.h:646-660) or a street's
+// transect: relative area, hydraulic radius and top width at nTbl equally
+// spaced depths, plus the section's full / maximum values.
+struct XTable {
+    std::string id;
+    double yFull = 0, aFull = 0, rFull = 0, wMax = 0, ywMax = 0, sMax = 0, aMax = 0,
+           lengthFactor = 1.0, roughness = 0;
+    int nTbl = 0;
+    bool valid = false;
+    std::vector<double> area, hrad, width;
+    int blockOff = -1;     // its [n][A n][W n][R n] block in Network::xTab
 };
 
 // ---- the network --------------------------------------------------------
@@ -162,6 +178,7 @@ struct Network {
         superCritical, linkRpt;
     std::vector<double> offset1, offset2, q0, qLimit, cLossInlet, cLossOutlet, cLossAvg,
         seepRate, length, roughness, modLength, roughFactor, slope, beta, qMax, qFull;
+    std::vector<double> lengthT;      // conduit_getLength: length / transect lengthFactor
     std::vector<Xsect> xsect;
     // pumps / orifices / weirs / outlets (link.c:315-399), indexed by link:
     // sub-type (pump type, orifice type, weir type, outlet curve type), curve
@@ -177,8 +194,14 @@ struct Network {
     std::vector<Pattern> patterns;
     std::vector<Tseries> tseries;
     std::vector<Curve> curves;
+    // irregular cross sections: [TRANSECTS] and SHAPE curves (curveShape: the
+    // shape of each curve, -1 for other curve types); xTab holds every table
+    // block the kernels read (xsect.h tabDesc)
+    std::vector<XTable> transects, shapes;
+    std::vector<int> curveShape;
+    std::vector<double> xTab;
     std::unordered_map<std::string, int> nodeIndex, linkIndex, pollutIndex, patternIndex,
-        tseriesIndex, curveIndex;
+        tseriesIndex, curveIndex, transectIndex;
     std::string title;
 
     int nNodes() const { return (int)nodeId.size(); }

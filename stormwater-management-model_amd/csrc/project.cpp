@@ -210,12 +210,12 @@ static bool getDouble(const char* s, double* y)
 enum Sect {
     S_NONE = -1, S_TITLE, S_OPTION, S_EVAP, S_JUNC, S_OUTFALL, S_CONDUIT, S_XSECT, S_LOSS,
     S_POLLUT, S_INFLOW, S_DWF, S_PATTERN, S_TSERIES, S_REPORT, S_FILES, S_STORAGE, S_CURVES,
-    S_PUMP, S_ORIFICE, S_WEIR, S_OUTLET, S_SKIP, S_UNSUPPORTED
+    S_PUMP, S_ORIFICE, S_WEIR, S_OUTLET, S_TRANSECT, S_SKIP, S_UNSUPPORTED
 };
 static const char* const kSectWords[] = {
     "[TITLE", "[OPTION", "[EVAP", "[JUNC", "[OUTFALL", "[CONDUIT", "[XSECT", "[LOSS",
     "[POLLUT", "[INFLOW", "[DWF", "[PATTERN", "[TIMESERIES", "[REPORT", "[FILES", "[STORAGE",
-    "[CURVE", "[PUMP", "[ORIFICE", "[WEIR", "[OUTLET", nullptr};
+    "[CURVE", "[PUMP", "[ORIFICE", "[WEIR", "[OUTLET", "[TRANSECT", nullptr};
 static const char* const kOffOnWords[] = {"OFF", "ON", nullptr};
 static const char* const kOrificeTypeWords[] = {"SIDE", "BOTTOM", nullptr};
 static const char* const kWeirTypeWords[] = {"TRANSVERSE", "SIDEFLOW", "V-NOTCH", "TRAPEZOIDAL",
@@ -225,6 +225,7 @@ static const char* const kRelationWords[] = {"TABULAR", "FUNCTIONAL", "CYLINDRIC
 static const char* const kCurveTypeWords[] = {"STORAGE", "DIVERSION", "TIDAL", "RATING", "CONTROL",
                                               "SHAPE", "WEIR", "PUMP1", "PUMP2", "PUMP3", "PUMP4",
                                               "PUMP5", nullptr};
+static const char* const kTransectWords[] = {"NC", "X1", "GR", nullptr};
 static const char* const kSkipWords[] = {
     "[MAP", "[COORDINATE", "[VERTICES", "[POLYGON", "[SYMBOL", "[LABEL", "[BACKDROP", "[TAG",
     "[PROFILE", nullptr};
@@ -350,7 +351,15 @@ int Project::readFile(const char* path)
             if (nt == 0 || tok[0][0] == ';') continue;
             if (tok[0][0] == '[') {
                 int s = kfind(tok[0], kSectWords);
-                if (s >= 0) { sect = s; continue; }
+                if (s >= 0) {
+                    // input.c:210-213 -- finish the last transect
+                    if (sect == S_TRANSECT && pass == 2) {
+                        validateTransect(tin_.count - 1);
+                        if (errorCode) return errorCode;
+                    }
+                    sect = s;
+                    continue;
+                }
                 if (kfind(tok[0], kSkipWords) >= 0) { sect = S_SKIP; continue; }
                 return setError(200, std::string("ERROR 200: input section ") + tok[0] +
                                           " is not supported by the MI355X dynamic-wave engine");
@@ -388,7 +397,7 @@ int Project::readFile(const char* path)
             net.hasFlapGate.assign(nl, 0); net.direction.assign(nl, 1); net.barrels.assign(nl, 1);
             net.hasLosses.assign(nl, 0); net.superCritical.assign(nl, 0); net.linkRpt.assign(nl, 0);
             for (auto* v : {&net.offset1, &net.offset2, &net.q0, &net.qLimit, &net.cLossInlet,
-                            &net.cLossOutlet, &net.cLossAvg, &net.seepRate, &net.length,
+                            &net.cLossOutlet, &net.cLossAvg, &net.seepRate, &net.length, &net.lengthT,
                             &net.roughness, &net.modLength, &net.roughFactor, &net.slope,
                             &net.beta, &net.qMax, &net.qFull})
                 v->assign(nl, 0.0);
@@ -428,6 +437,16 @@ int Project::parseLine(int sect, std::vector<char*>& tok, int pass)
         case S_OUTFALL:
         case S_STORAGE:
             if (addId(net.nodeIndex, net.nodeId, tok[0]) < 0) return setError(207, std::string("ERROR 207: duplicate ID name ") + tok[0]);
+            return 0;
+        case S_TRANSECT:
+            if (kfind(tok[0], kTransectWords) == 1 && nt >= 2) {
+                if (net.transectIndex.count(tok[1]))
+                    return setError(207, std::string("ERROR 207: duplicate ID name ") + tok[1]);
+                net.transectIndex.emplace(tok[1], (int)net.transects.size());
+                XTable t;
+                t.id = tok[1];
+                net.transects.push_back(t);
+            }
             return 0;
         case S_CURVES:
             if (!net.curveIndex.count(tok[0])) {
@@ -492,6 +511,7 @@ int Project::parseLine(int sect, std::vector<char*>& tok, int pass)
     case S_STORAGE: return readStorage(tok);
     case S_PUMP: case S_ORIFICE: case S_WEIR: case S_OUTLET: return readRegulator(sect, tok);
     case S_CURVES: return readCurve(tok);
+    case S_TRANSECT: return readTransect(tok);
     default: return 0;
     }
 }
@@ -792,6 +812,317 @@ int Project::readCurve(std::vector<char*>& tok)
         c.y.push_back(y);
     }
     return 0;
+}
+
+// ======================================================== irregular sections
+// transect_readParams (transect.c:105-190): NC / X1 / GR lines, HEC-2 format
+int Project::readTransect(std::vector<char*>& tok)
+{
+    int nt = (int)tok.size();
+    TransectInput& T = tin_;
+    int k = kfind(tok[0], kTransectWords);
+    if (k < 0) return 205;
+    double u = ucfLength();
+    if (k == 0) {                                       // NC nLeft nRight nChannel
+        validateTransect(T.count - 1);
+        if (errorCode) return errorCode;
+        if (nt < 4) return 203;
+        double n[4];
+        for (int i = 1; i <= 3; i++)
+            if (!getDouble(tok[i], &n[i])) return 211;
+        for (int i = 1; i <= 3; i++)                    // setManning transect.c:312-330
+            if (n[i] < 0.0) return 211;
+        if (n[1] > 0.0) T.nLeft = n[1];
+        if (n[2] > 0.0) T.nRight = n[2];
+        if (n[3] > 0.0) T.nChannel = n[3];
+        if (T.nLeft == 0.0) T.nLeft = T.nChannel;
+        if (T.nRight == 0.0) T.nRight = T.nChannel;
+        return 0;
+    }
+    if (k == 1) {                                       // X1 name nSta xLeft xRight 0 0 0 lFactor xFactor yFactor
+        if (nt < 10) return 203;
+        auto it = net.transectIndex.find(tok[1]);
+        if (it == net.transectIndex.end()) return 209;
+        double x[10];
+        for (int i = 2; i < 10; i++)
+            if (!getDouble(tok[i], &x[i])) return 211;
+        int idx = T.count;
+        T.count = idx + 1;
+        if (idx < 0 || idx >= (int)net.transects.size()) return 211;   // setParams transect.c:334-356
+        T.xLeft = x[3] / u;
+        T.xRight = x[4] / u;
+        T.lFactor = x[7];
+        if (T.lFactor == 0.0) T.lFactor = 1.0;
+        T.xFactor = x[8];
+        if (T.xFactor == 0.0) T.xFactor = 1.0;
+        T.xLeft *= T.xFactor;
+        T.xRight *= T.xFactor;
+        T.yFactor = x[9] / u;
+        T.nStations = 0;
+        T.station.assign(1, 0.0);
+        T.elev.assign(1, 0.0);
+        return 0;
+    }
+    if ((nt - 1) % 2 > 0) return 203;                   // GR elev station ...
+    for (int i = 1; i < nt; i += 2) {
+        double y, x;
+        if (!getDouble(tok[i], &y)) return 211;
+        if (!getDouble(tok[i + 1], &x)) return 211;
+        if (T.nStations < 0) return 219;                // addStation transect.c:360-384
+        T.nStations++;
+        if (T.nStations >= 1500) continue;
+        T.station.resize(T.nStations + 2, 0.0);
+        T.elev.resize(T.nStations + 2, 0.0);
+        T.station[T.nStations] = x * T.xFactor / u;
+        T.elev[T.nStations] = (y + T.yFactor) / u;
+        if (T.nStations > 1 && T.station[T.nStations] < T.station[T.nStations - 1]) return 221;
+    }
+    return 0;
+}
+
+namespace {
+// the transect under construction (transect.c's file-scope arrays)
+struct Slices {
+    const std::vector<double>& st;
+    const std::vector<double>& el;
+    int n;
+    double nLeft, nRight, nChannel, xLeft, xRight;
+};
+// getFlow (transect.c:519-566)
+double sliceFlow(const Slices& S, int k, double a, double wp, bool findFlow)
+{
+    if (!findFlow) {
+        if (k == S.n - 1) findFlow = true;
+        else if (S.st[k] == S.xLeft) {
+            if (S.nLeft != S.nChannel && S.st[k] != S.st[k - 1]) findFlow = true;
+        } else if (S.st[k] == S.xRight) {
+            if (S.nRight != S.nChannel && S.st[k] != S.st[k + 1]) findFlow = true;
+        }
+    }
+    if (findFlow) {
+        double n = S.nChannel;
+        if (S.st[k - 1] < S.xLeft) n = S.nLeft;
+        if (S.st[k] > S.xRight) n = S.nRight;
+        return kPhi / n * a * pow(a / wp, 2. / 3.);
+    }
+    return 0.0;
+}
+// createTables / getGeometry / getSliceGeom / setMaxSectionFactor
+// (transect.c:264-308, 388-515, 570-592)
+void transectTables(XTable& t, const Slices& S, double ymin, double ymax)
+{
+    int n = t.nTbl;
+    t.area.assign(n, 0.0);
+    t.hrad.assign(n, 0.0);
+    t.width.assign(n, 0.0);
+    t.yFull = ymax - ymin;
+    t.wMax = 0.0;
+    double dy = (ymax - ymin) / ((double)n - 1), y = ymin;
+    for (int i = 1; i < n; i++) {
+        y += dy;
+        double wpSum = 0.0, aSum = 0.0, qSum = 0.0;
+        for (int k = 1; k <= S.n; k++) {
+            double yhi, ylo;
+            if (S.el[k - 1] >= S.el[k]) { yhi = S.el[k - 1]; ylo = S.el[k]; }
+            else { yhi = S.el[k]; ylo = S.el[k - 1]; }
+            if (ylo >= y) continue;
+            double width = fabs(S.st[k] - S.st[k - 1]);
+            double w = width, wp = sqrt(width * width + (yhi - ylo) * (yhi - ylo)), a = 0.0;
+            if (y > yhi) a = width * ((y - yhi) + (y - ylo)) / 2.0;
+            else if (yhi > ylo) {
+                double ratio = (y - ylo) / (yhi - ylo);
+                a = width * (yhi - ylo) / 2.0 * ratio * ratio;
+                w *= ratio;
+                wp *= ratio;
+            }
+            wpSum += wp;
+            aSum += a;
+            t.area[i] += a;
+            t.width[i] += w;
+            double q = sliceFlow(S, k, aSum, wpSum, S.el[k] >= y);
+            if (q > 0.0) {
+                qSum += q;
+                aSum = 0.0;
+                wpSum = 0.0;
+            }
+        }
+        aSum = t.area[i];
+        if (aSum == 0.0) t.hrad[i] = t.hrad[i - 1];
+        else t.hrad[i] = pow(qSum * S.nChannel / 1.49 / aSum, 1.5);
+    }
+    t.aMax = 0.0;
+    t.sMax = 0.0;
+    for (int i = 1; i < n; i++) {
+        double sf = t.area[i] * pow(t.hrad[i], 2. / 3.);
+        if (sf > t.sMax) { t.sMax = sf; t.aMax = t.area[i]; }
+    }
+    int nLast = n - 1;
+    t.aFull = t.area[nLast];
+    t.rFull = t.hrad[nLast];
+    t.wMax = t.width[nLast];
+    for (int i = 1; i <= nLast; i++) {
+        t.area[i] /= t.aFull;
+        t.hrad[i] /= t.rFull;
+        t.width[i] /= t.wMax;
+    }
+    t.width[0] = t.width[1];
+}
+
+// shape.c:42-330 -- geometry tables of a custom shape curve (relative
+// height vs relative width)
+bool shapeTables(XTable& t, const Curve& c)
+{
+    size_t next = 0;
+    auto nextEntry = [&](double* x, double* y) {
+        if (next >= c.x.size()) return false;
+        *x = c.x[next];
+        *y = c.y[next];
+        next++;
+        return true;
+    };
+    double Atotal = 0.0, Ptotal = 0.0;
+    auto area = [](double y, double w, double y1, double w1) {
+        double wMin, wMax;
+        if (w > w1) { wMin = w1; wMax = w; } else { wMin = w; wMax = w1; }
+        return (wMin + (wMax - wMin) / 2.0) * (y - y1);
+    };
+    auto perim = [](double y, double w, double y1, double w1) {
+        double dy = y - y1, dw = fabs(w - w1) / 2.0;
+        return 2.0 * sqrt(dy * dy + dw * dw);
+    };
+    double y1, w1, y2, w2;
+    if (!nextEntry(&y1, &w1)) return false;
+    if (y1 < 0.0 || y1 >= 1.0 || w1 < 0.0) return false;
+    double wMax = w1;
+    if (y1 != 0.0) {
+        y2 = y1; w2 = w1; y1 = 0.0; w1 = 0.0;
+    } else {
+        if (!nextEntry(&y2, &w2)) return false;
+        if (y2 < y1 || w2 < 0.0) return false;
+        if (y2 > 1.0) y2 = 1.0;
+        if (w2 > wMax) wMax = w2;
+    }
+    t.nTbl = 51;
+    int n = t.nTbl - 1;
+    double dy = 1.0 / (double)(n);
+    t.area.assign(t.nTbl, 0.0);
+    t.hrad.assign(t.nTbl, 0.0);
+    t.width.assign(t.nTbl, 0.0);
+    t.width[0] = w1;
+    Ptotal = w1;
+    Atotal = 0.0;
+    double y = 0.0, w = w1;
+    for (int i = 1; i <= n; i++) {
+        double yLast = y, wLast = w;
+        y = y + dy;
+        if (fabs(y - 1.0) < 1.E-6) y = 1.0;
+        if (y > y2) {                                     // getNextInterval shape.c:270-310
+            while (y > y2) {
+                if (y2 > yLast) {
+                    Atotal += area(y2, w2, yLast, wLast);
+                    Ptotal += perim(y2, w2, yLast, wLast);
+                    yLast = y2;
+                    wLast = w2;
+                }
+                y1 = y2;
+                w1 = w2;
+                if (!nextEntry(&y2, &w2)) { y2 = 1.0; break; }
+                if (w2 > wMax) wMax = w2;
+                if (y2 < y1 || w2 < 0.0) return false;
+                if (y2 > 1.0) y2 = 1.0;
+            }
+            yLast = y1;
+            wLast = w1;
+        }
+        w = (y2 == y1) ? w2 : w1 + (y - y1) / (y2 - y1) * (w2 - w1);
+        Atotal += area(y, w, yLast, wLast);
+        Ptotal += perim(y, w, yLast, wLast);
+        if (y == 1.0) Ptotal += w2;
+        t.width[i] = w;
+        t.area[i] = Atotal;
+        t.hrad[i] = (Ptotal > 0.0) ? Atotal / Ptotal : 0.0;
+    }
+    t.aFull = t.area[n];
+    t.rFull = t.hrad[n];
+    t.wMax = wMax;
+    t.sMax = 0.0;
+    t.aMax = 0.0;
+    for (int i = 1; i <= n; i++) {
+        double sf = t.area[i] * pow(t.hrad[i], 2. / 3.);
+        if (sf > t.sMax) { t.sMax = sf; t.aMax = t.area[i]; }
+    }
+    if (t.aFull == 0.0 || t.rFull == 0.0 || t.wMax == 0.0) return false;
+    for (int i = 0; i <= n; i++) {
+        t.area[i] /= t.aFull;
+        t.hrad[i] /= t.rFull;
+        t.width[i] /= t.wMax;
+    }
+    return true;
+}
+}  // namespace
+
+// transect_validate (transect.c:194-260)
+void Project::validateTransect(int j)
+{
+    TransectInput& T = tin_;
+    double oldNchannel = T.nChannel;
+    if (j < 0 || j >= (int)net.transects.size()) return;
+    XTable& t = net.transects[j];
+    const std::string id = t.id;
+    if (T.nStations < 2) { setError(223, "ERROR 223: transect " + id + " has too few stations."); return; }
+    if (T.nStations >= 1500) { setError(225, "ERROR 225: transect " + id + " has too many stations."); return; }
+    if (T.nChannel <= 0.0) { setError(227, "ERROR 227: transect " + id + " has no Manning's N."); return; }
+    if (T.xLeft > T.xRight) { setError(229, "ERROR 229: transect " + id + " has invalid overbank locations."); return; }
+    T.nChannel = T.nChannel * sqrt(T.lFactor);
+    t.lengthFactor = T.lFactor;
+    double ymax = T.elev[1], ymin = T.elev[1];
+    for (int i = 2; i <= T.nStations; i++) {
+        ymax = gmax(T.elev[i], ymax);
+        ymin = gmin(T.elev[i], ymin);
+    }
+    if (ymin >= ymax) { setError(231, "ERROR 231: transect " + id + " has no depth."); return; }
+    T.station.resize(T.nStations + 2, 0.0);
+    T.elev.resize(T.nStations + 2, 0.0);
+    T.station[0] = T.station[1];
+    T.elev[0] = ymax;
+    T.nStations++;
+    T.station[T.nStations] = T.station[T.nStations - 1];
+    T.elev[T.nStations] = T.elev[0];
+    t.nTbl = 51;
+    Slices S{T.station, T.elev, T.nStations, T.nLeft, T.nRight, T.nChannel, T.xLeft, T.xRight};
+    transectTables(t, S, ymin, ymax);
+    t.roughness = oldNchannel;
+    t.valid = true;
+}
+
+// shape curves (project.c:220-231) and the device table blocks of every
+// transect and shape: [n][A n][W n][R n] (xsect.h tabDesc)
+void Project::buildXTables()
+{
+    net.curveShape.assign(net.curves.size(), -1);
+    net.shapes.clear();
+    for (size_t i = 0; i < net.curves.size(); i++) {
+        if (net.curves[i].type != CV_SHAPE) continue;
+        XTable t;
+        t.id = net.curves[i].id;
+        net.curveShape[i] = (int)net.shapes.size();
+        if (!shapeTables(t, net.curves[i])) {
+            setError(171, "ERROR 171: Curve " + net.curves[i].id + " has invalid or out of sequence data.");
+            return;
+        }
+        t.valid = true;
+        net.shapes.push_back(t);
+    }
+    net.xTab.clear();
+    for (auto* v : {&net.transects, &net.shapes})
+        for (XTable& t : *v) {
+            if (t.nTbl <= 0) continue;
+            t.blockOff = (int)net.xTab.size();
+            net.xTab.push_back((double)t.nTbl);
+            net.xTab.insert(net.xTab.end(), t.area.begin(), t.area.end());
+            net.xTab.insert(net.xTab.end(), t.width.begin(), t.width.end());
+            net.xTab.insert(net.xTab.end(), t.hrad.begin(), t.hrad.end());
+        }
 }
 
 int Project::readOutfall(std::vector<char*>& tok)  // node.c:1333-1409
@@ -1261,6 +1592,8 @@ bool setXsectParams(Xsect& x, int type, double p[4], double ucf)
         x.sMax = x.sFull;
         x.ywMax = 0.28 * x.yFull;
         break;
+    case X_CUSTOM:                  // parameters come from its shape curve (conduit_validate)
+        break;
     default:
         return false;
     }
@@ -1278,11 +1611,26 @@ int Project::readXsect(std::vector<char*>& tok)  // link.c:162-267
     if (k < 0) return 205;
     if (net.linkType[j] == CONDUIT) net.barrels[j] = 1;
     net.xsect[j].culvertCode = 0;
-    if (k == X_IRREGULAR || k == X_CUSTOM || k == X_STREET)
+    if (k == X_STREET)
         return setError(200, std::string("ERROR 200: cross-section shape ") + tok[1] +
                                  " is not supported by the MI355X engine yet");
+    if (k == X_IRREGULAR) {                            // link.c:196-203
+        auto t = net.transectIndex.find(tok[2]);
+        if (t == net.transectIndex.end()) return 209;
+        net.xsect[j].type = k;
+        net.xsect[j].transect = t->second;
+        return 0;
+    }
     if (nt < 6) return 203;
-    double x[4];
+    double x[4] = {0, 0, 0, 0};
+    if (k == X_CUSTOM) {                               // link.c:221-230
+        if (!getDouble(tok[2], &x[0]) || x[0] <= 0.0) return 211;
+        auto c = net.curveIndex.find(tok[3]);
+        if (c == net.curveIndex.end()) return 209;
+        net.xsect[j].type = k;
+        net.xsect[j].transect = c->second;
+        net.xsect[j].yFull = x[0] / ucfLength();
+    } else
     for (int i = 2; i <= 5; i++)
         if (!getDouble(tok[i], &x[i - 2])) return 211;
     if (net.linkType[j] != CONDUIT && k == X_RECT_OPEN) { x[2] = 0.0; x[3] = 0.0; }
@@ -1692,7 +2040,7 @@ int Project::readReport(std::vector<char*>& tok)  // report.c:report_readOptions
 // link.c:1258-1300
 static double conduitSlope(const Network& n, int j, const Options& o, int* warn)
 {
-    double length = n.length[j];
+    double length = n.lengthT[j];               // conduit_getLength
     double elev1 = n.offset1[j] + n.invertElev[n.node1[j]];
     double elev2 = n.offset2[j] + n.invertElev[n.node2[j]];
     double delta = fabs(elev1 - elev2), slope;
@@ -1708,6 +2056,49 @@ void Project::validateConduit(int j)  // link.c:992-1154 (supported shapes)
 {
     Xsect& xs = net.xsect[j];
     if (xs.type < 0) { setError(117, "ERROR 117: no cross section defined for link " + net.linkId[j]); return; }
+    const XTable* tt = nullptr;
+    if (xs.type == X_CUSTOM) {                         // xsect_setCustomXsectParams xsect.c:664-696
+        int sh = (xs.transect >= 0 && xs.transect < (int)net.curveShape.size()) ? net.curveShape[xs.transect] : -1;
+        if (sh < 0) { setError(119, "ERROR 119: invalid cross section for link " + net.linkId[j]); return; }
+        const XTable& t = net.shapes[sh];
+        double yFull = xs.yFull;
+        xs.wMax = t.wMax * yFull;
+        xs.aFull = t.aFull * yFull * yFull;
+        xs.rFull = t.rFull * yFull;
+        xs.sFull = xs.aFull * pow(xs.rFull, 2. / 3.);
+        xs.sMax = t.sMax * yFull * yFull * pow(yFull, 2. / 3.);
+        xs.aBot = t.aMax * yFull * yFull;
+        tt = &t;
+    } else if (xs.type == X_IRREGULAR) {               // getTransectParams xsect.c:1323-1355
+        const XTable& t = net.transects[xs.transect];
+        xs.yFull = t.yFull;
+        xs.wMax = t.wMax;
+        xs.aFull = t.aFull;
+        xs.rFull = t.rFull;
+        xs.sFull = xs.aFull * pow(xs.rFull, 2. / 3.);
+        xs.sMax = t.sMax;
+        xs.aBot = t.aMax;
+        net.roughness[j] = t.roughness;
+        tt = &t;
+    }
+    if (tt) {
+        // search the width table up to where the width decreases; depth of
+        // the lowest widest point (xsect.c:684-695, 1343-1354)
+        int iMax = 0;
+        double wMax = tt->width.empty() ? 0.0 : tt->width[0];
+        for (int i = 1; i < tt->nTbl; i++) {
+            if (tt->width[i] < wMax) break;
+            wMax = tt->width[i];
+            iMax = i;
+        }
+        if (xs.type == X_CUSTOM) xs.ywMax = xs.yFull * (double)iMax / (double)(51 - 1);
+        else xs.ywMax = xs.yFull * (double)iMax / ((double)(tt->nTbl) - 1);
+        xs.tabOff = tt->blockOff;
+    }
+    // conduit_getLength (link.c:1195-1206): irregular channels use the flood
+    // plain's length
+    net.lengthT[j] = net.length[j];
+    if (xs.type == X_IRREGULAR) net.lengthT[j] = net.length[j] / net.transects[xs.transect].lengthFactor;
     if (net.length[j] <= 0.0) { setError(111, "ERROR 111: invalid length for Conduit " + net.linkId[j]); return; }
     if (net.roughness[j] <= 0.0) { setError(113, "ERROR 113: invalid roughness for Conduit " + net.linkId[j]); return; }
     if (net.barrels[j] <= 0) { setError(114, "ERROR 114: invalid number of barrels for Conduit " + net.linkId[j]); return; }
@@ -1733,6 +2124,8 @@ void Project::validateConduit(int j)  // link.c:992-1154 (supported shapes)
         net.q0[j] = -net.q0[j];
     }
     double roughness = net.roughness[j];
+    if (xs.type == X_IRREGULAR)                        // meandering channels (link.c:1097-1102)
+        roughness *= sqrt(net.transects[xs.transect].lengthFactor);
     if (xs.type == X_FORCE_MAIN) {                     // forcemain_getEquivN forcmain.c:30-47
         double d = xs.yFull;
         if (opt.forceMainEqn == FM_H_W) roughness = 1.067 / xs.rBot * pow(d / net.slope[j], 0.04);
@@ -1743,17 +2136,17 @@ void Project::validateConduit(int j)  // link.c:992-1154 (supported shapes)
     }
     double lengthFactor = 1.0;
     if (opt.lengtheningStep > 0.0 && xs.type != X_DUMMY) {   // link.c:1217-1254
-        Geom g = geomOf(xs);
+        Geom g = geomOf(xs, net.xTab.data());
         double yFull = xs.yFull;
         if (isOpen(xs.type)) yFull = xs.aFull / getWofY(g, yFull, &SWX_CIRC_TABLES[0][0]);
         double vFull = kPhi / roughness * xs.sFull * sqrt(fabs(net.slope[j])) / xs.aFull;
         double tStep = (opt.lengtheningStep == 0.0) ? opt.routeStep
                                                     : gmin(opt.routeStep, opt.lengtheningStep);
-        double ratio = (sqrt(kGravity * yFull) + vFull) * tStep / net.length[j];
+        double ratio = (sqrt(kGravity * yFull) + vFull) * tStep / net.lengthT[j];
         lengthFactor = ratio > 1.0 ? ratio : 1.0;
     }
     if (lengthFactor != 1.0) {
-        net.modLength[j] = lengthFactor * net.length[j];
+        net.modLength[j] = lengthFactor * net.lengthT[j];
         slope /= lengthFactor;
         roughness = roughness / sqrt(lengthFactor);
     }
@@ -1852,6 +2245,17 @@ void Project::validate()  // project.c:186-270
     for (auto& ts : net.tseries)
         for (size_t i = 1; i < ts.x.size(); i++)
             if (ts.x[i] <= ts.x[i - 1]) { setError(173, "ERROR 173: time series " + ts.id + " has its data out of sequence."); return; }
+    buildXTables();                                      // shape curves (project.c:220-231)
+    if (errorCode) return;
+    for (size_t t = 0; t < net.transects.size(); t++)
+        if (!net.transects[t].valid) {
+            // a transect never validated has no geometry (aFull = 0, link.c:1052)
+            for (int j = 0; j < nl; j++)
+                if (net.xsect[j].type == X_IRREGULAR && net.xsect[j].transect == (int)t) {
+                    setError(119, "ERROR 119: invalid cross section for link " + net.linkId[j]);
+                    return;
+                }
+        }
     for (int j = 0; j < nl; j++) {
         if (opt.linkOffsetsElev) {                       // link.c:468-504
             for (int e = 0; e < 2; e++) {
@@ -1955,7 +2359,7 @@ void Project::initDepths()
     const double* ct = &SWX_CIRC_TABLES[0][0];
     auto geom = [&](int j) {
         const Xsect& x = net.xsect[j];
-        return geomOf(x);
+        return geomOf(x, net.xTab.data());
     };
     State& s = st;
     std::vector<double> acc(nn, 0.0), cnt(nn, 0.0);
@@ -2018,7 +2422,7 @@ int Project::initState()
     const double* ct = &SWX_CIRC_TABLES[0][0];
     auto geom = [&](int j) {
         const Xsect& x = net.xsect[j];
-        return geomOf(x);
+        return geomOf(x, net.xTab.data());
     };
     // project_init runs table_tseriesInit before routing_open
     for (auto& ts : net.tseries) {            // table_tseriesInit (table.c:730-740)
@@ -2136,7 +2540,7 @@ int Project::initState()
         s.q2[i] = s.q1[i];
         s.a1[i] = getAofY(geom(i), s.lNewDepth[i], ct);
         s.a2[i] = s.a1[i];
-        s.lNewVolume[i] = s.a1[i] * net.length[i] * net.barrels[i];
+        s.lNewVolume[i] = s.a1[i] * net.lengthT[i] * net.barrels[i];
         s.lOldVolume[i] = s.lNewVolume[i];
     }
     // qualrout_init (qualrout.c:63-96), skipped with a hot start file (routing.c:122)
@@ -2164,7 +2568,7 @@ void Project::ncCoefs(int j)
     State& s = st;
     NcLink L = ncLink(j);
     const Xsect& x = net.xsect[j];
-    Geom g = geomOf(x);
+    Geom g = geomOf(x, net.xTab.data());
     if (net.linkType[j] == ORIFICE) {
         NcCoef c{};
         orificeCoefs(L, g, s.setting[j], ct, &c);

@@ -82,6 +82,17 @@ private:
     int readFiles(std::vector<char*>& tok);
     int readStorage(std::vector<char*>& tok);
     int readCurve(std::vector<char*>& tok);
+    int readTransect(std::vector<char*>& tok);
+    void validateTransect(int j);
+    void buildXTables();
+    // transect_readParams state carried from line to line (and, as in the
+    // reference, from one transect to the next: transect.c:28-41)
+    struct TransectInput {
+        int count = 0, nStations = 0;
+        double nLeft = 0, nRight = 0, nChannel = 0, xLeft = 0, xRight = 0, xFactor = 1,
+               yFactor = 0, lFactor = 1;
+        std::vector<double> station, elev;
+    } tin_;
     int readRegulator(int sect, std::vector<char*>& tok);
     void validateRegulator(int j);
     int readHotstart();
@@ -102,13 +113,15 @@ private:
 bool setXsectParams(Xsect& x, int type, double p[4], double ucf);
 
 // the kernels' geometry record of a cross-section (tabulated shapes point at
-// their block of SWX_SHAPE_TAB)
-inline swx::Geom geomOf(const Xsect& x)
+// their block of SWX_SHAPE_TAB; transect / custom / street sections at their
+// block of the network's xTab, passed as xtab)
+inline swx::Geom geomOf(const Xsect& x, const double* xtab = nullptr)
 {
     swx::Geom g{x.type, x.yFull, x.wMax, x.ywMax, x.aFull, x.rFull, x.sFull, x.sMax,
                 x.yBot, x.aBot, x.sBot, x.rBot};
     int off = swx::shapeTabOffset(x.type);
     if (off >= 0) g.tb = SWX_SHAPE_TAB + off;
+    else if (x.tabOff >= 0 && xtab) g.tb = xtab + x.tabOff;
     return g;
 }
 

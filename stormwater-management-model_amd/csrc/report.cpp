@@ -417,6 +417,7 @@ void writeRunReport(FILE* f, Project& prj, const ReportTotals& tot, long long no
         for (int j = 0; j < nL; j++) {
             w.printf("\n  %-20s", net.linkId[j].c_str());
             if (net.xsect[j].type == X_DUMMY) w.printf(" DUMMY   ");
+            else if (net.xsect[j].type == X_IRREGULAR) w.printf(" CHANNEL ");
             else w.printf(" %-7s ", kLinkWords[net.linkType[j]]);
             elapsed(R.lMaxFlowDate[j], rptStart, &d, &h, &m);
             w.printf(flowFmt, R.lMaxFlow[j] * ucfQ);

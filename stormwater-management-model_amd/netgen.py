@@ -334,11 +334,47 @@ _SHAPES = {
 }
 
 
+# irregular natural-channel transects (HEC-2 NC / X1 / GR records, with
+# overbank roughness, meander length factor, station and elevation
+# adjustments) and a custom closed shape, replacing open / closed channels of
+# the Example network (transect.c, shape.c)
+_IRREGULAR = {
+    "C4": "IRREGULAR    TR1   0    0    0",
+    "C9": "IRREGULAR    TR2   0    0    0",
+    "C14": "IRREGULAR   TR1   0    0    0",
+    "C16": "IRREGULAR   TR3   0    0    0",
+    "C7": "CUSTOM       3.0   SHAPE1  0  0",
+    "C12": "CUSTOM      2.0   SHAPE1  0  0",
+}
+_TRANSECTS = """
+[TRANSECTS]
+;;Transect Data in HEC-2 format
+NC 0.08     0.07     0.035
+X1 TR1      9        20       70       0.0      0.0      0.0      1.2      1.0      0.0
+GR 10.0     0        8.0      10       6.0      20       3.0      30       2.0      45
+GR 3.0      60       6.0      70       8.0      80       10.0     90
+NC 0.0      0.0      0.04
+X1 TR2      6        0.0      0.0      0.0      0.0      0.0      0.0      0.0      0.0
+GR 5.0      0        3.0      5        1.0      10       1.0      15       3.0      20
+GR 5.0      25
+NC 0.05     0.05     0.03
+X1 TR3      7        5.0      15.0     0.0      0.0      0.0      1.0      0.8      -1.0
+GR 8.0      0        5.0      5        2.5      8        2.0      11       2.5      14
+GR 5.0      15       8.0      20
+"""
+_SHAPE_CURVE = """SHAPE1       SHAPE   0.0   0.5
+SHAPE1               0.2   0.9
+SHAPE1               0.5   1.0
+SHAPE1               0.8   0.8
+SHAPE1               1.0   0.3
+"""
+
+
 def write_example(path: str, *, route_step: float = 5.0,
                   variable_step: float = 0.0, end_time: str = "04:00:00",
                   pollutants: bool = False, files: str = "", storage: bool = False,
                   regulators: bool = False, shapes: bool = False,
-                  force_main_eqn: str = "") -> None:
+                  force_main_eqn: str = "", irregular: bool = False) -> None:
     """Write the authored Example network (see module docstring).  `files`
     is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf");
     `storage` turns six junctions into storage units (_STORAGE)."""
@@ -366,6 +402,20 @@ def write_example(path: str, *, route_step: float = 5.0,
             txt = txt.replace("[OPTIONS]\n", "[OPTIONS]\nFORCE_MAIN_EQUATION " + force_main_eqn + "\n", 1)
             if force_main_eqn == "D-W":          # roughness height (in) instead of a C-factor
                 txt = txt.replace("FORCE_MAIN      1.0  120", "FORCE_MAIN      1.0  0.01")
+    if irregular:
+        out = []
+        for ln in txt.split("\n"):
+            t = ln.split()
+            if len(t) == 7 and t[0] in _IRREGULAR and t[1] in (
+                    "CIRCULAR", "RECT_OPEN", "RECT_CLOSED", "TRAPEZOIDAL", "TRIANGULAR"):
+                ln = "%-4s %s  %s" % (t[0], _IRREGULAR[t[0]], t[6])
+            out.append(ln)
+        txt = "\n".join(out)
+        txt = txt.replace("[LOSSES]\n", _TRANSECTS.lstrip("\n") + "\n[LOSSES]\n", 1)
+        if "[CURVES]" in txt:
+            txt = txt.replace("[CURVES]\n", "[CURVES]\n" + _SHAPE_CURVE, 1)
+        else:
+            txt += "\n[CURVES]\n" + _SHAPE_CURVE
     if regulators:
         storage = True
         out = []
