@@ -756,6 +756,7 @@ long DLLEXPORT swmmx_getArray(const char* name, double* dst, long n)
         ARR("stat.link.maxFlow", R.lMaxFlow) ARR("stat.link.maxFlowDate", R.lMaxFlowDate)
         ARR("stat.link.maxVeloc", R.lMaxVeloc) ARR("stat.link.maxDepth", R.lMaxDepth)
         ARR("stat.link.timeNormalFlow", R.lTimeNormalFlow) ARR("stat.link.timeSurcharged", R.lTimeSurcharged)
+        ARR("stat.link.timeInletControl", R.lTimeInletControl)
         ARR("stat.link.timeFullUpstream", R.lTimeFullUpstream)
         ARR("stat.link.timeFullDnstream", R.lTimeFullDnstream) ARR("stat.link.timeFullFlow", R.lTimeFullFlow)
         ARR("stat.link.timeCapacityLimited", R.lTimeCapacityLimited)

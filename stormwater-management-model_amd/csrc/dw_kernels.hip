@@ -36,6 +36,7 @@
 
 #include "router.h"
 #include "xsect.h"
+#include "culvert.h"
 #include "storage.h"
 #include "regulators.h"
 
@@ -78,6 +79,7 @@ enum : uint32_t {
     LF_COLD = 1u << 22,           // an invert offset: may need normal/critical depth
     LF_NC = 1u << 23,             // pump / orifice / weir / outlet (k_nc; also LF_COLD)
     LF_PUMP = 1u << 24,
+    LF_CULVERT_SHIFT = 25,        // bits 25-30 culvert code (cold conduits only)
 };
 // ---- packed per-node flags -------------------------------------------------
 enum : uint32_t {
@@ -137,7 +139,7 @@ struct StatsDev {
     double *mbIn, *mbOut, *mbPendIn, *mbPendOut;      // node volume totals + pending rates
     double *oAvgFlow, *oMaxFlow, *oLoad;               // outfalls ([p][node] loads)
     int* oPeriods;
-    double *lMaxFlow, *lMaxFlowDate, *lMaxVeloc, *lMaxDepth, *lTimeNormal, *lTimeSurch;
+    double *lMaxFlow, *lMaxFlowDate, *lMaxVeloc, *lMaxDepth, *lTimeNormal, *lTimeSurch, *lTimeInlet;
     double *lTimeFullUp, *lTimeFullDn, *lTimeFullFlow, *lTimeCapLim, *lTimeClass, *lTimeCourant;
     int *lTurns, *lTurnSign;
     const double* qFull;
@@ -543,7 +545,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         p.evapLoss[j] = 0.0;
         p.seepLoss[j] = 0.0;
         int old = p.lstate[j];
-        p.lstate[j] = (old & ~0x40F) | fc;    // fullState / normalFlow untouched (dwflow.c:165-180)
+        p.lstate[j] = (old & ~0xF) | fc;      // fullState / normalFlow / inletControl untouched (dwflow.c:165-180)
         return;
     }
 
@@ -598,8 +600,14 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     double q = (qOld - dq2 + dq3 + dq4 + dq6) / denom;
     p.dqdh[j] = 1.0 / denom * 32.2 * dt * aWtd / length * barrels;
 
-    int normalFlow = 0;
+    int normalFlow = 0, inletCtl = 0;
+    const int culvert = kCold ? (int)((f >> LF_CULVERT_SHIFT) & 0x3F) : 0;
     if (q > 0.0) {
+        if (kCold && culvert > 0 && !isFull) {                  // dwflow.c:250-252
+            double dq = 0.0;
+            q = culvertInflow(x, culvert, p.slope[j], q, h1 - z1, &dq, &inletCtl, ct);
+            if (inletCtl) p.dqdh[j] = dq;
+        } else
         if (p.normalFlowLtd != NFL_NEITHER && y1 < x.yFull && (fc == F_SUBCRIT || fc == F_SUPCRIT)) {
             // checkNormalFlow dwflow.c:637-686
             bool hasOutfall = (f & (LF_N1_OUTFALL | LF_N2_OUTFALL)) != 0;
@@ -658,7 +666,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     p.evapLoss[j] = evapRate;
     p.seepLoss[j] = seepRate;
     int old = p.lstate[j];
-    p.lstate[j] = (old & (1 << 9)) | fc | (fs << 4) | (normalFlow << 8);
+    p.lstate[j] = (old & (1 << 9)) | fc | (fs << 4) | (normalFlow << 8) | (inletCtl << 10);
 }
 
 // ===========================================================================
@@ -1564,6 +1572,7 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
             if (v > S.lMaxVeloc[j]) S.lMaxVeloc[j] = v;
             if (depth > S.lMaxDepth[j]) S.lMaxDepth[j] = depth;
             if (s & (1 << 8)) S.lTimeNormal[j] += dt;
+            if (s & (1 << 10)) S.lTimeInlet[j] += dt;
             int fc = s & 0xF;
             if (fc < 7) S.lTimeClass[(size_t)fc * p.nL + j] += dt;
             if (q >= S.qFull[j] * barrels) S.lTimeFullFlow[j] += dt;
@@ -2210,7 +2219,9 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (net.linkType[g] != CONDUIT) {
             f |= LF_NC | LF_COLD;                   // k_nc, not the conduit kernels
             if (net.linkType[g] == PUMP) f |= LF_PUMP;
-        } else if (net.offset1[g] > 0.0 || net.offset2[g] > 0.0 || !isBasicShape(x.type)) {
+        } else if (net.offset1[g] > 0.0 || net.offset2[g] > 0.0 || !isBasicShape(x.type) ||
+                   x.culvertCode > 0) {
+            if (x.culvertCode > 0) f |= ((uint32_t)std::min(x.culvertCode, 63) & 0x3Fu) << LF_CULVERT_SHIFT;
             f |= LF_COLD;
             coldLinks.push_back(j);
         }
@@ -2589,7 +2600,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         UPI(S.oPeriods, iz, nN);
         UPI(S.lTurns, iz, nL);
         UPI(S.lTurnSign, iz, nL);
-        for (double** a : {&S.lMaxFlow, &S.lMaxFlowDate, &S.lMaxVeloc, &S.lMaxDepth, &S.lTimeNormal,
+        for (double** a : {&S.lMaxFlow, &S.lMaxFlowDate, &S.lMaxVeloc, &S.lMaxDepth, &S.lTimeNormal, &S.lTimeInlet,
                            &S.lTimeSurch, &S.lTimeFullUp, &S.lTimeFullDn, &S.lTimeFullFlow,
                            &S.lTimeCapLim, &S.lTimeCourant})
             UPD(*a, l0, nL);
@@ -3086,6 +3097,7 @@ int Router::downloadStats(Project& prj)
     HIPCHECK(link(R.lMaxVeloc, S.lMaxVeloc, 1));
     HIPCHECK(link(R.lMaxDepth, S.lMaxDepth, 1));
     HIPCHECK(link(R.lTimeNormalFlow, S.lTimeNormal, 1));
+    HIPCHECK(link(R.lTimeInletControl, S.lTimeInlet, 1));
     HIPCHECK(link(R.lTimeSurcharged, S.lTimeSurch, 1));
     HIPCHECK(link(R.lTimeFullUpstream, S.lTimeFullUp, 1));
     HIPCHECK(link(R.lTimeFullDnstream, S.lTimeFullDn, 1));

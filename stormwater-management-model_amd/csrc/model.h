@@ -247,6 +247,7 @@ struct RunStats {
     std::vector<double> pUtilized, pMinFlow, pAvgFlow, pMaxFlow, pVolume, pEnergy, pOffLow, pOffHigh,
         pStartUps, pPeriods;
     std::vector<double> outfallAvgFlow, outfallMaxFlow, outfallPeriods, outfallLoad;   // load [p][node]
+    std::vector<double> lTimeInletControl;
     std::vector<double> lMaxFlow, lMaxFlowDate, lMaxVeloc, lMaxDepth, lTimeNormalFlow,
         lTimeSurcharged, lTimeFullUpstream, lTimeFullDnstream, lTimeFullFlow, lTimeCapacityLimited,
         lTimeInFlowClass, lTimeCourantCritical, lFlowTurns, lFlowTurnSign;   // class: [k][link]

@@ -1644,7 +1644,6 @@ int Project::readXsect(std::vector<char*>& tok)  // link.c:162-267
     if (nt >= 8) {
         int i = atoi(tok[7]);
         if (i < 0) return 211;
-        if (i > 0) return setError(200, "ERROR 200: culvert inlet control is not supported by the MI355X engine yet");
         net.xsect[j].culvertCode = i;
     }
     return 0;

@@ -460,7 +460,7 @@ void writeRunReport(FILE* f, Project& prj, const ReportTotals& tot, long long no
         for (int i = 0; i < RunStats::kClasses; i++)
             w.printf("  %4.2f", R.lTimeInFlowClass[(size_t)i * nL + j] / R.routingTimeSpan);
         w.printf("  %4.2f", R.lTimeNormalFlow[j] / R.routingTimeSpan);
-        w.printf("  %4.2f", 0.0 / R.routingTimeSpan);          // inlet control: culverts only
+        w.printf("  %4.2f", R.lTimeInletControl[j] / R.routingTimeSpan);
     }
     w.blank();
 

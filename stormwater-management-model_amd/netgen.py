@@ -370,11 +370,18 @@ SHAPE1               1.0   0.3
 """
 
 
+# culvert inlet-control codes (FHWA HDS-5 table, culvert.c) on conduits of the
+# Example network: form-1 (Ridder-solved) and form-2 equations, the
+# mitered-inlet slope correction (code 5) and a two-barrel culvert
+_CULVERTS = {"C3": 1, "C7": 12, "C8": 14, "C10": 5, "C13": 2, "C19": 3}
+
+
 def write_example(path: str, *, route_step: float = 5.0,
                   variable_step: float = 0.0, end_time: str = "04:00:00",
                   pollutants: bool = False, files: str = "", storage: bool = False,
                   regulators: bool = False, shapes: bool = False,
-                  force_main_eqn: str = "", irregular: bool = False) -> None:
+                  force_main_eqn: str = "", irregular: bool = False,
+                  culverts: bool = False) -> None:
     """Write the authored Example network (see module docstring).  `files`
     is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf");
     `storage` turns six junctions into storage units (_STORAGE)."""
@@ -402,6 +409,14 @@ def write_example(path: str, *, route_step: float = 5.0,
             txt = txt.replace("[OPTIONS]\n", "[OPTIONS]\nFORCE_MAIN_EQUATION " + force_main_eqn + "\n", 1)
             if force_main_eqn == "D-W":          # roughness height (in) instead of a C-factor
                 txt = txt.replace("FORCE_MAIN      1.0  120", "FORCE_MAIN      1.0  0.01")
+    if culverts:
+        out = []
+        for ln in txt.split("\n"):
+            t = ln.split()
+            if len(t) == 7 and t[0] in _CULVERTS and t[1] in ("CIRCULAR", "RECT_CLOSED"):
+                ln = ln + "  %d" % _CULVERTS[t[0]]
+            out.append(ln)
+        txt = "\n".join(out)
     if irregular:
         out = []
         for ln in txt.split("\n"):

@@ -36,7 +36,8 @@ REFDUMP_X87 = os.path.join(ROOT, "oracle", "_ref", "x87", "refdump")
 # depth by enumeration): the fixture also stores, per recorded step and state
 # array, the largest |FMA build - reference| ("env.<key>"), made with
 # `make -C oracle ref-fma`
-ENVELOPE = {"example_shapes", "example_shapes_var", "example_irregular", "example_irregular_var"}
+ENVELOPE = {"example_shapes", "example_shapes_var", "example_irregular", "example_irregular_var",
+            "example_culverts", "example_culverts_var"}
 
 # name -> (writer, kwargs, every)
 CASES = {
@@ -87,6 +88,11 @@ CASES = {
     "example_irregular_var": (netgen.write_example, dict(end_time="02:00:00", route_step=10.0,
                                                          variable_step=0.75, irregular=True,
                                                          pollutants=True), 1),
+    # culverts under inlet control (culvert.c): both equation forms
+    "example_culverts": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0,
+                                                    culverts=True), 1),
+    "example_culverts_var": (netgen.write_example, dict(end_time="02:00:00", route_step=10.0,
+                                                        variable_step=0.75, culverts=True), 1),
     # swmm_setValue between steps: external inflow, outfall stage, routing step
     "example_api": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
                                                variable_step=0.75), 1),
