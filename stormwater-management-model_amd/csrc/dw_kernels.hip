@@ -220,6 +220,9 @@ struct Params {
     const double* gXTab;          // transect / custom-shape table blocks (Network::xTab)
     const int* lTabOff;           // per link: its block in gXTab (-1: none); null without any
     const double* lengthRaw;      // Conduit.length as input (findLimitedLinks); = length unless irregular
+    const double* ofTab;          // tidal curves / stage series of outfalls: (x, y) pairs
+    const int* ofOff;             // per node: {offset of its pairs in ofTab, count} (-1: none)
+    double startDateTime;         // StartDateTime (days)
     double* partials;             // [nBlocksEnd][kNumPartials]
     int nBlocksEnd;
     StatsDev st;
@@ -757,6 +760,30 @@ __device__ __forceinline__ double outfallPart(const Params& p, int j, uint32_t f
     if (kPart == 0) return linkYnorm<kAll>(x, q, p.qMax[j], p.beta[j], ct);
     return getYcrit<kAll>(x, q, ct);
 }
+// table_lookup (table.c:395-426) and table_tseriesLookup with extend = TRUE
+// (table.c:745-804) on (x, y) pairs: first / last value outside the range,
+// linear interpolation (tableInterp, storage.h) inside
+__device__ double curveLookup(const double* t, int n, double x)
+{
+    if (n <= 0) return 0.0;
+    double x1 = t[0], y1 = t[1];
+    if (x <= x1) return y1;
+    for (int m = 1; m < n; m++) {
+        double x2 = t[2 * m], y2 = t[2 * m + 1];
+        if (x <= x2) return tableInterp(x, x1, y1, x2, y2);
+        x1 = x2;
+        y1 = y2;
+    }
+    return y1;
+}
+__device__ double tseriesLookupExt(const double* t, int n, double x)
+{
+    if (n <= 0) return 0.0;
+    if (x < t[0]) return t[1];
+    for (int m = 1; m < n; m++)
+        if (x <= t[2 * m]) return tableInterp(x, t[2 * m - 2], t[2 * m - 1], t[2 * m], t[2 * m + 1]);
+    return t[2 * n - 1];
+}
 __device__ __forceinline__ double outfallCombine(const Params& p, int i, uint32_t nf, int j,
                                                  double yNorm, double yCrit)
 {
@@ -767,6 +794,18 @@ __device__ __forceinline__ double outfallCombine(const Params& p, int i, uint32_
     if (ot == O_FREE) return (z > 0.0) ? 0.0 : gmin(yNorm, yCrit);
     if (ot == O_NORMAL) return (z > 0.0) ? 0.0 : yNorm;
     double stage = (ot == O_FIXED) ? p.fixedStage[i] : inv;
+    if (ot == O_TIDAL || ot == O_TSERIES) {             // node.c:1446-1459
+        const double* t = p.ofTab + p.ofOff[2 * i];
+        int n = p.ofOff[2 * i + 1];
+        double tEnd = p.ctl->newRoutingTime + 1000.0 * p.ctl->dt;   // NewRoutingTime of this step
+        if (ot == O_TIDAL) {
+            double currentDate = tEnd / 86400000.0;
+            double x = t[0] + (currentDate - floor(currentDate)) * 24.0;
+            stage = curveLookup(t, n, x) / p.ucfL;
+        } else {
+            stage = tseriesLookupExt(t, n, p.startDateTime + tEnd / 86400000.0) / p.ucfL;
+        }
+    }
     yCrit = gmin(yCrit, yNorm);
     double yNew;
     if (yCrit + z + inv < stage) yNew = stage - inv;
@@ -2313,11 +2352,32 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (!part.owned[i]) f |= NF_REPLICA;
         nflags[i] = (int)f;
         yCrown[i] = net.crownElev[g] - net.invertElev[g];
-        if (net.nodeType[g] == OUTFALL && net.outfallType[g] > O_FIXED) {
-            fail("TIMESERIES outfalls are not supported on the device yet");
-            return err_;
+    }
+    // tidal-curve / stage-time-series outfalls: their (x, y) tables
+    p.ofTab = nullptr;
+    p.ofOff = nullptr;
+    {
+        std::vector<double> tab;
+        std::vector<int> off(2 * nN, -1);
+        for (int i = 0; i < nN; i++) {
+            const int g = LN[i];
+            if (net.nodeType[g] != OUTFALL || net.outfallType[g] <= O_FIXED) continue;
+            const std::vector<double>* xs;
+            const std::vector<double>* ys;
+            if (net.outfallType[g] == O_TIDAL) { xs = &net.curves[net.outfallSeries[g]].x; ys = &net.curves[net.outfallSeries[g]].y; }
+            else { xs = &net.tseries[net.outfallSeries[g]].x; ys = &net.tseries[net.outfallSeries[g]].y; }
+            off[2 * i] = (int)tab.size();
+            off[2 * i + 1] = (int)xs->size();
+            for (size_t m = 0; m < xs->size(); m++) { tab.push_back((*xs)[m]); tab.push_back((*ys)[m]); }
+        }
+        if (!tab.empty()) {
+            UPD(tmp, tab, tab.size()); p.ofTab = tmp;
+            int* o;
+            UPI(o, off, off.size());
+            p.ofOff = o;
         }
     }
+    p.startDateTime = prj.opt.startDateTime;
     // CSR: incident links per node, ascending link index (all links are true
     // conduits, so this is exactly the order of dynwave.c:398-401)
     // Pumps / regulators are not in it: their flows join the node sums after

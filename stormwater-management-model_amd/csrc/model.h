@@ -186,6 +186,8 @@ struct Network {
     std::vector<int> ncSub, ncCurve, ncCanSurcharge;
     std::vector<double> ncC1, ncC2, ncEndCon, ncSlope, ncLength, ncYOn, ncYOff, ncXMin, ncXMax,
         ncInitSetting;
+    std::vector<double> ncRoadWidth;    // roadway weirs (link.c:381-382)
+    std::vector<int> ncRoadSurf;
     int nNC = 0, nPumps = 0;
     // inflows / quality inputs
     std::vector<ExtInflow> extInflows;

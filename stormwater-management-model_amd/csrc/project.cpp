@@ -403,6 +403,7 @@ int Project::readFile(const char* path)
                 v->assign(nl, 0.0);
             net.xsect.assign(nl, Xsect());
             net.ncSub.assign(nl, 0); net.ncCurve.assign(nl, -1); net.ncCanSurcharge.assign(nl, 1);
+            net.ncRoadWidth.assign(nl, 0.0); net.ncRoadSurf.assign(nl, 0);
             for (auto* v : {&net.ncC1, &net.ncC2, &net.ncEndCon, &net.ncSlope, &net.ncLength,
                             &net.ncYOn, &net.ncYOff, &net.ncXMin, &net.ncXMax})
                 v->assign(nl, 0.0);
@@ -1145,8 +1146,10 @@ int Project::readOutfall(std::vector<char*>& tok)  // node.c:1333-1409
             auto it = net.tseriesIndex.find(tok[3]);
             if (it == net.tseriesIndex.end()) return 209;
             series = it->second;
-        } else {
-            return setError(200, "ERROR 200: TIDAL outfalls are not supported by the MI355X engine");
+        } else {                                    // TIDAL: the tide curve (node.c:1380-1384)
+            auto it = net.curveIndex.find(tok[3]);
+            if (it == net.curveIndex.end()) return 209;
+            series = it->second;
         }
     }
     if (nt == n) {
@@ -1276,8 +1279,6 @@ int Project::readRegulator(int sect, std::vector<char*>& tok)
         if (nt < 6) return 203;
         int m = kfind(tok[3], kWeirTypeWords);
         if (m < 0) return 205;
-        if (m == WR_ROADWAY)
-            return setError(200, "ERROR 200: roadway weirs are not supported by the MI355X engine yet");
         double crest, cd1, endCon = 0.0, cd2 = 0.0;
         if (opt.linkOffsetsElev && *tok[4] == '*') crest = kMissing;
         else if (!getDouble(tok[4], &crest)) return 211;
@@ -1287,7 +1288,18 @@ int Project::readRegulator(int sect, std::vector<char*>& tok)
         if (nt >= 8 && *tok[7] != '*' && (!getDouble(tok[7], &endCon) || endCon < 0.0)) return 211;
         if (nt >= 9 && *tok[8] != '*' && (!getDouble(tok[8], &cd2) || cd2 < 0.0)) return 211;
         if (nt >= 10 && *tok[9] != '*') { surch = kfind(tok[9], kNoYes); if (surch < 0) return 205; }
+        double roadWidth = 0.0;
+        int roadSurf = 0;
+        if (m == WR_ROADWAY) {                            // link.c:2074-2086
+            if (nt >= 11 && (!getDouble(tok[10], &roadWidth) || roadWidth < 0.0)) return 211;
+            if (nt >= 12) {
+                if (strcasecmp(tok[11], "PAVED") == 0) roadSurf = 1;
+                else if (strcasecmp(tok[11], "GRAVEL") == 0) roadSurf = 2;
+            }
+        }
         if (nt >= 13 && *tok[12] != '*') { cdCurve = curveOf(tok[12]); if (cdCurve < 0) return 209; }
+        net.ncRoadWidth[j] = roadWidth / u;
+        net.ncRoadSurf[j] = roadSurf;
         net.linkType[j] = WEIR;
         net.ncSub[j] = m;
         net.offset1[j] = crest <= kMissing ? crest : crest / u;
@@ -2218,7 +2230,7 @@ void Project::validateRegulator(int j)
     } else if (type == WEIR) {
         int w = net.ncSub[j];
         bool ok = true;
-        if (w == WR_TRANSVERSE || w == WR_SIDEFLOW) { ok = xs.type == X_RECT_OPEN; net.ncSlope[j] = 0.0; }
+        if (w == WR_TRANSVERSE || w == WR_SIDEFLOW || w == WR_ROADWAY) { ok = xs.type == X_RECT_OPEN; net.ncSlope[j] = 0.0; }
         else if (w == WR_VNOTCH) { ok = xs.type == X_TRIANGULAR; if (ok) net.ncSlope[j] = xs.sBot; }
         else if (w == WR_TRAPEZOIDAL) { ok = xs.type == X_TRAPEZOIDAL; if (ok) net.ncSlope[j] = xs.sBot; }
         if (!ok) {
@@ -2391,6 +2403,10 @@ void Project::initDepths()
         if (ot == O_FREE) { s.newDepth[k] = (zz > 0.0) ? 0.0 : gmin(yNorm, yCrit); continue; }
         if (ot == O_NORMAL) { s.newDepth[k] = (zz > 0.0) ? 0.0 : yNorm; continue; }
         if (ot == O_FIXED) stage = net.fixedStage[k];
+        else if (ot == O_TIDAL) {                      // hour 0 of the tide curve
+            const Curve& c = net.curves[net.outfallSeries[k]];
+            stage = (c.y.empty() ? 0.0 : c.y[0]) / ucfLength();
+        }
         else stage = tseriesLookup(net.outfallSeries[k], opt.startDateTime + 0.0 / kMsecPerDay, true) / ucfLength();
         yCrit = gmin(yCrit, yNorm);
         if (yCrit + zz + net.invertElev[k] < stage) yNew = stage - net.invertElev[k];
@@ -2608,6 +2624,8 @@ NcLink Project::ncLink(int j) const
     L.ucfL = ucfLength();
     L.ucfQ = ucfFlow();
     L.si = opt.unitSystem;
+    L.roadWidth = net.ncRoadWidth[j];
+    L.roadSurf = net.ncRoadSurf[j];
     return L;
 }
 

@@ -31,6 +31,8 @@ struct NcLink {
     double yOn, yOff, xMin, xMax, qFull;   // pumps
     double ucfL, ucfQ;          // UCF(LENGTH), UCF(FLOW)
     int si;                     // UnitSystem == SI
+    double roadWidth;           // roadway weirs: road width (ft), surface 1 paved / 2 gravel
+    int roadSurf;
 };
 
 // setting-dependent coefficients (orifice_setSetting, weir_setSetting)
@@ -278,7 +280,74 @@ SWX_HD double weirOrificeFlow(const NcLink& L, const Geom& g, double setting, do
     return q;
 }
 
-// weir_getInflow (link.c:2190-2312), dynamic wave, non-roadway weirs
+// Roadway overflow (roadway.c, FHWA HDS-5 roadway discharge coefficients and
+// submergence factors, as (x, y) tables)
+static constexpr double kCrLowPaved[4][2] = {{0.0, 2.85}, {0.2, 2.95}, {0.7, 3.03}, {4.0, 3.05}};
+static constexpr double kCrLowGravel[8][2] = {{0.0, 2.5}, {0.5, 2.7}, {1.0, 2.8}, {1.5, 2.9},
+                                              {2.0, 2.98}, {2.5, 3.02}, {3.0, 3.03}, {4.0, 3.05}};
+static constexpr double kCrHighPaved[2][2] = {{0.15, 3.05}, {0.25, 3.10}};
+static constexpr double kCrHighGravel[2][2] = {{0.15, 2.95}, {0.30, 3.10}};
+static constexpr double kKtPaved[9][2] = {{0.8, 1.0}, {0.85, 0.98}, {0.90, 0.92}, {0.93, 0.85}, {0.95, 0.80},
+                                          {0.97, 0.70}, {0.98, 0.60}, {0.99, 0.50}, {1.00, 0.40}};
+static constexpr double kKtGravel[12][2] = {{0.75, 1.00}, {0.80, 0.985}, {0.83, 0.97}, {0.86, 0.93},
+                                            {0.89, 0.90}, {0.90, 0.87}, {0.92, 0.80}, {0.94, 0.70},
+                                            {0.96, 0.60}, {0.98, 0.50}, {0.99, 0.40}, {1.00, 0.24}};
+// getY (roadway.c:176-194)
+SWX_HD double roadwayY(double x, const double (*t)[2], int n)
+{
+    if (x <= t[0][0]) return t[0][1];
+    if (x >= t[n - 1][0]) return t[n - 1][1];
+    for (int i = 1; i < n; i++) {
+        if (x <= t[i][0]) {
+            double x1 = t[i - 1][0], dx = t[i][0] - x1;
+            double y1 = t[i - 1][1], dy = t[i][1] - y1;
+            return y1 + (x - x1) * dy / dx;
+        }
+    }
+    return t[n - 1][1];
+}
+// getCd (roadway.c:146-172)
+SWX_HD double roadwayCd(double hWr, double ht, double roadWidth, int roadSurf)
+{
+    double kT = 1.0, cR;
+    if (hWr <= 0.0) return 0.0;
+    double hL = hWr / roadWidth;
+    if (hL <= 0.15) {
+        if (roadSurf == 1) cR = roadwayY(hWr, kCrLowPaved, 4);
+        else cR = roadwayY(hWr, kCrLowGravel, 8);
+    } else {
+        if (roadSurf == 1) cR = roadwayY(hL, kCrHighPaved, 2);
+        else cR = roadwayY(hL, kCrHighGravel, 2);
+    }
+    if (ht > 0.0) {
+        double htH = ht / hWr;
+        if (roadSurf == 1) kT = roadwayY(htH, kKtPaved, 9);
+        else kT = roadwayY(htH, kKtGravel, 12);
+    }
+    return cR * kT;
+}
+// roadway_getInflow (roadway.c:85-142): h1 / h2 already ordered by dir
+SWX_HD double roadwayInflow(const NcLink& L, const Geom& g, double dir, double hRoad, double h1, double h2,
+                            NcOut* o)
+{
+    double cD = L.c1;
+    if (L.si) cD = cD / 0.552;
+    bool useVariableCd = L.roadWidth > 0.0 && L.roadSurf >= 1;
+    double hWr = h1 - hRoad, ht = h2 - hRoad, q = 0.0, dqdh = 0.0;
+    if (hWr > 0.0001) {
+        if (useVariableCd) cD = roadwayCd(hWr, ht, L.roadWidth, L.roadSurf);
+        double length = g.wMax;
+        q = cD * length * pow(hWr, 1.5);
+        dqdh = 1.5 * q / hWr;
+    }
+    o->dqdh = dqdh;
+    o->depth = gmax(h1 - hRoad, 0.0);
+    o->flowClass = FC_SUBCRITICAL;
+    if (hRoad > h2) o->flowClass = (dir == 1.0) ? FC_DN_CRITICAL : FC_UP_CRITICAL;
+    return dir * q;
+}
+
+// weir_getInflow (link.c:2190-2312), dynamic wave
 SWX_HD double weirInflow(const NcLink& L, const Geom& g, const NcCoef& c, const double* cx,
                          const double* cy, double setting, double y1n, double y2n, double inv1,
                          double inv2, bool of1, bool of2, NcOut* o, const double* ct)
@@ -293,6 +362,7 @@ SWX_HD double weirInflow(const NcLink& L, const Geom& g, const NcCoef& c, const 
     }
     double hcrest = inv1 + L.offset1;
     double hcrown = hcrest + g.yFull;
+    if (L.sub == WR_ROADWAY) return roadwayInflow(L, g, dir, hcrest, h1, h2, o);
     hcrest += (1.0 - setting) * g.yFull;
     head = h1 - hcrest;
     o->dqdh = 0.0;

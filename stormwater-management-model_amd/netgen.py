@@ -381,7 +381,7 @@ def write_example(path: str, *, route_step: float = 5.0,
                   pollutants: bool = False, files: str = "", storage: bool = False,
                   regulators: bool = False, shapes: bool = False,
                   force_main_eqn: str = "", irregular: bool = False,
-                  culverts: bool = False) -> None:
+                  culverts: bool = False, tidal: bool = False) -> None:
     """Write the authored Example network (see module docstring).  `files`
     is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf");
     `storage` turns six junctions into storage units (_STORAGE)."""
@@ -409,6 +409,22 @@ def write_example(path: str, *, route_step: float = 5.0,
             txt = txt.replace("[OPTIONS]\n", "[OPTIONS]\nFORCE_MAIN_EQUATION " + force_main_eqn + "\n", 1)
             if force_main_eqn == "D-W":          # roughness height (in) instead of a C-factor
                 txt = txt.replace("FORCE_MAIN      1.0  120", "FORCE_MAIN      1.0  0.01")
+    if tidal:
+        # O1: tide curve (stage vs hour of day), O2: stage time series
+        # (node.c:1446-1459)
+        txt = txt.replace("O1  103.0  FREE   NO", "O1  103.0  TIDAL  TIDE1  NO")
+        txt = txt.replace("O2  104.0  FIXED  105.2  NO", "O2  104.0  TIMESERIES  STAGE2  YES")
+        tide = ("TIDE1  Tidal  0   103.2\nTIDE1         3   104.6\nTIDE1         6   105.9\n"
+                "TIDE1         9   104.8\nTIDE1         12  103.4\nTIDE1         15  104.1\n"
+                "TIDE1         18  105.5\nTIDE1         21  104.3\nTIDE1         24  103.2\n")
+        stage = ("STAGE2  0:00  104.5\nSTAGE2  0:25  105.8\nSTAGE2  0:55  106.4\n"
+                 "STAGE2  1:30  105.1\nSTAGE2  2:10  104.2\n")
+        txt = txt.replace("[TIMESERIES]\n;;Name Date Time Value\n",
+                          "[TIMESERIES]\n;;Name Date Time Value\n" + stage, 1)
+        if "[CURVES]" in txt:
+            txt = txt.replace("[CURVES]\n;;Name Type X Y\n", "[CURVES]\n;;Name Type X Y\n" + tide, 1)
+        else:
+            txt += "\n[CURVES]\n" + tide
     if culverts:
         out = []
         for ln in txt.split("\n"):

@@ -93,6 +93,10 @@ CASES = {
                                                     culverts=True), 1),
     "example_culverts_var": (netgen.write_example, dict(end_time="02:00:00", route_step=10.0,
                                                         variable_step=0.75, culverts=True), 1),
+    # tidal-curve and stage-time-series outfalls (node.c:1446-1459)
+    "example_tidal": (netgen.write_example, dict(end_time="03:00:00", route_step=5.0, tidal=True), 1),
+    "example_tidal_var": (netgen.write_example, dict(end_time="03:00:00", route_step=10.0,
+                                                     variable_step=0.75, tidal=True), 1),
     # swmm_setValue between steps: external inflow, outfall stage, routing step
     "example_api": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
                                                variable_step=0.75), 1),
