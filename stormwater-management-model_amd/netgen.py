@@ -381,7 +381,7 @@ def write_example(path: str, *, route_step: float = 5.0,
                   pollutants: bool = False, files: str = "", storage: bool = False,
                   regulators: bool = False, shapes: bool = False,
                   force_main_eqn: str = "", irregular: bool = False,
-                  culverts: bool = False, tidal: bool = False) -> None:
+                  culverts: bool = False, tidal: bool = False, roadway: bool = False) -> None:
     """Write the authored Example network (see module docstring).  `files`
     is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf");
     `storage` turns six junctions into storage units (_STORAGE)."""
@@ -447,21 +447,30 @@ def write_example(path: str, *, route_step: float = 5.0,
             txt = txt.replace("[CURVES]\n", "[CURVES]\n" + _SHAPE_CURVE, 1)
         else:
             txt += "\n[CURVES]\n" + _SHAPE_CURVE
+    regs_def = dict(_REGULATORS)
+    if roadway:
+        # roadway weirs (roadway.c): variable discharge coefficient on a paved
+        # road of given width, constant coefficient without a width
+        regulators = True
+        regs_def["C3"] = ("[WEIRS]", "C3  N3  N4  ROADWAY  0.5  3.0  NO  0  0  NO  40  PAVED",
+                          "C3  RECT_OPEN  2.0  3.0  0  0")
+        regs_def["C20"] = ("[WEIRS]", "C20 N9  N13 ROADWAY  0.3  2.8  NO  0  0  NO  0  GRAVEL",
+                           "C20 RECT_OPEN  1.5  6.0  0  0")
     if regulators:
         storage = True
         out = []
         for ln in txt.split("\n"):
             t = ln.split()
-            if t and t[0] in _REGULATORS and len(t) in (5, 7, 9):   # conduit / xsection / loss lines
+            if t and t[0] in regs_def and len(t) in (5, 7, 9):   # conduit / xsection / loss lines
                 continue
             out.append(ln)
         txt = "\n".join(out)
         regs = ""                      # before [XSECTIONS], as the reference's GUI writes them
         for sect in ("[PUMPS]", "[ORIFICES]", "[WEIRS]", "[OUTLETS]"):
-            body = [v[1] for v in _REGULATORS.values() if v[0] == sect]
+            body = [v[1] for v in regs_def.values() if v[0] == sect]
             regs += sect + "\n" + "\n".join(body) + "\n\n"
         txt = txt.replace("[XSECTIONS]\n", regs + "[XSECTIONS]\n", 1)
-        xs = [v[2] for v in _REGULATORS.values() if v[2]]
+        xs = [v[2] for v in regs_def.values() if v[2]]
         txt = txt.replace("[XSECTIONS]\n;;Link Shape Geom1 Geom2 Geom3 Geom4 Barrels\n",
                           "[XSECTIONS]\n;;Link Shape Geom1 Geom2 Geom3 Geom4 Barrels\n" + "\n".join(xs) + "\n")
     if storage:

@@ -97,6 +97,8 @@ CASES = {
     "example_tidal": (netgen.write_example, dict(end_time="03:00:00", route_step=5.0, tidal=True), 1),
     "example_tidal_var": (netgen.write_example, dict(end_time="03:00:00", route_step=10.0,
                                                      variable_step=0.75, tidal=True), 1),
+    # roadway weirs (roadway.c)
+    "example_roadway": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, roadway=True), 1),
     # swmm_setValue between steps: external inflow, outfall stage, routing step
     "example_api": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
                                                variable_step=0.75), 1),
