@@ -157,6 +157,12 @@ struct Curve {
     std::vector<double> x, y;
 };
 
+// [DIVIDERS] (TDivider, objects.h): checked at validation, routed as junctions
+struct Divider {
+    int node = -1, link = -1, type = 0;
+    double qMin = 0, dhMax = 0, cWeir = 0;
+};
+
 struct Network {
     // nodes
     std::vector<std::string> nodeId;
@@ -186,6 +192,7 @@ struct Network {
     std::vector<int> ncSub, ncCurve, ncCanSurcharge;
     std::vector<double> ncC1, ncC2, ncEndCon, ncSlope, ncLength, ncYOn, ncYOff, ncXMin, ncXMax,
         ncInitSetting;
+    std::vector<Divider> dividers;
     std::vector<double> ncRoadWidth;    // roadway weirs (link.c:381-382)
     std::vector<int> ncRoadSurf;
     int nNC = 0, nPumps = 0;

@@ -210,12 +210,12 @@ static bool getDouble(const char* s, double* y)
 enum Sect {
     S_NONE = -1, S_TITLE, S_OPTION, S_EVAP, S_JUNC, S_OUTFALL, S_CONDUIT, S_XSECT, S_LOSS,
     S_POLLUT, S_INFLOW, S_DWF, S_PATTERN, S_TSERIES, S_REPORT, S_FILES, S_STORAGE, S_CURVES,
-    S_PUMP, S_ORIFICE, S_WEIR, S_OUTLET, S_TRANSECT, S_SKIP, S_UNSUPPORTED
+    S_PUMP, S_ORIFICE, S_WEIR, S_OUTLET, S_TRANSECT, S_DIVIDER, S_SKIP, S_UNSUPPORTED
 };
 static const char* const kSectWords[] = {
     "[TITLE", "[OPTION", "[EVAP", "[JUNC", "[OUTFALL", "[CONDUIT", "[XSECT", "[LOSS",
     "[POLLUT", "[INFLOW", "[DWF", "[PATTERN", "[TIMESERIES", "[REPORT", "[FILES", "[STORAGE",
-    "[CURVE", "[PUMP", "[ORIFICE", "[WEIR", "[OUTLET", "[TRANSECT", nullptr};
+    "[CURVE", "[PUMP", "[ORIFICE", "[WEIR", "[OUTLET", "[TRANSECT", "[DIVIDER", nullptr};
 static const char* const kOffOnWords[] = {"OFF", "ON", nullptr};
 static const char* const kOrificeTypeWords[] = {"SIDE", "BOTTOM", nullptr};
 static const char* const kWeirTypeWords[] = {"TRANSVERSE", "SIDEFLOW", "V-NOTCH", "TRAPEZOIDAL",
@@ -437,6 +437,7 @@ int Project::parseLine(int sect, std::vector<char*>& tok, int pass)
         case S_JUNC:
         case S_OUTFALL:
         case S_STORAGE:
+        case S_DIVIDER:
             if (addId(net.nodeIndex, net.nodeId, tok[0]) < 0) return setError(207, std::string("ERROR 207: duplicate ID name ") + tok[0]);
             return 0;
         case S_TRANSECT:
@@ -498,6 +499,7 @@ int Project::parseLine(int sect, std::vector<char*>& tok, int pass)
     case S_OPTION: return 0;
     case S_EVAP: return readEvap(tok);
     case S_JUNC: return readJunction(tok);
+    case S_DIVIDER: return readDivider(tok);
     case S_OUTFALL: return readOutfall(tok);
     case S_CONDUIT: return readConduit(tok);
     case S_XSECT: return readXsect(tok);
@@ -676,6 +678,72 @@ int Project::readEvap(std::vector<char*>& tok)  // climate.c:285 (CONSTANT only)
     if (kmatch(tok[0], "DRY_ONLY")) return 0;
     return setError(200, std::string("ERROR 200: EVAPORATION option ") + tok[0] +
                              " is not supported by the MI355X engine (CONSTANT only)");
+}
+
+// divider_readParams (node.c:1124-1212).  Under dynamic wave a flow divider
+// routes as a junction (its diversion rule serves kinematic-wave routing
+// only); its parameters are read and validated as the reference does.
+int Project::readDivider(std::vector<char*>& tok)
+{
+    int nt = (int)tok.size();
+    if (nt < 4) return 203;
+    int j = net.nodeIndex.at(tok[0]);
+    double x[11];
+    if (!getDouble(tok[1], &x[0])) return 211;
+    for (int i = 1; i < 11; i++) x[i] = 0.0;
+    if (strlen(tok[2]) == 0 || strcmp(tok[2], "*") == 0) x[1] = -1.0;
+    else {
+        auto it = net.linkIndex.find(tok[2]);
+        if (it == net.linkIndex.end()) return 209;
+        x[1] = it->second;
+    }
+    static const char* const kDividerWords[] = {"CUTOFF", "TABULAR", "WEIR", "OVERFLOW", nullptr};
+    int n = 4;
+    int m1 = kfind(tok[3], kDividerWords);
+    if (m1 < 0) return 205;
+    x[2] = m1;
+    x[3] = -1;
+    if (m1 == 1) {                                   // TABULAR: diversion curve
+        if (nt < 5) return 203;
+        auto it = net.curveIndex.find(tok[4]);
+        if (it == net.curveIndex.end()) return 209;
+        x[3] = it->second;
+        n = 5;
+    }
+    if (m1 == 0) {                                   // CUTOFF: cutoff flow
+        if (nt < 5) return 203;
+        if (!getDouble(tok[4], &x[4])) return 211;
+        n = 5;
+    }
+    if (m1 == 2) {                                   // WEIR: qMin, dhMax, cWeir
+        if (nt < 7) return 203;
+        for (int i = 4; i < 7; i++)
+            if (!getDouble(tok[i], &x[i])) return 211;
+        n = 7;
+    }
+    if (m1 == 3) n = 4;
+    int m = 7;
+    for (int i = n; i < nt && m < 11; i++) {
+        if (!getDouble(tok[i], &x[m])) return 211;
+        m++;
+    }
+    double u = ucfLength();
+    net.nodeType[j] = DIVIDER;
+    net.invertElev[j] = x[0] / u;
+    net.crownElev[j] = net.invertElev[j];
+    net.fullDepth[j] = x[7] / u;
+    net.initDepth[j] = x[8] / u;
+    net.surDepth[j] = x[9] / u;
+    net.pondedArea[j] = x[10] / (u * u);
+    Divider dv;
+    dv.node = j;
+    dv.link = (int)x[1];
+    dv.type = m1;
+    dv.qMin = x[4] / ucfFlow();
+    dv.dhMax = x[5];
+    dv.cWeir = x[6];
+    net.dividers.push_back(dv);
+    return 0;
 }
 
 int Project::readJunction(std::vector<char*>& tok)  // node.c:606-648, 125-196
@@ -2256,6 +2324,24 @@ void Project::validate()  // project.c:186-270
     for (auto& ts : net.tseries)
         for (size_t i = 1; i < ts.x.size(); i++)
             if (ts.x[i] <= ts.x[i - 1]) { setError(173, "ERROR 173: time series " + ts.id + " has its data out of sequence."); return; }
+    for (const Divider& dv : net.dividers) {              // divider_validate (node.c:1216-1247)
+        int i = dv.link;
+        if (i < 0 || (net.node1[i] != dv.node && net.node2[i] != dv.node)) {
+            setError(136, "ERROR 136: invalid diverted link for flow divider node " + net.nodeId[dv.node]);
+            return;
+        }
+        if (dv.type == 2) {
+            if (dv.dhMax <= 0.0 || dv.cWeir <= 0.0) {
+                setError(137, "ERROR 137: invalid parameters for weir divider node " + net.nodeId[dv.node]);
+                return;
+            }
+            double qMax = dv.cWeir * pow(dv.dhMax, 1.5) / ucfFlow();
+            if (dv.qMin > qMax) {
+                setError(137, "ERROR 137: invalid parameters for weir divider node " + net.nodeId[dv.node]);
+                return;
+            }
+        }
+    }
     buildXTables();                                      // shape curves (project.c:220-231)
     if (errorCode) return;
     for (size_t t = 0; t < net.transects.size(); t++)

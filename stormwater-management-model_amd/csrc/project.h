@@ -83,6 +83,7 @@ private:
     int readStorage(std::vector<char*>& tok);
     int readCurve(std::vector<char*>& tok);
     int readTransect(std::vector<char*>& tok);
+    int readDivider(std::vector<char*>& tok);
     void validateTransect(int j);
     void buildXTables();
     // transect_readParams state carried from line to line (and, as in the

@@ -381,7 +381,8 @@ def write_example(path: str, *, route_step: float = 5.0,
                   pollutants: bool = False, files: str = "", storage: bool = False,
                   regulators: bool = False, shapes: bool = False,
                   force_main_eqn: str = "", irregular: bool = False,
-                  culverts: bool = False, tidal: bool = False, roadway: bool = False) -> None:
+                  culverts: bool = False, tidal: bool = False, roadway: bool = False,
+                  dividers: bool = False) -> None:
     """Write the authored Example network (see module docstring).  `files`
     is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf");
     `storage` turns six junctions into storage units (_STORAGE)."""
@@ -447,6 +448,13 @@ def write_example(path: str, *, route_step: float = 5.0,
             txt = txt.replace("[CURVES]\n", "[CURVES]\n" + _SHAPE_CURVE, 1)
         else:
             txt += "\n[CURVES]\n" + _SHAPE_CURVE
+    if dividers:
+        # flow dividers (node.c:1124-1247; junctions under dynamic wave)
+        txt = txt.replace("N7  114.0  10 0    0  0\n", "")
+        txt = txt.replace("N12 108.7  10 0    0  0\n", "")
+        txt = txt.replace("[CONDUITS]\n", "[DIVIDERS]\n;;Name Elev DivLink Type Params MaxDepth InitDepth "
+                          "SurDepth Aponded\nN7  114.0  C17  CUTOFF  1.5  10  0  0  0\n"
+                          "N12 108.7  C18  WEIR  0.5  1.0  3.0  10  0  0  0\n\n[CONDUITS]\n", 1)
     regs_def = dict(_REGULATORS)
     if roadway:
         # roadway weirs (roadway.c): variable discharge coefficient on a paved

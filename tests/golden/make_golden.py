@@ -99,6 +99,9 @@ CASES = {
                                                      variable_step=0.75, tidal=True), 1),
     # roadway weirs (roadway.c)
     "example_roadway": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, roadway=True), 1),
+    # flow dividers (routed as junctions under dynamic wave)
+    "example_dividers": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, dividers=True,
+                                                    pollutants=True), 1),
     # swmm_setValue between steps: external inflow, outfall stage, routing step
     "example_api": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
                                                variable_step=0.75), 1),

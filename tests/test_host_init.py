@@ -94,7 +94,7 @@ def test_missing_input_file(tmp_path):
 @pytest.mark.parametrize("section", ["[SUBCATCHMENTS]\nS1 RG1 N1 1 25 500 0.5 0\n",
                                      "[STORAGE]\nST1 100 10 0 FUNCTIONAL 1000 0 0 0 0 1.5\n",
                                      "[CONTROLS]\nRULE R1\nIF NODE N1 DEPTH > 1\nTHEN LINK C1 STATUS = OFF\n",
-                                     "[DIVIDERS]\nD1 100 C1 CUTOFF 1.0\n"])
+                                     "[STREETS]\nS1 20 0.5 2 0.016\n"])
 def test_unsupported_sections_fail_loudly(section, tmp_path):
     src = open(_golden.inp("example")).read()
     p = tmp_path / "u.inp"
@@ -103,6 +103,16 @@ def test_unsupported_sections_fail_loudly(section, tmp_path):
     err = s.open(str(p), str(tmp_path / "u.rpt"), str(tmp_path / "u.out"))
     assert err == 200
     assert "not supported" in s.getError()[1]
+    s.close()
+
+
+def test_divider_with_unattached_link_is_rejected(tmp_path):
+    """divider_validate (node.c:1216-1231): ERROR 136 like the reference."""
+    src = open(_golden.inp("example")).read()
+    p = tmp_path / "d.inp"
+    p.write_text(src.replace("[JUNCTIONS]", "[DIVIDERS]\nD1 100 C1 CUTOFF 1.0\n\n[JUNCTIONS]"))
+    s = swmm5.SWMM()
+    assert s.open(str(p), str(tmp_path / "d.rpt"), str(tmp_path / "d.out")) == 136
     s.close()
 
 
