@@ -206,11 +206,11 @@ struct Network {
     // irregular cross sections: [TRANSECTS] and SHAPE curves (curveShape: the
     // shape of each curve, -1 for other curve types); xTab holds every table
     // block the kernels read (xsect.h tabDesc)
-    std::vector<XTable> transects, shapes;
+    std::vector<XTable> transects, shapes, streets;
     std::vector<int> curveShape;
     std::vector<double> xTab;
     std::unordered_map<std::string, int> nodeIndex, linkIndex, pollutIndex, patternIndex,
-        tseriesIndex, curveIndex, transectIndex;
+        tseriesIndex, curveIndex, transectIndex, streetIndex;
     std::string title;
 
     int nNodes() const { return (int)nodeId.size(); }

@@ -210,12 +210,12 @@ static bool getDouble(const char* s, double* y)
 enum Sect {
     S_NONE = -1, S_TITLE, S_OPTION, S_EVAP, S_JUNC, S_OUTFALL, S_CONDUIT, S_XSECT, S_LOSS,
     S_POLLUT, S_INFLOW, S_DWF, S_PATTERN, S_TSERIES, S_REPORT, S_FILES, S_STORAGE, S_CURVES,
-    S_PUMP, S_ORIFICE, S_WEIR, S_OUTLET, S_TRANSECT, S_DIVIDER, S_SKIP, S_UNSUPPORTED
+    S_PUMP, S_ORIFICE, S_WEIR, S_OUTLET, S_TRANSECT, S_DIVIDER, S_STREET, S_SKIP, S_UNSUPPORTED
 };
 static const char* const kSectWords[] = {
     "[TITLE", "[OPTION", "[EVAP", "[JUNC", "[OUTFALL", "[CONDUIT", "[XSECT", "[LOSS",
     "[POLLUT", "[INFLOW", "[DWF", "[PATTERN", "[TIMESERIES", "[REPORT", "[FILES", "[STORAGE",
-    "[CURVE", "[PUMP", "[ORIFICE", "[WEIR", "[OUTLET", "[TRANSECT", "[DIVIDER", nullptr};
+    "[CURVE", "[PUMP", "[ORIFICE", "[WEIR", "[OUTLET", "[TRANSECT", "[DIVIDER", "[STREET", nullptr};
 static const char* const kOffOnWords[] = {"OFF", "ON", nullptr};
 static const char* const kOrificeTypeWords[] = {"SIDE", "BOTTOM", nullptr};
 static const char* const kWeirTypeWords[] = {"TRANSVERSE", "SIDEFLOW", "V-NOTCH", "TRAPEZOIDAL",
@@ -440,6 +440,13 @@ int Project::parseLine(int sect, std::vector<char*>& tok, int pass)
         case S_DIVIDER:
             if (addId(net.nodeIndex, net.nodeId, tok[0]) < 0) return setError(207, std::string("ERROR 207: duplicate ID name ") + tok[0]);
             return 0;
+        case S_STREET:
+            if (net.streetIndex.count(tok[0]))
+                return setError(207, std::string("ERROR 207: duplicate ID name ") + tok[0]);
+            net.streetIndex.emplace(tok[0], (int)net.streets.size());
+            net.streets.push_back(XTable());
+            net.streets.back().id = tok[0];
+            return 0;
         case S_TRANSECT:
             if (kfind(tok[0], kTransectWords) == 1 && nt >= 2) {
                 if (net.transectIndex.count(tok[1]))
@@ -515,6 +522,7 @@ int Project::parseLine(int sect, std::vector<char*>& tok, int pass)
     case S_PUMP: case S_ORIFICE: case S_WEIR: case S_OUTLET: return readRegulator(sect, tok);
     case S_CURVES: return readCurve(tok);
     case S_TRANSECT: return readTransect(tok);
+    case S_STREET: return readStreet(tok);
     default: return 0;
     }
 }
@@ -928,8 +936,6 @@ int Project::readTransect(std::vector<char*>& tok)
         T.xRight *= T.xFactor;
         T.yFactor = x[9] / u;
         T.nStations = 0;
-        T.station.assign(1, 0.0);
-        T.elev.assign(1, 0.0);
         return 0;
     }
     if ((nt - 1) % 2 > 0) return 203;                   // GR elev station ...
@@ -940,8 +946,6 @@ int Project::readTransect(std::vector<char*>& tok)
         if (T.nStations < 0) return 219;                // addStation transect.c:360-384
         T.nStations++;
         if (T.nStations >= 1500) continue;
-        T.station.resize(T.nStations + 2, 0.0);
-        T.elev.resize(T.nStations + 2, 0.0);
         T.station[T.nStations] = x * T.xFactor / u;
         T.elev[T.nStations] = (y + T.yFactor) / u;
         if (T.nStations > 1 && T.station[T.nStations] < T.station[T.nStations - 1]) return 221;
@@ -1130,6 +1134,85 @@ bool shapeTables(XTable& t, const Curve& c)
 }
 }  // namespace
 
+// street_readParams (street.c:58-137) and transect_createStreetTransect
+// (transect.c:596-680), which builds the street's transect in the transect
+// module's shared arrays and roughness state
+int Project::readStreet(std::vector<char*>& tok)
+{
+    int nt = (int)tok.size();
+    if (nt < 5) return 203;
+    auto it = net.streetIndex.find(tok[0]);
+    if (it == net.streetIndex.end()) return 209;
+    double x[11];
+    for (int k = 0; k <= 10; k++) x[k] = 0.0;
+    for (int k = 1; k <= 4; k++)
+        if (!getDouble(tok[k], &x[k]) || x[k] <= 0.0) return 211;
+    if (nt > 5 && (!getDouble(tok[5], &x[5]) || x[5] < 0.0)) return 211;
+    if (nt > 6 && (!getDouble(tok[6], &x[6]) || x[6] < 0.0)) return 211;
+    int sides = 2;
+    if (nt > 7) {
+        char* e = nullptr;
+        long v = strtol(tok[7], &e, 10);
+        if (!e || *e || v < 1 || v > 2) return 211;
+        sides = (int)v;
+    }
+    if (nt > 8) {
+        if (!getDouble(tok[8], &x[8]) || x[8] < 0.0) return 211;
+        if (x[8] > 0.0) {
+            if (nt < 11) return 203;
+            for (int k = 9; k <= 10; k++)
+                if (!getDouble(tok[k], &x[k]) || x[k] <= 0.0) return 211;
+        }
+    }
+    double u = ucfLength();
+    double width = x[1] / u, curbHeight = x[2] / u, slope = x[3] / 100.0, roughness = x[4];
+    double gutterDepression = x[5] / u, gutterWidth = x[6] / u;
+    double backWidth = x[8] / u, backSlope = x[9] / 100.0, backRoughness = x[10];
+    TransectInput& T = tin_;
+    double ymin = 0.0;
+    double w1 = backWidth, w2 = gutterWidth, w3 = width, w4 = w3 - w2;
+    double y3 = gutterDepression + slope * w2;
+    double y1 = curbHeight + gutterDepression;
+    double ymax = backSlope * backWidth + y1;
+    double y4 = y3 + slope * w4;
+    ymax = gmax(ymax, y4);
+    T.station[0] = 0.0; T.elev[0] = ymax;
+    T.station[1] = w1; T.elev[1] = y1;
+    T.station[2] = w1; T.elev[2] = 0.0;
+    T.station[3] = w1 + w2; T.elev[3] = y3;
+    T.station[4] = w1 + w3; T.elev[4] = y4;
+    if (sides == 1) {
+        T.station[5] = T.station[4]; T.elev[5] = ymax;
+        T.nStations = 5;
+    } else {
+        T.station[5] = T.station[4] + w4; T.elev[5] = y3;
+        T.station[6] = T.station[5] + w2; T.elev[6] = 0.0;
+        T.station[7] = T.station[6]; T.elev[7] = y1;
+        T.station[8] = T.station[7] + w1; T.elev[8] = ymax;
+        T.nStations = 8;
+    }
+    T.nChannel = roughness;
+    if (backWidth == 0.0) {
+        T.nLeft = T.nChannel;
+        T.nRight = T.nChannel;
+        T.xLeft = T.station[0];
+        T.xRight = T.station[T.nStations];
+    } else {
+        T.nLeft = backRoughness;
+        T.nRight = T.nLeft;
+        T.xLeft = T.station[1];
+        T.xRight = (sides == 2) ? T.station[T.nStations - 1] : T.station[T.nStations];
+    }
+    XTable& t = net.streets[it->second];
+    t.nTbl = 51;
+    t.lengthFactor = 0.0;                             // never set for streets (calloc)
+    Slices S{T.station, T.elev, T.nStations, T.nLeft, T.nRight, T.nChannel, T.xLeft, T.xRight};
+    transectTables(t, S, ymin, ymax);
+    t.roughness = roughness;
+    t.valid = true;
+    return 0;
+}
+
 // transect_validate (transect.c:194-260)
 void Project::validateTransect(int j)
 {
@@ -1150,8 +1233,6 @@ void Project::validateTransect(int j)
         ymin = gmin(T.elev[i], ymin);
     }
     if (ymin >= ymax) { setError(231, "ERROR 231: transect " + id + " has no depth."); return; }
-    T.station.resize(T.nStations + 2, 0.0);
-    T.elev.resize(T.nStations + 2, 0.0);
     T.station[0] = T.station[1];
     T.elev[0] = ymax;
     T.nStations++;
@@ -1183,7 +1264,7 @@ void Project::buildXTables()
         net.shapes.push_back(t);
     }
     net.xTab.clear();
-    for (auto* v : {&net.transects, &net.shapes})
+    for (auto* v : {&net.transects, &net.shapes, &net.streets})
         for (XTable& t : *v) {
             if (t.nTbl <= 0) continue;
             t.blockOff = (int)net.xTab.size();
@@ -1691,9 +1772,13 @@ int Project::readXsect(std::vector<char*>& tok)  // link.c:162-267
     if (k < 0) return 205;
     if (net.linkType[j] == CONDUIT) net.barrels[j] = 1;
     net.xsect[j].culvertCode = 0;
-    if (k == X_STREET)
-        return setError(200, std::string("ERROR 200: cross-section shape ") + tok[1] +
-                                 " is not supported by the MI355X engine yet");
+    if (k == X_STREET) {                               // link.c:205-213
+        auto t = net.streetIndex.find(tok[2]);
+        if (t == net.streetIndex.end()) return 209;
+        net.xsect[j].type = k;
+        net.xsect[j].transect = t->second;
+        return 0;
+    }
     if (k == X_IRREGULAR) {                            // link.c:196-203
         auto t = net.transectIndex.find(tok[2]);
         if (t == net.transectIndex.end()) return 209;
@@ -2148,8 +2233,8 @@ void Project::validateConduit(int j)  // link.c:992-1154 (supported shapes)
         xs.sMax = t.sMax * yFull * yFull * pow(yFull, 2. / 3.);
         xs.aBot = t.aMax * yFull * yFull;
         tt = &t;
-    } else if (xs.type == X_IRREGULAR) {               // getTransectParams xsect.c:1323-1355
-        const XTable& t = net.transects[xs.transect];
+    } else if (xs.type == X_IRREGULAR || xs.type == X_STREET) {   // getTransectParams xsect.c:1323-1355
+        const XTable& t = (xs.type == X_IRREGULAR) ? net.transects[xs.transect] : net.streets[xs.transect];
         xs.yFull = t.yFull;
         xs.wMax = t.wMax;
         xs.aFull = t.aFull;
@@ -2157,7 +2242,7 @@ void Project::validateConduit(int j)  // link.c:992-1154 (supported shapes)
         xs.sFull = xs.aFull * pow(xs.rFull, 2. / 3.);
         xs.sMax = t.sMax;
         xs.aBot = t.aMax;
-        net.roughness[j] = t.roughness;
+        net.roughness[j] = t.roughness;               // transect / street roughness (link.c:1018-1029)
         tt = &t;
     }
     if (tt) {

@@ -84,6 +84,7 @@ private:
     int readCurve(std::vector<char*>& tok);
     int readTransect(std::vector<char*>& tok);
     int readDivider(std::vector<char*>& tok);
+    int readStreet(std::vector<char*>& tok);
     void validateTransect(int j);
     void buildXTables();
     // transect_readParams state carried from line to line (and, as in the
@@ -92,7 +93,10 @@ private:
         int count = 0, nStations = 0;
         double nLeft = 0, nRight = 0, nChannel = 0, xLeft = 0, xRight = 0, xFactor = 1,
                yFactor = 0, lFactor = 1;
-        std::vector<double> station, elev;
+        // transect.c's static Station / Elev arrays (MAXSTATION + 1 entries,
+        // zero-initialised, never cleared: entries past the current transect
+        // keep earlier values, which getFlow can read)
+        std::vector<double> station = std::vector<double>(1502, 0.0), elev = std::vector<double>(1502, 0.0);
     } tin_;
     int readRegulator(int sect, std::vector<char*>& tok);
     void validateRegulator(int j);

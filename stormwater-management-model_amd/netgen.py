@@ -382,7 +382,7 @@ def write_example(path: str, *, route_step: float = 5.0,
                   regulators: bool = False, shapes: bool = False,
                   force_main_eqn: str = "", irregular: bool = False,
                   culverts: bool = False, tidal: bool = False, roadway: bool = False,
-                  dividers: bool = False) -> None:
+                  dividers: bool = False, streets: bool = False) -> None:
     """Write the authored Example network (see module docstring).  `files`
     is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf");
     `storage` turns six junctions into storage units (_STORAGE)."""
@@ -455,6 +455,14 @@ def write_example(path: str, *, route_step: float = 5.0,
         txt = txt.replace("[CONDUITS]\n", "[DIVIDERS]\n;;Name Elev DivLink Type Params MaxDepth InitDepth "
                           "SurDepth Aponded\nN7  114.0  C17  CUTOFF  1.5  10  0  0  0\n"
                           "N12 108.7  C18  WEIR  0.5  1.0  3.0  10  0  0  0\n\n[CONDUITS]\n", 1)
+    if streets:
+        # street cross sections (street.c, transect_createStreetTransect): a
+        # two-sided street with a depressed gutter and backing, a one-sided one
+        txt = txt.replace("C4  RECT_OPEN    2.0  3.0  0    0  1", "C4   STREET  ST1")
+        txt = txt.replace("C16 RECT_OPEN    3.0  4.0  0    0  1", "C16  STREET  ST2")
+        txt = txt.replace("[LOSSES]\n", "[STREETS]\n;;Name Tcrown Hcurb Sx nRoad a W Sides Tback Sback nBack\n"
+                          "ST1  20  0.5  2  0.016  0.17  2  2  10  4  0.03\n"
+                          "ST2  15  0.6  3  0.015  0  0  1\n\n[LOSSES]\n", 1)
     regs_def = dict(_REGULATORS)
     if roadway:
         # roadway weirs (roadway.c): variable discharge coefficient on a paved

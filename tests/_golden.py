@@ -14,7 +14,8 @@ CASES = ["grid12", "grid12_var_qual", "grid10_surcharge", "example", "example_va
          "example_storage_var", "example_storage_qual", "example_regulators",
          "example_regulators_var_qual", "example_shapes", "example_shapes_var",
          "example_irregular", "example_irregular_var", "example_culverts", "example_culverts_var",
-         "example_tidal", "example_tidal_var", "example_roadway", "example_dividers"]
+         "example_tidal", "example_tidal_var", "example_roadway", "example_dividers",
+         "example_streets"]
 # cases using objects outside the C restatement's scope (oracle/dw_oracle.c
 # covers junctions, outfalls and conduits): pinned by the GPU tests against the
 # reference's own fixtures only
@@ -22,7 +23,7 @@ BEYOND_ORACLE = {"example_storage", "example_storage_var", "example_storage_qual
                  "example_regulators", "example_regulators_var_qual", "example_shapes",
                  "example_shapes_var", "example_irregular", "example_irregular_var",
                  "example_culverts", "example_culverts_var", "example_tidal", "example_tidal_var",
-                 "example_roadway", "example_dividers"}
+                 "example_roadway", "example_dividers", "example_streets"}
 # cases whose input writes a file next to itself ([FILES] SAVE ...): they run
 # from a private copy so the fixtures directory is never written to
 SAVES = {"example_hotsave": "example_hotsave.hsf"}
@@ -35,7 +36,7 @@ GRID_CONC = [5.0, 10.0, 15.0, 20.0, 25.0, 30.0]
 # ill-conditioned cases: the fixture carries the reference's build-to-build
 # spread ("env.*", tests/golden/make_golden.py ENVELOPE)
 ENVELOPE = {"example_shapes", "example_shapes_var", "example_irregular", "example_irregular_var",
-            "example_culverts", "example_culverts_var"}
+            "example_culverts", "example_culverts_var", "example_streets"}
 
 
 def first_divergence(d, node_f, link_f, rtol, atol):

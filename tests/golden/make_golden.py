@@ -37,7 +37,7 @@ REFDUMP_X87 = os.path.join(ROOT, "oracle", "_ref", "x87", "refdump")
 # array, the largest |FMA build - reference| ("env.<key>"), made with
 # `make -C oracle ref-fma`
 ENVELOPE = {"example_shapes", "example_shapes_var", "example_irregular", "example_irregular_var",
-            "example_culverts", "example_culverts_var"}
+            "example_culverts", "example_culverts_var", "example_streets"}
 
 # name -> (writer, kwargs, every)
 CASES = {
@@ -102,6 +102,8 @@ CASES = {
     # flow dividers (routed as junctions under dynamic wave)
     "example_dividers": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, dividers=True,
                                                     pollutants=True), 1),
+    # street cross sections (street.c)
+    "example_streets": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, streets=True), 1),
     # swmm_setValue between steps: external inflow, outfall stage, routing step
     "example_api": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
                                                variable_step=0.75), 1),

@@ -94,7 +94,7 @@ def test_missing_input_file(tmp_path):
 @pytest.mark.parametrize("section", ["[SUBCATCHMENTS]\nS1 RG1 N1 1 25 500 0.5 0\n",
                                      "[STORAGE]\nST1 100 10 0 FUNCTIONAL 1000 0 0 0 0 1.5\n",
                                      "[CONTROLS]\nRULE R1\nIF NODE N1 DEPTH > 1\nTHEN LINK C1 STATUS = OFF\n",
-                                     "[STREETS]\nS1 20 0.5 2 0.016\n"])
+                                     "[INLETS]\nI1 GRATE 2 2 P_BAR-50\n"])
 def test_unsupported_sections_fail_loudly(section, tmp_path):
     src = open(_golden.inp("example")).read()
     p = tmp_path / "u.inp"
