@@ -1851,8 +1851,14 @@ int Project::readPollutant(std::vector<char*>& tok)  // landuse.c:readPollutPara
     if (!getDouble(tok[5], &x[3])) return 211;
     double cDWF = 0.0, cInit = 0.0;
     if (nt >= 7 && kfind(tok[6], kNoYes) < 0) return 205;
-    if (nt >= 9 && strcmp(tok[7], "*") != 0)
-        return setError(200, "ERROR 200: co-pollutants are not supported by the MI355X engine");
+    // co-pollutant (landuse.c:144-154): validated like the reference; it only
+    // adds to runoff washoff (landuse_getCoPollutLoad), and a network without
+    // subcatchments has none, so it leaves routing unchanged
+    if (nt >= 9 && strcmp(tok[7], "*") != 0) {
+        if (!net.pollutIndex.count(tok[7])) return 209;
+        double coFrac;
+        if (!getDouble(tok[8], &coFrac) || coFrac < 0.0) return 211;
+    }
     if (nt >= 10 && (!getDouble(tok[9], &cDWF) || cDWF < 0.0)) return 211;
     if (nt >= 11 && (!getDouble(tok[10], &cInit) || cInit < 0.0)) return 211;
     Pollutant& p = net.pollut[j];
