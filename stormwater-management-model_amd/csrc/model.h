@@ -99,6 +99,7 @@ struct Pattern {
 struct Tseries {
     std::string id;
     std::vector<double> x, y;
+    std::string file;            // external data file (FILE keyword), read at validation
     double lastDate = 0.0;
     // lookup cursor (table.c:730-806)
     double x1 = 0, y1 = 0, x2 = 0, y2 = 0;

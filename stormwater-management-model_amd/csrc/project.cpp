@@ -1987,8 +1987,12 @@ int Project::readTimeseries(std::vector<char*>& tok)  // table.c:113-202
     int nt = (int)tok.size();
     if (nt < 3) return 203;
     Tseries& ts = net.tseries[net.tseriesIndex.at(tok[0])];
-    if (kmatch(tok[1], "FILE"))
-        return setError(200, "ERROR 200: external time series files are not supported by the MI355X engine");
+    if (kmatch(tok[1], "FILE")) {                       // table.c:143-149
+        std::string fname = tok[2];
+        bool rel = !(strchr(fname.c_str(), ':') || fname[0] == '\\' || fname[0] == '/');
+        ts.file = rel ? inpDir + fname : fname;
+        return 0;
+    }
     double x = 0.0, y, d, t;
     int k = 1, state = 1;
     while (k < nt) {
@@ -2412,6 +2416,37 @@ void Project::validateRegulator(int j)
 void Project::validate()  // project.c:186-270
 {
     int nn = net.nNodes(), nl = net.nLinks();
+    for (auto& ts : net.tseries) {
+        // an external file's entries (table_validate / table_parseFileLine,
+        // table.c:290-330, 833-895): "date time value" or "time value" lines,
+        // the date carried from the last dated line; ';' starts a comment
+        if (ts.file.empty()) continue;
+        FILE* fp = fopen(ts.file.c_str(), "rt");
+        if (!fp) { setError(361, "ERROR 361: could not open external file used for Time Series " + ts.id); return; }
+        char line[1025];
+        bool bad = false;
+        while (fgets(line, sizeof line, fp)) {
+            char s1[50] = "", s2[50] = "", s3[50] = "";
+            int n = sscanf(line, "%49s %49s %49s", s1, s2, s3);
+            if (n <= 0 || s1[0] == ';') continue;
+            double d, t, y;
+            const char *tStr, *yStr;
+            if (n == 2) { d = ts.lastDate; tStr = s1; yStr = s2; }
+            else if (n == 3) {
+                if (!strToDate(s1, &d)) { bad = true; break; }
+                ts.lastDate = d;
+                tStr = s2;
+                yStr = s3;
+            } else { bad = true; break; }
+            if (getDouble(tStr, &t)) t /= 24.0;
+            else if (!strToTime(tStr, &t)) { bad = true; break; }
+            if (!getDouble(yStr, &y)) { bad = true; break; }
+            ts.x.push_back(d + t);
+            ts.y.push_back(y);
+        }
+        fclose(fp);
+        if (bad || ts.x.empty()) { setError(363, "ERROR 363: invalid data in external file used for Time Series " + ts.id); return; }
+    }
     for (auto& ts : net.tseries)
         for (size_t i = 1; i < ts.x.size(); i++)
             if (ts.x[i] <= ts.x[i - 1]) { setError(173, "ERROR 173: time series " + ts.id + " has its data out of sequence."); return; }

@@ -382,7 +382,7 @@ def write_example(path: str, *, route_step: float = 5.0,
                   regulators: bool = False, shapes: bool = False,
                   force_main_eqn: str = "", irregular: bool = False,
                   culverts: bool = False, tidal: bool = False, roadway: bool = False,
-                  dividers: bool = False, streets: bool = False) -> None:
+                  dividers: bool = False, streets: bool = False, extfile: bool = False) -> None:
     """Write the authored Example network (see module docstring).  `files`
     is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf");
     `storage` turns six junctions into storage units (_STORAGE)."""
@@ -500,6 +500,18 @@ def write_example(path: str, *, route_step: float = 5.0,
             txt = txt.replace("SC1           9  1500\n", "SC1           9  1500\n" + _REGULATOR_CURVES)
     if files:
         txt += "\n[FILES]\n" + files.rstrip("\n") + "\n"
+    if extfile:
+        # HYD1 read from an external time series file (table.c:833-895):
+        # undated, dated and commented lines
+        dat = os.path.splitext(os.path.basename(path))[0] + "_hyd1.dat"
+        out = [ln for ln in txt.split("\n") if not ln.startswith("HYD1  ")]
+        txt = "\n".join(out).replace("[TIMESERIES]\n;;Name Date Time Value\n",
+                                      "[TIMESERIES]\n;;Name Date Time Value\nHYD1  FILE  \"%s\"\n" % dat, 1)
+        d0 = os.path.dirname(os.path.abspath(path))
+        os.makedirs(d0, exist_ok=True)
+        with open(os.path.join(d0, dat), "w") as g:
+            g.write(";HYD1 inflow hydrograph\n0:00  0.0\n0:15  4.0\n01/01/2020 0:30  9.0\n"
+                    "1:00  6.0\n\n; recession\n01/01/2020 1:30  2.0\n3:00  0.0\n")
     d = os.path.dirname(os.path.abspath(path))
     os.makedirs(d, exist_ok=True)
     with open(path, "w") as f:

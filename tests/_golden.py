@@ -15,7 +15,7 @@ CASES = ["grid12", "grid12_var_qual", "grid10_surcharge", "example", "example_va
          "example_regulators_var_qual", "example_shapes", "example_shapes_var",
          "example_irregular", "example_irregular_var", "example_culverts", "example_culverts_var",
          "example_tidal", "example_tidal_var", "example_roadway", "example_dividers",
-         "example_streets"]
+         "example_streets", "example_extfile"]
 # cases using objects outside the C restatement's scope (oracle/dw_oracle.c
 # covers junctions, outfalls and conduits): pinned by the GPU tests against the
 # reference's own fixtures only

@@ -104,6 +104,8 @@ CASES = {
                                                     pollutants=True), 1),
     # street cross sections (street.c)
     "example_streets": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, streets=True), 1),
+    # inflow hydrograph from an external time series file
+    "example_extfile": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, extfile=True), 1),
     # swmm_setValue between steps: external inflow, outfall stage, routing step
     "example_api": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
                                                variable_step=0.75), 1),
