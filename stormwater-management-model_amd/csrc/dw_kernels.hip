@@ -2629,16 +2629,23 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     int maxBlocks = 8 * std::max(prop.multiProcessorCount, 1);
     // streaming kernels: one resident wave of workgroups (grid-stride loops),
     // so early-exited Picard iterations dispatch few workgroups
-    auto resident = [&](const void* fn, int n) {
+    auto resident = [&](const void* fn, int n, double factor = 1.0) {
         int per = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kBlock, 0) != hipSuccess || per < 1)
             per = 2;
-        int cap = per * std::max(prop.multiProcessorCount, 1);
+        int cap = (int)(per * std::max(prop.multiProcessorCount, 1) * factor);
         if (const char* g = getenv("SWMM5_GRID_FACTOR")) cap = (int)(cap * atof(g));
         return std::max(1, std::min((n + kBlock - 1) / kBlock, std::max(cap, 1)));
     };
     d->gridL = resident((const void*)linkKernel(false, d->linkWaves, d->fastLinks), nL);
-    d->gridN = resident((const void*)nodeKernel(false, d->general), nN);
+    // k_node: two resident waves of workgroups.  Its per-node work is short
+    // and gather-latency bound, and the extra workgroups keep more gathers in
+    // flight (SWMM5_GRID_FACTOR sweep on the 1M surcharged grid: k_node 24.7 ->
+    // 22.7 us per iteration, the streaming link kernel unchanged, the step-end
+    // kernel slower, so only k_node takes it)
+    double nodeFactor = 2.0;
+    if (const char* g = getenv("SWMM5_NODE_GRID_FACTOR")) nodeFactor = atof(g);
+    d->gridN = resident((const void*)nodeKernel(false, d->general), nN, nodeFactor);
     d->gridC = std::max(1, std::min((p.nCold + kBlock - 1) / kBlock, maxBlocks));
     d->gridEnd = resident((const void*)stepEndKernel(d->fastLinks, d->allShapes),
                           std::max(nN, nL));

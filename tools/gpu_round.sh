@@ -26,7 +26,8 @@ for s in $STEPS; do
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --no-cpu ;;
     probe)  run probe 120 ./tools/outfall_latency ;;
     mrehearse) run mrehearse 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 5 --grid 120 --spinup 50 --exchange host --no-cpu ;;
-    gsweep) for g in 0.34 0.67 2; do SWMM5_GRID_FACTOR=$g run gsweep_$g 300 python bench.py --no-cpu; done ;;
+    gsweep) for g in ${GFACTORS:-0.34 0.67 2}; do SWMM5_GRID_FACTOR=$g run gsweep_$g 300 python bench.py --no-cpu; done ;;
+    nsweep) for g in ${NFACTORS:-1 2 3}; do SWMM5_NODE_GRID_FACTOR=$g run nsweep_$g 300 python bench.py --no-cpu; done ;;
     sweep)  for w in 1 3 4 5; do SWMM5_LINK_WAVES=$w run sweep_w$w 300 python bench.py --steps 200 --no-cpu; done ;;
     pmc)    run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu \
               && run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu ;;
