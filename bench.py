@@ -79,8 +79,8 @@ def cpu_baseline(dump, steps, q, route_step, variable):
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _dumpio import read_dump
-    from _oracle import oracle_from_dump
-    o = oracle_from_dump(read_dump(dump))
+    from _oracle import oracle_resume
+    o = oracle_resume(read_dump(dump))
     lat = np.full(o.nN, q)
     lat[-1] = 0.0                       # the outfall has no DWF
     o.d("node.latIn")[:] = lat

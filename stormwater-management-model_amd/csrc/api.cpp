@@ -859,7 +859,7 @@ int DLLEXPORT swmmx_exportState(const char* path)
         const Options& o = prj.opt;
         double od[12] = {o.routeStep, o.courantFactor, o.minRouteStep, o.minSurfArea, o.headTol,
                          o.crownCutoff, o.lengtheningStep, o.evapRate, o.totalDuration,
-                         (double)o.reportStep, o.startDateTime, 0.0};
+                         (double)o.reportStep, o.startDateTime, prj.st.variableStep};
         int oi[12] = {o.maxTrials, o.surchargeMethod, o.inertDamping, o.normalFlowLtd,
                       o.allowPonding, o.routeModel, o.forceMainEqn, o.flowUnits, o.unitSystem,
                       o.ignoreQuality, 0, 0};

@@ -158,3 +158,20 @@ def oracle_from_dump(d: dict) -> Oracle:
         o.d("pollut.kDecay")[:] = d["pollut.kDecay"]
     o.prepare()
     return o
+
+
+def oracle_resume(d: dict) -> Oracle:
+    """Oracle seeded from a mid-run engine dump (swmmx_exportState): the state
+    of oracle_from_dump plus what persists across steps -- Xnode.oldSurfArea
+    (surcharge denominator, dynwave.c:700, 728-729), Xnode.dYdT and the static
+    VariableStep of the Courant step (dynwave.c:84, 209-218, 878-921)."""
+    o = oracle_from_dump(d)
+    for k in ("node.oldSurfArea", "node.dYdT", "link.froude"):
+        if k in d:
+            o.d(k)[:] = d[k]
+    if o.nP:
+        for k in ("node.newQual", "node.oldQual", "link.newQual", "link.oldQual"):
+            if k in d:
+                o.d(k)[:] = d[k]
+    o.opt("variableStep", float(d["opt.d"][11]))
+    return o

@@ -66,10 +66,13 @@ def _dates_agree(a, b, frac=0.97, value=None, series=None, times=None, spread=No
     same = np.isclose(a, b, rtol=0, atol=1e-9)
     if spread is not None:
         same |= spread > 0            # the reference's own builds disagree on this date
-    if same.mean() >= frac:
+    if same.size == 0 or same.all():
         return
-    assert value is not None, (same.mean(), np.nonzero(~same)[0][:10])
-    for i in np.nonzero(~same)[0]:
+    if value is None or times is None:
+        # no per-step series recorded: only a small share may differ
+        assert same.mean() >= frac, (same.mean(), np.nonzero(~same)[0][:10])
+        return
+    for i in np.nonzero(~same)[0]:    # every other date must sit on a plateau of the series
         k = int(np.argmin(np.abs(times - a[i])))
         assert abs(times[k] - a[i]) < 1e-6, (i, a[i])        # the step of our date
         assert np.isclose(series[k][i], value[i], rtol=1e-6, atol=1e-9), (i, series[k][i], value[i])

@@ -189,12 +189,18 @@ def _merge(parts):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kw", [dict(route_step=1.0),
-                                dict(route_step=5.0, variable_step=0.75, diameter=1.0, q=0.1)])
-def test_two_ranks_match_one_gpu(kw, tmp_path):
+@pytest.mark.parametrize("kw,steps,surcharged", [
+    (dict(route_step=1.0), 120, False),
+    # the benchmark's regime: surcharged, non-converging, iterations >= 2 with
+    # bypassed conduits on both ranks and the cross-rank convergence flag
+    (dict(route_step=5.0, variable_step=0.75, diameter=1.0, q=0.5), 250, True)])
+def test_two_ranks_match_one_gpu(kw, steps, surcharged, tmp_path):
     inp = _grid(tmp_path, 30, 30, **kw)
-    steps = 120
     one = _run_workers(inp, steps, tmp_path, 1, "host", "one")[0]
+    if surcharged:
+        st, its, nonconv = one["counters"]
+        assert nonconv > 20 and its / st > 3.0, one["counters"]
+        assert (one["node.newDepth"][:-1] > kw["diameter"]).sum() > 100
     parts = _run_workers(inp, steps, tmp_path, 2, "host", "two")
     node, link = _merge(parts)
     for k, v in node.items():
