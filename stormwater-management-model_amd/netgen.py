@@ -271,6 +271,36 @@ DRY_ONLY  NO
 """
 
 
+# ponding variant: shallow upstream junctions with ponded areas (they flood
+# under the HYD1 / HYD2 inflows) -> (original line, replacement)
+_PONDING = {
+    "N1": ("N1  120.0  8  0.0  0  0\n", "N1  120.0  2.5  0.0  0  1500\n"),
+    "N5": ("N5  119.0  7  0    0  0\n", "N5  119.0  2.0  0    0  800\n"),
+    "N10": ("N10 113.2  6  0    0  0\n", "N10 113.2  2.0  0    0  400\n"),
+}
+
+# backwater branch (appended to the Example network): outfall O3's stage rises
+# above the downstream end of CB1, whose upstream end sits 1.5 ft above B1's
+# invert, so water flows back over the offset into the dry B1 (UP_CRITICAL,
+# dwflow.c:391, then dwflow.c:347 once B1 is wet); it also backs up over the
+# crest of weir WB into B3 (UP_CRITICAL, link.c:2274); the depth-curve pump
+# PB starts at 0.5 ft (DN_DRY below it, link.c:1624)
+_BRANCHES = {
+    "[JUNCTIONS]": "B1  110.0  8  0  0  0\nB2  109.5  8  0  0  0\nB3  109.0  8  0  0  0\n"
+                   "B4  108.8  8  0  0  0\n",
+    "[OUTFALLS]": "O3  108.5  TIMESERIES  STAGE3  NO\nO4  108.0  FREE  NO\n",
+    "[CONDUITS]": "CB1 B1  B2  300  0.013  1.5  0  0  0\nCB2 B2  O3  250  0.013  0  0  0  0\n"
+                  "CB3 B4  O4  200  0.013  0  0  0  0\n",
+    "[PUMPS]": "PB  B3  B4  P5  ON  0  0\n",
+    "[WEIRS]": "WB  B3  B2  TRANSVERSE  1.0  3.33  NO  0  0  NO\n",
+    "[XSECTIONS]": "CB1 CIRCULAR  1.5  0  0  0  1\nCB2 CIRCULAR  2.0  0  0  0  1\n"
+                   "CB3 CIRCULAR  1.5  0  0  0  1\nWB  RECT_OPEN  3.0  4.0  0  0\n",
+    "[TIMESERIES]": "STAGE3  0:00  108.6\nSTAGE3  0:20  112.5\nSTAGE3  0:50  113.0\n"
+                    "STAGE3  1:20  110.0\nSTAGE3  1:50  108.6\n",
+    "[CURVES]": "P5   Pump4  0.5   0.0\nP5          1.0   1.0\nP5          3.0   2.0\n",
+    "[DWF]": "B3   FLOW  0.05\n",
+}
+
 # pumps (all curve types + ideal), side / bottom orifices, transverse and
 # V-notch weirs, functional and tabular outlets replacing conduits of the
 # storage variant (link.c:1406-2692): name -> (section line, xsection line)
@@ -382,10 +412,18 @@ def write_example(path: str, *, route_step: float = 5.0,
                   regulators: bool = False, shapes: bool = False,
                   force_main_eqn: str = "", irregular: bool = False,
                   culverts: bool = False, tidal: bool = False, roadway: bool = False,
-                  dividers: bool = False, streets: bool = False, extfile: bool = False) -> None:
+                  dividers: bool = False, streets: bool = False, extfile: bool = False,
+                  options: dict | None = None, ponding: bool = False,
+                  branches: bool = False) -> None:
     """Write the authored Example network (see module docstring).  `files`
     is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf");
-    `storage` turns six junctions into storage units (_STORAGE)."""
+    `storage` turns six junctions into storage units (_STORAGE); `options`
+    sets or adds [OPTIONS] keywords (e.g. {"SURCHARGE_METHOD": "SLOT"});
+    `ponding` gives three upstream junctions shallow maximum depths and ponded
+    areas (flooding and ponding, dynwave.c:661-795, node.c:562-585);
+    `branches` adds the backwater branch _BRANCHES (reverse flow over an
+    invert offset and a weir crest: UP_CRITICAL, dwflow.c:347, 391,
+    link.c:2274; a depth-curve pump below its curve: DN_DRY, link.c:1624)."""
     if pollutants:
         pollut = ("TSS MG/L 0 0 0 0.5 NO * 0 20 0\n"
                   "BOD MG/L 0 0 0 0 NO * 0 10 0\n")
@@ -498,6 +536,25 @@ def write_example(path: str, *, route_step: float = 5.0,
         txt += "\n".join(_STORAGE.values()) + "\n" + _STORAGE_EXTRA
         if regulators:
             txt = txt.replace("SC1           9  1500\n", "SC1           9  1500\n" + _REGULATOR_CURVES)
+    if ponding:
+        for name, (old_ln, new_ln) in _PONDING.items():
+            assert old_ln in txt, name
+            txt = txt.replace(old_ln, new_ln)
+    if branches:
+        for sect, body in _BRANCHES.items():
+            if sect in txt:
+                txt = txt.replace(sect + "\n", sect + "\n" + body, 1)
+            else:
+                txt += "\n" + sect + "\n" + body
+    if options:
+        lines = txt.split("\n")
+        for key, val in options.items():
+            hit = [i for i, ln in enumerate(lines) if ln.split()[:1] == [key]]
+            if hit:
+                lines[hit[0]] = "%s %s" % (key, val)
+            else:
+                lines.insert(lines.index("[OPTIONS]") + 1, "%s %s" % (key, val))
+        txt = "\n".join(lines)
     if files:
         txt += "\n[FILES]\n" + files.rstrip("\n") + "\n"
     if extfile:

@@ -15,7 +15,8 @@ CASES = ["grid12", "grid12_var_qual", "grid10_surcharge", "example", "example_va
          "example_regulators_var_qual", "example_shapes", "example_shapes_var",
          "example_irregular", "example_irregular_var", "example_culverts", "example_culverts_var",
          "example_tidal", "example_tidal_var", "example_roadway", "example_dividers",
-         "example_streets", "example_extfile"]
+         "example_streets", "example_extfile", "example_branches", "example_branches_var",
+         "example_slot_pond", "example_options", "grid10_slot"]
 # cases using objects outside the C restatement's scope (oracle/dw_oracle.c
 # covers junctions, outfalls and conduits): pinned by the GPU tests against the
 # reference's own fixtures only
@@ -23,13 +24,14 @@ BEYOND_ORACLE = {"example_storage", "example_storage_var", "example_storage_qual
                  "example_regulators", "example_regulators_var_qual", "example_shapes",
                  "example_shapes_var", "example_irregular", "example_irregular_var",
                  "example_culverts", "example_culverts_var", "example_tidal", "example_tidal_var",
-                 "example_roadway", "example_dividers", "example_streets"}
+                 "example_roadway", "example_dividers", "example_streets", "example_branches",
+                 "example_branches_var"}
 # cases whose input writes a file next to itself ([FILES] SAVE ...): they run
 # from a private copy so the fixtures directory is never written to
 SAVES = {"example_hotsave": "example_hotsave.hsf"}
 # DWF-only networks: lateral inflow is constant and pollutant loads are
 # q * concentration, so the oracle can be fed without the inflow machinery
-DWF_ONLY = {"grid12", "grid12_var_qual", "grid10_surcharge"}
+DWF_ONLY = {"grid12", "grid12_var_qual", "grid10_surcharge", "grid10_slot"}
 GRID_CONC = [5.0, 10.0, 15.0, 20.0, 25.0, 30.0]
 
 

@@ -106,6 +106,34 @@ CASES = {
     "example_streets": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, streets=True), 1),
     # inflow hydrograph from an external time series file
     "example_extfile": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, extfile=True), 1),
+    # every flow class (dwflow.c:297-413): backwater over an invert offset and
+    # a weir crest (UP_CRITICAL), a depth-curve pump below its curve (DN_DRY)
+    "example_branches": (netgen.write_example, dict(end_time="01:40:00", route_step=5.0, branches=True), 1),
+    "example_branches_var": (netgen.write_example, dict(end_time="01:40:00", route_step=10.0,
+                                                        variable_step=0.75, branches=True,
+                                                        options={"INERTIAL_DAMPING": "NONE"}), 1),
+    # Preissmann slot surcharge (dwflow.c:575-588, dynwave.c:159), ponding
+    # (dynwave.c:309, 661, 766-795), full inertial damping, slope-only
+    # normal-flow limitation
+    "example_slot_pond": (netgen.write_example, dict(end_time="01:40:00", route_step=5.0, ponding=True,
+                                                     options={"SURCHARGE_METHOD": "SLOT",
+                                                              "ALLOW_PONDING": "YES",
+                                                              "NORMAL_FLOW_LIMITED": "SLOPE",
+                                                              "INERTIAL_DAMPING": "FULL"}), 1),
+    # no inertial damping, Froude-only normal-flow limitation, conduit
+    # lengthening (link.c:1104-1118, 1217-1254), ponding under EXTRAN
+    "example_options": (netgen.write_example, dict(end_time="01:40:00", route_step=30.0,
+                                                   variable_step=0.75, ponding=True,
+                                                   options={"ALLOW_PONDING": "YES",
+                                                            "INERTIAL_DAMPING": "NONE",
+                                                            "NORMAL_FLOW_LIMITED": "FROUDE",
+                                                            "LENGTHENING_STEP": "60"}), 1),
+    # the surcharged grid under the slot method, no normal-flow limitation
+    "grid10_slot": (netgen.write_grid, dict(nx=10, ny=10, end_time="00:40:00", variable_step=0.75,
+                                            route_step=5, diameter=1.0, q=0.1,
+                                            extra_options=("SURCHARGE_METHOD SLOT",
+                                                           "NORMAL_FLOW_LIMITED NONE",
+                                                           "INERTIAL_DAMPING NONE")), 3),
     # swmm_setValue between steps: external inflow, outfall stage, routing step
     "example_api": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
                                                variable_step=0.75), 1),
