@@ -38,7 +38,8 @@ GRID_CONC = [5.0, 10.0, 15.0, 20.0, 25.0, 30.0]
 # ill-conditioned cases: the fixture carries the reference's build-to-build
 # spread ("env.*", tests/golden/make_golden.py ENVELOPE)
 ENVELOPE = {"example_shapes", "example_shapes_var", "example_irregular", "example_irregular_var",
-            "example_culverts", "example_culverts_var", "example_streets"}
+            "example_culverts", "example_culverts_var", "example_streets", "example_branches",
+            "example_branches_var"}
 
 
 def first_divergence(d, node_f, link_f, rtol, atol):
@@ -80,6 +81,15 @@ def fma_out(name: str) -> bytes:
 
 def fma_rpt(name: str) -> str:
     with open(os.path.join(GOLDEN, name + ".fma_rpt.txt")) as f:
+        return f.read()
+
+
+def x87_rpt(name: str) -> str | None:
+    """The reference x87 build's report (ill-conditioned cases), if stored."""
+    p = os.path.join(GOLDEN, name + ".x87_rpt.txt")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
         return f.read()
 
 

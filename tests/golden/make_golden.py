@@ -37,7 +37,12 @@ REFDUMP_X87 = os.path.join(ROOT, "oracle", "_ref", "x87", "refdump")
 # array, the largest |FMA build - reference| ("env.<key>"), made with
 # `make -C oracle ref-fma`
 ENVELOPE = {"example_shapes", "example_shapes_var", "example_irregular", "example_irregular_var",
-            "example_culverts", "example_culverts_var", "example_streets"}
+            "example_culverts", "example_culverts_var", "example_streets", "example_branches",
+            "example_branches_var"}
+
+# envelope cases whose report tables also carry the x87 build's report (the
+# report test then accepts twice the larger of the two builds' differences)
+X87_RPT = {"example_branches", "example_branches_var"}
 
 # name -> (writer, kwargs, every)
 CASES = {
@@ -188,6 +193,9 @@ def make(name):
             d["env." + k] = e[k]
         with open(tmp + "_fma.rpt", "rb") as f, open(os.path.join(HERE, name + ".fma_rpt.txt"), "wb") as g:
             g.write(f.read())
+        if name in X87_RPT:
+            with open(tmp + "_x87.rpt", "rb") as f, open(os.path.join(HERE, name + ".x87_rpt.txt"), "wb") as g:
+                g.write(f.read())
         with open(tmp + "_fma.out", "rb") as f:
             np.save(os.path.join(HERE, name + ".fma_out.npy"), np.frombuffer(f.read(), dtype=np.uint8))
     if name in ACTIONS:
