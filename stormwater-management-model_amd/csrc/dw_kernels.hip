@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <map>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -80,7 +82,14 @@ enum : uint32_t {
     LF_NC = 1u << 23,             // pump / orifice / weir / outlet (k_nc; also LF_COLD)
     LF_PUMP = 1u << 24,
     LF_CULVERT_SHIFT = 25,        // bits 25-30 culvert code (cold conduits only)
+    LF_GEOM_SHIFT = 25,           // bits 25-31 geometry id (streaming conduits, kFast only)
 };
+// kFast: the streaming conduits' distinct circular sections (at most kGeomMax)
+// are one table staged into LDS behind the circular tables; a conduit carries
+// its section's id in LF_GEOM_SHIFT instead of loading 7 geometry doubles
+constexpr int kGeomMax = 128;
+constexpr int kGeomVals = 7;      // yFull wMax aFull rFull sFull sMax ywMax
+constexpr int kCtFast = 5 * SWX_CIRC_N + kGeomVals * kGeomMax;
 // ---- packed per-node flags -------------------------------------------------
 enum : uint32_t {
     NF_TYPE = 0x3u,               // node type
@@ -215,7 +224,9 @@ struct Params {
     const double* qualIn;         // mass loads for this step [p][node]
     const double* kDecay;
     // misc
-    const double* gTables;        // global copy of the 5x51 circular tables
+    const double* gTables;        // global copy of the 5x51 circular tables, then
+                                  // (kFast) nGeom x kGeomVals section geometries
+    int nGeom;
     const double* gShapeTab;      // SWX_SHAPE_TAB: tabulated shapes' geometry
     const double* gXTab;          // transect / custom-shape table blocks (Network::xTab)
     const int* lTabOff;           // per link: its block in gXTab (-1: none); null without any
@@ -249,10 +260,18 @@ struct Params {
 // kFast: every streaming conduit is CIRCULAR and the surcharge method is not
 // SLOT (host-checked); the shape switches and the slot branch then fold away.
 template <bool kFast = false>
-__device__ __forceinline__ Geom loadGeom(const Params& p, int j, uint32_t f)
+__device__ __forceinline__ Geom loadGeom(const Params& p, int j, uint32_t f, const double* ct = nullptr)
 {
     Geom g;
-    g.type = kFast ? (int)G_CIRCULAR : (int)(f & LF_XTYPE);
+    if (kFast) {                  // LDS geometry table (stageTables with kFast)
+        const double* t = ct + 5 * SWX_CIRC_N + kGeomVals * (int)(f >> LF_GEOM_SHIFT);
+        g.type = G_CIRCULAR;
+        g.yFull = t[0]; g.wMax = t[1]; g.aFull = t[2]; g.rFull = t[3];
+        g.sFull = t[4]; g.sMax = t[5]; g.ywMax = t[6];
+        g.yBot = g.aBot = g.sBot = g.rBot = 0.0;
+        return g;
+    }
+    g.type = (int)(f & LF_XTYPE);
     g.yFull = p.yFull[j];
     g.wMax = p.wMax[j];
     g.aFull = p.aFull[j];
@@ -417,7 +436,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     int n1 = nn.x, n2 = nn.y;
     const double off1 = kCold ? p.off1[j] : 0.0;     // hot links: both offsets are 0
     const double off2 = kCold ? p.off2[j] : 0.0;
-    Geom x = loadGeom<kFast>(p, j, f);
+    Geom x = loadGeom<kFast>(p, j, f, ct);
     double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
 
     // iteration 0: link_setOldHydState (link.c:564-583), a2 <- a1 (dynwave.c:292)
@@ -545,8 +564,10 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         p.lNewDepth[j] = gmin(yMid, x.yFull);
         p.lNewVolume[j] = a1n * len0 * barrels;
         p.lNewFlow[j] = 0.0;
-        p.evapLoss[j] = 0.0;
-        p.seepLoss[j] = 0.0;
+        if (f & LF_SEEP) {            // always 0 without LF_SEEP: not rewritten
+            p.evapLoss[j] = 0.0;
+            p.seepLoss[j] = 0.0;
+        }
         int old = p.lstate[j];
         p.lstate[j] = (old & ~0xF) | fc;      // fullState / normalFlow / inletControl untouched (dwflow.c:165-180)
         return;
@@ -666,8 +687,10 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     else if (a2 >= x.aFull) fs = FS_DN_FULL;
     p.lNewVolume[j] = aAvg * len0 * barrels;
     p.lNewFlow[j] = q * barrels;
-    p.evapLoss[j] = evapRate;
-    p.seepLoss[j] = seepRate;
+    if (f & LF_SEEP) {
+        p.evapLoss[j] = evapRate;
+        p.seepLoss[j] = seepRate;
+    }
     int old = p.lstate[j];
     p.lstate[j] = (old & (1 << 9)) | fc | (fs << 4) | (normalFlow << 8) | (inletCtl << 10);
 }
@@ -675,9 +698,10 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
 // ===========================================================================
 //  kernels
 // ===========================================================================
-__device__ __forceinline__ void stageTables(double* ct, const double* g)
+__device__ __forceinline__ void stageTables(double* ct, const double* g, int nGeom = 0)
 {
-    for (int i = threadIdx.x; i < 5 * SWX_CIRC_N; i += blockDim.x) ct[i] = g[i];
+    const int n = 5 * SWX_CIRC_N + kGeomVals * nGeom;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) ct[i] = g[i];
     __syncthreads();
 }
 
@@ -691,12 +715,12 @@ void k_link(Params p, int k)
 {
     if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;     // converged: dynwave.c:249-251
     if (p.nShared && blockIdx.x == 0 && threadIdx.x == 0) p.xsend[p.xflag] = 0.0;   // k_node sets it
-    __shared__ double ct[5 * SWX_CIRC_N];
+    __shared__ double ct[kFast ? kCtFast : 5 * SWX_CIRC_N];
     double dt = p.ctl->dt;
     int work = 0;
     if (kFirst && blockIdx.x == 0 && threadIdx.x < kMaxTrialsCap) p.ctl->ucount[threadIdx.x] = 0;
     if (kFirst || k < 2) {
-        stageTables(ct, p.gTables);
+        stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
         for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nL; j += gridDim.x * kBlock) {
             uint32_t f = p.lflags[j];
             if (f & LF_COLD) continue;
@@ -713,7 +737,7 @@ void k_link(Params p, int k)
         const int* list = p.ulist + (size_t)((k - 1) & 1) * p.nN;
         const int slots = 4 * cnt;
         if (blockIdx.x * kBlock < slots) {                  // uniform per block
-            stageTables(ct, p.gTables);
+            stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
             for (int t = blockIdx.x * kBlock + threadIdx.x; t < slots; t += gridDim.x * kBlock) {
                 int u = list[t >> 2];
                 int e1 = p.rowptr[u + 1];
@@ -1499,7 +1523,7 @@ __device__ __forceinline__ double conduitVelocity(const Params& p, int j, uint32
     if (depth <= 0.01) return 0.0;
     double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
     q /= barrels;
-    Geom x = loadGeom<kFast>(p, j, f);
+    Geom x = loadGeom<kFast>(p, j, f, ct);
     double area = getAofY<kAll>(x, depth, ct);
     return (area > 0.0001) ? q / area : 0.0;
 }
@@ -1513,8 +1537,8 @@ template <bool kFast, bool kAll>
 __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
 {
     __shared__ double red[kNumPartials][kBlock / 64];
-    __shared__ double ct[5 * SWX_CIRC_N];
-    stageTables(ct, p.gTables);
+    __shared__ double ct[kFast ? kCtFast : 5 * SWX_CIRC_N];
+    stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
     double acc[kNumPartials];
     for (int q = 0; q < kNumPartials; q++) acc[q] = 0.0;
     acc[5] = p.routeStep; acc[8] = 1.0e300;
@@ -1760,8 +1784,17 @@ template <int kPhase>
 __global__ void k_finalize(Params p)
 {
     __shared__ double sum[kNumPartials][kBlock];
+    // the step-control block is staged through LDS: one coalesced load and
+    // store instead of a chain of dependent single-lane HBM round trips
+    __shared__ unsigned long long cw[sizeof(StepCtl) / 8];
+    static_assert(sizeof(StepCtl) % 8 == 0, "StepCtl staged as 8-byte words");
+    constexpr int nw = (int)(sizeof(StepCtl) / 8);
     int t = threadIdx.x;
-    StepCtl* c = p.ctl;
+    {
+        const unsigned long long* g = (const unsigned long long*)p.ctl;
+        for (int w = t; w < nw; w += kBlock) cw[w] = g[w];
+    }
+    StepCtl* c = (StepCtl*)cw;
     if (kPhase != 2) {
         double acc[kNumPartials];
         for (int q = 0; q < kNumPartials; q++) acc[q] = partialIsMin(q) || q == 8 || q == 9 ? 1.0e300 : 0.0;
@@ -1784,7 +1817,8 @@ __global__ void k_finalize(Params p)
         if (t == 0)
             for (int q = 0; q < kNumPartials; q++) c->stepRed[q] = sum[q][0];
     }
-    if (t != 0 || kPhase == 1) return;
+    __syncthreads();
+    if (t == 0 && kPhase != 1) {
     double tot[kNumPartials];
     for (int q = 0; q < kNumPartials; q++) tot[q] = c->stepRed[q];
     // Picard step count / convergence (dynwave.c:242-257)
@@ -1859,6 +1893,10 @@ __global__ void k_finalize(Params p)
     // without a copy command in the step (totalSteps = index of that step)
     p.hostDt[c->totalSteps % kDtRing] = dtn;
     __threadfence_system();
+    }
+    __syncthreads();
+    unsigned long long* g = (unsigned long long*)p.ctl;
+    for (int w = t; w < nw; w += kBlock) g[w] = cw[w];
 }
 
 // Results of one reporting period (node_getResults node.c:497-528,
@@ -1870,8 +1908,8 @@ template <bool kFast>
 __global__ __launch_bounds__(kBlock) void k_pack_results(Params p, double f, double uL, double uV,
                                                          double uQ, float* outN, float* outL)
 {
-    __shared__ double ct[5 * SWX_CIRC_N];
-    stageTables(ct, p.gTables);
+    __shared__ double ct[kFast ? kCtFast : 5 * SWX_CIRC_N];
+    stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
     const double f1 = 1.0 - f;
     const int nv = 6 + p.P, lv = 5 + p.P;
     int n = gridDim.x * kBlock;
@@ -1898,7 +1936,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_results(Params p, double f, dou
     for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nL; j += n) {
         float* x = outL + (size_t)j * lv;
         uint32_t fl = p.lflags[j];
-        Geom g = (fl & LF_COLD) ? loadGeom<false>(p, j, fl) : loadGeom<kFast>(p, j, fl);
+        Geom g = (fl & LF_COLD) ? loadGeom<false>(p, j, fl) : loadGeom<kFast>(p, j, fl, ct);
         double y = f1 * p.lOldDepth[j] + f * p.lNewDepth[j];
         double q = f1 * p.lOldFlow[j] + f * p.lNewFlow[j];
         double v = f1 * p.lOldVolume[j] + f * p.lNewVolume[j];
@@ -2195,7 +2233,11 @@ int Router::init(Project& prj, int device, const Partition* partIn)
 
     Params& p = d->p;
     p.nN = nN; p.nL = nL; p.P = P;
-    p.maxTrials = std::min(prj.opt.maxTrials, kMaxTrialsCap);
+    if (prj.opt.maxTrials > kMaxTrialsCap) {        // one flag per iteration in StepCtl
+        fail("MAX_TRIALS above " + std::to_string(kMaxTrialsCap) + " is not supported");
+        return err_;
+    }
+    p.maxTrials = prj.opt.maxTrials;
     p.surchargeMethod = prj.opt.surchargeMethod;
     p.forceMainEqn = prj.opt.forceMainEqn;
     p.inertDamping = prj.opt.inertDamping;
@@ -2268,6 +2310,36 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         xd[0][j] = x.yFull; xd[1][j] = x.wMax; xd[2][j] = x.ywMax; xd[3][j] = x.aFull;
         xd[4][j] = x.rFull; xd[5][j] = x.sFull; xd[6][j] = x.sMax; xd[7][j] = x.yBot;
         xd[8][j] = x.aBot; xd[9][j] = x.sBot; xd[10][j] = x.rBot;
+    }
+    // kFast: every streaming conduit circular, no SLOT surcharge, and at most
+    // kGeomMax distinct sections; the sections become one LDS table and each
+    // streaming conduit's flags carry its section id
+    std::vector<double> geomTab;
+    {
+        bool fast = prj.opt.surchargeMethod != SUR_SLOT;
+        const char* gl = getenv("SWMM5_GENERIC_LINKS");
+        if (gl && atoi(gl)) fast = false;
+        std::map<std::array<double, kGeomVals>, int> ids;
+        std::vector<int> gid(nL, 0);
+        for (int j = 0; j < nL && fast; j++) {
+            if (lflags[j] & LF_COLD) continue;
+            if ((lflags[j] & LF_XTYPE) != G_CIRCULAR) { fast = false; break; }
+            std::array<double, kGeomVals> key = {xd[0][j], xd[1][j], xd[3][j], xd[4][j], xd[5][j], xd[6][j], xd[2][j]};
+            auto it = ids.find(key);
+            if (it == ids.end()) {
+                if ((int)ids.size() == kGeomMax) { fast = false; break; }
+                it = ids.emplace(key, (int)ids.size()).first;
+                geomTab.insert(geomTab.end(), key.begin(), key.end());
+            }
+            gid[j] = it->second;
+        }
+        d->fastLinks = fast;
+        p.nGeom = fast ? (int)ids.size() : 0;
+        if (fast)
+            for (int j = 0; j < nL; j++)
+                if (!(lflags[j] & LF_COLD))
+                    lflags[j] = (int)((uint32_t)lflags[j] | ((uint32_t)gid[j] << LF_GEOM_SHIFT));
+        if (!fast) geomTab.clear();
     }
     {
         int* ptr = upI(nodes2, nodes2.size());
@@ -2601,6 +2673,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     // ---- tables, partials, control ---------------------------------------
     {
         std::vector<double> t(&SWX_CIRC_TABLES[0][0], &SWX_CIRC_TABLES[0][0] + 5 * SWX_CIRC_N);
+        t.insert(t.end(), geomTab.begin(), geomTab.end());
         UPD(tmp, t, t.size()); p.gTables = tmp;
         std::vector<double> st(SWX_SHAPE_TAB, SWX_SHAPE_TAB + SWX_SHAPE_TAB_LEN);
         UPD(tmp, st, st.size()); p.gShapeTab = tmp;
@@ -2619,13 +2692,6 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     for (int j = 0; j < nL; j++)
         if (!isBasicShape((int)(lflags[j] & LF_XTYPE))) d->allShapes = true;
     d->general = prj.net.nStorage > 0 || d->allShapes;
-    {
-        bool fast = prj.opt.surchargeMethod != SUR_SLOT;
-        for (int j = 0; j < nL && fast; j++)
-            if (!(lflags[j] & LF_COLD) && (lflags[j] & LF_XTYPE) != G_CIRCULAR) fast = false;
-        const char* g = getenv("SWMM5_GENERIC_LINKS");
-        d->fastLinks = fast && !(g && atoi(g));
-    }
     int maxBlocks = 8 * std::max(prop.multiProcessorCount, 1);
     // streaming kernels: one resident wave of workgroups (grid-stride loops),
     // so early-exited Picard iterations dispatch few workgroups
@@ -2788,10 +2854,16 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         //   iterations >= 1: reads oldFlow setting q1 a2 4x8 + lstate 4 = 36
         //   a bypassed conduit costs flags 4 + nodes 8 + 2 conv flags 8 = 20,
         //   a cold conduit skipped by the streaming kernel costs its flags 4
+        //   (kFast: the geometry comes from the LDS section table: static 60;
+        //   evap and seep are written only by conduits with losses, LF_SEEP)
         d->nHot = L - p.nCold;
         d->nColdD = p.nCold;
-        d->kbytes[0] = d->nHot * (116 + 16 + 92 + 84) + d->nColdD * 4;
-        d->kbytes[4] = 116 + 16 + 92 + 36;
+        double nSeepHot = 0;
+        for (int j = 0; j < nL; j++)
+            if (!(lflags[j] & LF_COLD) && (lflags[j] & LF_SEEP)) nSeepHot += 1;
+        const double stat = d->fastLinks ? 60 : 116;
+        d->kbytes[0] = d->nHot * (stat + 16 + 76 + 84) + nSeepHot * 16 + d->nColdD * 4;
+        d->kbytes[4] = stat + 16 + 76 + 36 + (d->nHot > 0 ? 16.0 * nSeepHot / d->nHot : 0.0);
         // node update: per node static (flags, fullDepth, surDepth, yCrown,
         //   fullVolume, ponded: 4+5x8) + rowptr 4 + dynamic reads (newDepth,
         //   oldDepth, oldNetInflow, newLat, oldSurfArea: 40) + writes (inflow,
