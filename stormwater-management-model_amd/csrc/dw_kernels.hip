@@ -88,7 +88,7 @@ enum : uint32_t {
 // are one table staged into LDS behind the circular tables; a conduit carries
 // its section's id in LF_GEOM_SHIFT instead of loading 7 geometry doubles
 constexpr int kGeomMax = 128;
-constexpr int kGeomVals = 7;      // yFull wMax aFull rFull sFull sMax ywMax
+constexpr int kGeomVals = 9;      // yFull wMax aFull rFull sFull sMax ywMax, 1/yFull (divdd.h pair)
 constexpr int kCtFast = 5 * SWX_CIRC_N + kGeomVals * kGeomMax;
 // ---- packed per-node flags -------------------------------------------------
 enum : uint32_t {
@@ -268,6 +268,7 @@ __device__ __forceinline__ Geom loadGeom(const Params& p, int j, uint32_t f, con
         g.type = G_CIRCULAR;
         g.yFull = t[0]; g.wMax = t[1]; g.aFull = t[2]; g.rFull = t[3];
         g.sFull = t[4]; g.sMax = t[5]; g.ywMax = t[6];
+        g.rYh = t[7]; g.rYl = t[8];
         g.yBot = g.aBot = g.sBot = g.rBot = 0.0;
         return g;
     }
@@ -312,7 +313,7 @@ __device__ __forceinline__ double widthAt(const Params& p, const Geom& x, double
 {
     double wSlot = slotWidth<kFast>(p, x, y);
     if (wSlot > 0.0) return wSlot;
-    if (y / x.yFull >= p.crownCutoff && !isOpen(x.type)) y = p.crownCutoff * x.yFull;
+    if (normDepth(x, y) >= p.crownCutoff && !isOpen(x.type)) y = p.crownCutoff * x.yFull;
     return getWofY<kAll>(x, y, ct);
 }
 // dwflow.c:609-619, 623-633
@@ -454,7 +455,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         oldFlow = p.lOldFlow[j];
     }
     bool isClosed = (p.setting[j] == 0);
-    double qOld = oldFlow / barrels;
+    double qOld = (barrels == 1.0) ? oldFlow : oldFlow / barrels;   // x / 1 == x
     double qLast = p.q1[j];
     double evapRate = 0.0, seepRate = 0.0;
 
@@ -617,7 +618,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         (void)oldDepth;
         dq6 = conduitLossRate<kCold>(p, j, x, dt, &evapRate, &seepRate, ct) * 2.5 * dt * v / len0;
     } else {
-        dq6 = 0.0 * 2.5 * dt * v / len0;
+        dq6 = copysign(0.0, v);       // == 0.0 * 2.5 * dt * v / len0 (dt, len0 > 0)
     }
 
     double denom = 1.0 + dq1 + dq5;
@@ -2319,17 +2320,21 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         bool fast = prj.opt.surchargeMethod != SUR_SLOT;
         const char* gl = getenv("SWMM5_GENERIC_LINKS");
         if (gl && atoi(gl)) fast = false;
-        std::map<std::array<double, kGeomVals>, int> ids;
+        std::map<std::array<double, 7>, int> ids;
         std::vector<int> gid(nL, 0);
         for (int j = 0; j < nL && fast; j++) {
             if (lflags[j] & LF_COLD) continue;
             if ((lflags[j] & LF_XTYPE) != G_CIRCULAR) { fast = false; break; }
-            std::array<double, kGeomVals> key = {xd[0][j], xd[1][j], xd[3][j], xd[4][j], xd[5][j], xd[6][j], xd[2][j]};
+            std::array<double, 7> key = {xd[0][j], xd[1][j], xd[3][j], xd[4][j], xd[5][j], xd[6][j], xd[2][j]};
             auto it = ids.find(key);
             if (it == ids.end()) {
                 if ((int)ids.size() == kGeomMax) { fast = false; break; }
                 it = ids.emplace(key, (int)ids.size()).first;
                 geomTab.insert(geomTab.end(), key.begin(), key.end());
+                double rh, rl;
+                recipDD(key[0], &rh, &rl);
+                geomTab.push_back(rh);
+                geomTab.push_back(rl);
             }
             gid[j] = it->second;
         }

@@ -15,6 +15,7 @@
 #include <math.h>
 #include "xsect_tables.h"
 #include "shape_tables.h"
+#include "divdd.h"
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -35,7 +36,16 @@ struct Geom {                 // TXsect (objects.h:581-599), packed per link
     // tabulated shapes: the shape's table block (SWX_SHAPE_TAB, or a
     // transect's own tables); unused by the closed-form shapes
     const double* tb = nullptr;
+    // reciprocal pair of yFull (divdd.h) when the kernels' section table
+    // supplies one; 0: y / yFull is a plain division
+    double rYh = 0.0, rYl = 0.0;
 };
+// y / yFull, the normalised depth of every geometry relation
+SWX_HD double normDepth(const Geom& x, double y)
+{
+    if (x.rYh != 0.0) return divDD(y, x.yFull, x.rYh, x.rYl);
+    return y / x.yFull;
+}
 
 // xsection types in the reference's enum order (enums.h)
 enum GeomType {
@@ -77,6 +87,26 @@ SWX_HD int isOpen(int t) { return amaxRatio(t) >= 1.0 ? 1 : 0; }     // xsect.c:
 // xsect.c:1474-1507 -- uniform table lookup, quadratic near the origin
 SWX_HD double lookup(double x, const double* t, int n)
 {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the circular tables (n = 51): the two divisions by the step are
+    // divisions by a known constant (divdd.h), bit-identical
+    if (n == SWX_CIRC_N) {
+        const double delta = kCircDelta;
+        int i = (int)divDD(x, delta, kCircDeltaRh, kCircDeltaRl);
+        if (i >= n - 1) return t[n - 1];
+        double x0 = i * delta;
+        double x1 = ((double)i + 1) * delta;
+        double y = t[i] + divDD((x - x0) * (t[i + 1] - t[i]), delta, kCircDeltaRh, kCircDeltaRl);
+        if (i < 2) {
+            double y2 = y + divDD((x - x0) * (x - x1), kCircDelta2, kCircDelta2Rh, kCircDelta2Rl) *
+                            (t[i] / 2.0 - t[i + 1] + t[i + 2] / 2.0);
+            if (y2 > 0.0) y = y2;
+        }
+        if (y < 0.0) y = 0.0;
+        return y;
+    }
+#endif
+
     double delta = 1.0 / ((double)n - 1);
     int i = (int)(x / delta);
     if (i >= n - 1) return t[n - 1];
@@ -490,7 +520,7 @@ SWX_HD double exYofA(const Geom& x, double a, const double* ct)
 template <bool kAll = true>
 SWX_HD double getAofY(const Geom& x, double y, const double* ct)
 {
-    double yNorm = y / x.yFull;
+    double yNorm = normDepth(x, y);
     if (y <= 0.0) return 0.0;
     switch (x.type) {
     case G_CIRCULAR: case G_FORCE_MAIN: return x.aFull * lookup(yNorm, SWX_TA(ct), SWX_CIRC_N);
@@ -508,7 +538,7 @@ SWX_HD double getAofY(const Geom& x, double y, const double* ct)
 template <bool kAll = true>
 SWX_HD double getWofY(const Geom& x, double y, const double* ct)
 {
-    double yNorm = y / x.yFull;
+    double yNorm = normDepth(x, y);
     switch (x.type) {
     case G_CIRCULAR: case G_FORCE_MAIN: return x.wMax * lookup(yNorm, SWX_TW(ct), SWX_CIRC_N);
     case G_RECT_CLOSED: if (yNorm == 1.0) return 0.0; return x.wMax;
@@ -585,7 +615,7 @@ SWX_HD double getRofA(const Geom& x, double a, const double* ct)
 template <bool kAll = true>
 SWX_HD double getRofY(const Geom& x, double y, const double* ct)
 {
-    double yNorm = y / x.yFull;
+    double yNorm = normDepth(x, y);
     switch (x.type) {
     case G_CIRCULAR: case G_FORCE_MAIN: return x.rFull * lookup(yNorm, SWX_TR(ct), SWX_CIRC_N);
     case G_TRAPEZOIDAL:
