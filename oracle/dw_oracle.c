@@ -61,6 +61,7 @@ struct orc_net
     double routeStep, courantFactor, minRouteStep, minSurfArea, headTol, crownCutoff, evapRate,
            variableStep, omega;
     int maxTrials, surchargeMethod, inertDamping, normalFlowLtd, allowPonding, steps;
+    int threads;          /* OpenMP threads for the per-link / per-node loops (bench cpu_baseline) */
     long nonConverge;
     /* node static */
     int *nType, *degree, *outfallType, *outfallFlap;
@@ -194,6 +195,7 @@ int orc_set_opt(orc_net* n, const char* k, double v)
     else if (!strcmp(k, "inertDamping"))    n->inertDamping = (int)v;
     else if (!strcmp(k, "normalFlowLtd"))   n->normalFlowLtd = (int)v;
     else if (!strcmp(k, "allowPonding"))    n->allowPonding = (int)v;
+    else if (!strcmp(k, "threads"))         n->threads = (int)v;
     else return -1;
     return 0;
 }
@@ -1344,6 +1346,12 @@ static int dynwaveExecute(orc_net* n, double dt)
     double yOld;
     n->steps = 0;
     n->omega = O_OMEGA;
+    /* The per-link loops (conduitFlow writes only link j) and per-node loops
+       (setNodeDepth writes only node i) may run on several OpenMP threads, as
+       the reference's own findLinkFlows does (dynwave.c:387-395); the node sums
+       (updateNodeFlows) stay in serial link order, so the result is the same
+       bits for any thread count. */
+    const int nt = n->threads > 1 ? n->threads : 1;
     /* initRoutingStep */
     for (i = 0; i < nN; i++) { n->converged[i] = 0; n->dYdT[i] = 0.0; }
     for (i = 0; i < nL; i++) { n->bypassed[i] = 0; n->surfArea1[i] = 0.0; n->surfArea2[i] = 0.0; }
@@ -1366,11 +1374,13 @@ static int dynwaveExecute(orc_net* n, double dt)
             n->sumdqdh[i] = 0.0;
         }
         /* findLinkFlows */
+        #pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static)
         for (i = 0; i < nL; i++)
             if (!n->bypassed[i]) conduitFlow(n, i, n->steps, n->omega, dt);
         for (i = 0; i < nL; i++) updateNodeFlows(n, i);
         /* findNodeDepths */
         for (i = 0; i < nL; i++) setOutfallDepth(n, i);
+        #pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static) private(yOld)
         for (i = 0; i < nN; i++)
         {
             if (n->nType[i] == N_OUTFALL) continue;
@@ -1389,6 +1399,7 @@ static int dynwaveExecute(orc_net* n, double dt)
         if (n->steps > 1)
         {
             if (converged) break;
+            #pragma omp parallel for num_threads(nt) if (nt > 1) schedule(static)
             for (i = 0; i < nL; i++)
                 n->bypassed[i] = (n->converged[n->node1[i]] && n->converged[n->node2[i]]) ? 1 : 0;
         }

@@ -194,6 +194,14 @@ struct Params {
     // flooded, no volume) has an unchanged unrelaxed depth yRaw = yOld + dV /
     // surfArea, so its next update is just the relaxation 0.5 yLast + 0.5 yRaw
     double *yRaw, *yMaxNP;        // yMaxNP = fullDepth + surDepth (non-ponding yMax)
+    // frozen junctions: a clean plain junction that has converged and whose
+    // relaxation stays inside [0, min(yCrown, yMax)] keeps converging, and its
+    // later updates are the bare relaxation y <- 0.5 y + 0.5 yRaw; it is not
+    // visited again until an incident conduit is updated, and its depth is
+    // advanced on demand (frozenDepth).  frz: 0 = live; f > 0: frozen, the
+    // stored depth is that of iteration f - 1
+    unsigned char* frz;
+    int freeze;                   // freezing enabled (headTol > 0)
     // storage units (node.c:170-179), per node (stShape -1: not a storage unit)
     const int* stShape;
     const double *stA0, *stA1, *stA2, *stFEvap;
@@ -367,6 +375,20 @@ __device__ double conduitLossRate(const Params& p, int j, const Geom& x, double 
     return totalLossRate;
 }
 
+// depth of node i at Picard iteration m: a frozen junction (Params::frz)
+// advances by the relaxation of setNodeDepth's plain branch (dynwave.c:
+// 700-715, omega = 0.5, yNew = yOld + dV / surfArea = yRaw unchanged), the
+// same operations the live update would have made
+__device__ __forceinline__ double frozenDepth(const Params& p, int i, int fz, int m)
+{
+    double y = p.nNewDepth[i];
+    if (fz) {
+        const double yr = p.yRaw[i];
+        for (int j = fz - 1; j < m; j++) y = (1.0 - 0.5) * y + 0.5 * yr;
+    }
+    return y;
+}
+
 // dwflow.c:297-413.  kCold = false is the specialisation for links with both
 // offsets zero (LF_COLD clear): z1 = z2 = 0 (at an outfall end too, since
 // max(0, 0 - depth) = 0), so the branches that need normal / critical depth
@@ -374,7 +396,7 @@ __device__ double conduitLossRate(const Params& p, int j, const Geom& x, double 
 // kernel.
 template <bool kCold>
 __device__ __forceinline__ int flowClassOf(const Params& p, int j, const Geom& x, uint32_t f,
-                                           int n1, int n2, double q, double h1, double h2,
+                                           double yn1, double yn2, double q, double h1, double h2,
                                            double y1, double y2, double* yC, double* yN,
                                            double* fasnh, const double* ct)
 {
@@ -382,8 +404,8 @@ __device__ __forceinline__ int flowClassOf(const Params& p, int j, const Geom& x
     if (kCold) {
         z1 = p.off1[j];
         z2 = p.off2[j];
-        if (f & LF_N1_OUTFALL) z1 = gmax(0.0, (z1 - p.nNewDepth[n1]));
-        if (f & LF_N2_OUTFALL) z2 = gmax(0.0, (z2 - p.nNewDepth[n2]));
+        if (f & LF_N1_OUTFALL) z1 = gmax(0.0, (z1 - yn1));
+        if (f & LF_N2_OUTFALL) z2 = gmax(0.0, (z2 - yn2));
     }
     int fc = F_SUBCRIT;
     *fasnh = 1.0;
@@ -431,10 +453,10 @@ __device__ __forceinline__ int flowClassOf(const Params& p, int j, const Geom& x
 // dwflow.c:57-293 -- one conduit, one Picard iteration.
 template <bool kFirst, bool kCold, bool kFast = false>
 __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, int2 nn, int steps,
-                                            double dt, const double* ct)
+                                            double dt, const double* ct, double yn1, double yn2)
 {
     const double omega = 0.5;
-    int n1 = nn.x, n2 = nn.y;
+    (void)nn;                     // end-node depths arrive as yn1 / yn2
     const double off1 = kCold ? p.off1[j] : 0.0;     // hot links: both offsets are 0
     const double off2 = kCold ? p.off2[j] : 0.0;
     Geom x = loadGeom<kFast>(p, j, f, ct);
@@ -462,8 +484,8 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     double inv1 = p.inv1[j], inv2 = p.inv2[j];
     double z1 = inv1 + off1;
     double z2 = inv2 + off2;
-    double h1 = p.nNewDepth[n1] + inv1;
-    double h2 = p.nNewDepth[n2] + inv2;
+    double h1 = yn1 + inv1;
+    double h2 = yn2 + inv2;
     h1 = gmax(h1, z1);
     h2 = gmax(h2, z2);
     double y1 = h1 - z1;
@@ -486,7 +508,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         double yNorm = (d1 + d2) / 2.0;
         double yCrit = yNorm;
         if (d1 >= x.yFull && d2 >= x.yFull) fc = F_SUBCRIT;
-        else fc = flowClassOf<kCold>(p, j, x, f, n1, n2, qLast, h1, h2, y1, y2, &yCrit, &yNorm, &fasnh, ct);
+        else fc = flowClassOf<kCold>(p, j, x, f, yn1, yn2, qLast, h1, h2, y1, y2, &yCrit, &yNorm, &fasnh, ct);
         // Every wet class evaluates the top width at (d1, d2, dMid) after
         // adjusting one end; the widths are computed once, outside the switch,
         // so the geometry code is instantiated three times instead of fifteen.
@@ -676,8 +698,8 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         }
         if (closed) q = 0.0;
     }
-    if (q > 0.0001 && p.nNewDepth[n1] <= 0.0001) q = 0.0001;
-    if (q < -0.0001 && p.nNewDepth[n2] <= 0.0001) q = -0.0001;
+    if (q > 0.0001 && yn1 <= 0.0001) q = 0.0001;
+    if (q < -0.0001 && yn2 <= 0.0001) q = -0.0001;
 
     p.a1[j] = aMid;
     p.q1[j] = q;
@@ -714,7 +736,21 @@ template <bool kFirst, int kWaves, bool kFast>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves)))
 void k_link(Params p, int k)
 {
-    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;     // converged: dynwave.c:249-251
+    if (k >= 2 && p.ctl->unconv[k - 1] == 0) {            // converged: dynwave.c:249-251
+        // the first launch after the step converged (iteration k-1 ran): the
+        // frozen junctions take their depth at that last iteration (a step
+        // that runs all MaxTrials iterations does this in its last k_node)
+        if (p.freeze && (k == 2 || p.ctl->unconv[k - 2] != 0)) {
+            for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
+                const int fz = p.frz[i];
+                if (fz) {
+                    p.nNewDepth[i] = frozenDepth(p, i, fz, k - 1);
+                    p.frz[i] = 0;
+                }
+            }
+        }
+        return;
+    }
     if (p.nShared && blockIdx.x == 0 && threadIdx.x == 0) p.xsend[p.xflag] = 0.0;   // k_node sets it
     __shared__ double ct[kFast ? kCtFast : 5 * SWX_CIRC_N];
     double dt = p.ctl->dt;
@@ -725,7 +761,8 @@ void k_link(Params p, int k)
         for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nL; j += gridDim.x * kBlock) {
             uint32_t f = p.lflags[j];
             if (f & LF_COLD) continue;
-            conduitFlow<kFirst, false, kFast>(p, j, f, p.lnodes[j], k, dt, ct);
+            int2 nn = p.lnodes[j];
+            conduitFlow<kFirst, false, kFast>(p, j, f, nn, k, dt, ct, p.nNewDepth[nn.x], p.nNewDepth[nn.y]);
         }
     } else {
         // Later iterations: a conduit is updated unless both end nodes have
@@ -749,7 +786,9 @@ void k_link(Params p, int k)
                     int2 nn = p.lnodes[l];
                     int v = (nn.x == u) ? nn.y : nn.x;
                     if (!p.conv[v] && v < u) continue;        // listed too: v takes it
-                    conduitFlow<kFirst, false, kFast>(p, l, f, nn, k, dt, ct);
+                    double y1 = frozenDepth(p, nn.x, p.frz[nn.x], k - 1);
+                    double y2 = frozenDepth(p, nn.y, p.frz[nn.y], k - 1);
+                    conduitFlow<kFirst, false, kFast>(p, l, f, nn, k, dt, ct, y1, y2);
                     p.dirty[nn.x] = 1;
                     p.dirty[nn.y] = 1;
                     work++;
@@ -856,7 +895,9 @@ __global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
         uint32_t f = p.lflags[j];
         int2 nn = p.lnodes[j];
         if (k >= 2 && p.conv[nn.x] && p.conv[nn.y]) continue;
-        conduitFlow<kFirst, true>(p, j, f, nn, k, dt, ct);
+        double y1 = frozenDepth(p, nn.x, (k >= 2) ? p.frz[nn.x] : 0, k - 1);
+        double y2 = frozenDepth(p, nn.y, (k >= 2) ? p.frz[nn.y] : 0, k - 1);
+        conduitFlow<kFirst, true>(p, j, f, nn, k, dt, ct, y1, y2);
         if (k >= 2) { p.dirty[nn.x] = 1; p.dirty[nn.y] = 1; }
     }
 }
@@ -892,6 +933,18 @@ __device__ __attribute__((noinline)) double devStorageLosses(const Params& p, in
                                                             double volume, double dt, double* evapVol)
 {
     return storageLosses(devStorageGeom(p, i), p.stFEvap[i], p.evapRate, depth, volume, dt, evapVol);
+}
+
+// A converged plain junction (not surcharged, ponded or flooded, no storage
+// volume) whose sums stay unchanged relaxes toward yRaw with a step that
+// halves every iteration, so it stays converged; it stays on the plain branch
+// when its depth and yRaw both lie in [0, yCrown (EXTRAN)] and [0, yMax]
+// (relaxed values lie between them).  Such a junction may be frozen.
+__device__ __forceinline__ bool freezable(const Params& p, double yNew, double yRaw, double yMax, double yCrown)
+{
+    if (!(yRaw >= 0.0) || yNew > yMax || yRaw > yMax) return false;
+    if (p.surchargeMethod == SUR_EXTRAN && yCrown > 0.0 && (yNew > yCrown || yRaw > yCrown)) return false;
+    return true;
 }
 
 // setNodeDepth (dynwave.c:636-762) for node i given its summed inflow,
@@ -944,8 +997,8 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
     if (!canPond) yMax += p.surDepth[i];
     double fullVolume = p.fullVolume[i];
     const bool flooded = yNew > yMax;
+    const bool plain = !isSurcharged && !canPond && !flooded && fullVolume == 0.0 && !isStorage;
     if (k >= 1) {                                      // fast-path cache for the next iteration
-        bool plain = !isSurcharged && !canPond && !flooded && fullVolume == 0.0 && !isStorage;
         if (plain) p.yRaw[i] = yRaw;
         p.dirty[i] = plain ? 2 : 0;
     }
@@ -971,6 +1024,9 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
     p.nNewDepth[i] = yNew;        // Xnode.dYdT = |yNew - yOld| / dt: formed at the step end
     int c = (fabs(yLast - yNew) > p.headTol) ? 0 : 1;  // dynwave.c:615-621
     p.conv[i] = c;
+    if (k >= 1 && k + 1 < p.maxTrials && p.freeze && plain && c && !(nf & (NF_SHARED | NF_DEFER | NF_REPLICA)) &&
+        freezable(p, yNew, yRaw, yMax, yCrown))
+        p.frz[i] = (unsigned char)(k + 1);
     return c;
 }
 
@@ -1024,16 +1080,33 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         uint32_t nf = p.nflags[i];
         int type = (int)(nf & NF_TYPE);
         // an outfall's depth is written by the prologue above: not read here
-        double yLast = (type == OUTFALL) ? 0.0 : p.nNewDepth[i];
+        double yLast = 0.0;
+        bool haveYLast = false;
         bool listMe = (type == OUTFALL);       // unconverged after this iteration
         bool done = false;
         if (!kFirst && k >= 2) {
-            // all fast-path operands issued at once (one memory round trip)
             unsigned char cache = p.dirty[i];
-            double yLast2 = p.nNewDepth[i], yCrown = p.yCrown[i], yRaw = p.yRaw[i], yMax = p.yMaxNP[i];
-            if (type != OUTFALL && !(nf & (NF_SHARED | NF_DEFER)) && cache == 2) {
+            const int fz = p.frz[i];
+            if (fz) {
+                // frozen junction: nothing to do while its conduits are
+                // bypassed (it stays converged; none of its operands is
+                // read); once one is updated it is live again from its
+                // depth at the last iteration
+                if (cache & 1) {
+                    yLast = frozenDepth(p, i, fz, k - 1);
+                    haveYLast = true;
+                    p.frz[i] = 0;
+                } else {
+                    if (k == p.maxTrials - 1) {            // the last possible iteration
+                        p.nNewDepth[i] = frozenDepth(p, i, fz, k);
+                        p.frz[i] = 0;
+                    }
+                    done = true;
+                }
+            } else if (type != OUTFALL && !(nf & (NF_SHARED | NF_DEFER)) && cache == 2) {
                 // plain clean junction: the relaxation step of setNodeDepth
                 // (dynwave.c:700-715) on the cached unrelaxed depth
+                double yLast2 = p.nNewDepth[i], yCrown = p.yCrown[i], yRaw = p.yRaw[i], yMax = p.yMaxNP[i];
                 bool sur = p.surchargeMethod == SUR_EXTRAN && yCrown > 0.0 && yLast2 > yCrown;
                 if (!sur) {
                     const double omega = 0.5;
@@ -1044,12 +1117,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                         int c = (fabs(yLast2 - yNew) > p.headTol) ? 0 : 1;
                         p.conv[i] = c;
                         if (!c) { anyUnconv = true; listMe = true; }
+                        else if (p.freeze && k + 1 < p.maxTrials && freezable(p, yNew, yRaw, yMax, yCrown))
+                            p.frz[i] = (unsigned char)(k + 1);
                         done = true;
                     }
                 }
             }
         }
         if (!done) {
+        if (!haveYLast) yLast = (type == OUTFALL) ? 0.0 : p.nNewDepth[i];
         double yOld, lat;
         if (kFirst) {
             // routing.c:328-332, node.c:293-304, 325-341 -- step-begin rotation
@@ -1420,6 +1496,7 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
 {
     const double dt = p.ctl->dt;
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
+        const double depth = p.nNewDepth[i];
         double qIn = p.inflow[i];
         double oldVol = p.nOldVolume[i];
         int e0 = p.qrowptr[i], e1 = p.qrowptr[i + 1];
@@ -1450,11 +1527,11 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
             if (isStorage || oldVol > 0.0353147) {
                 double c1 = reactedQual(p.kDecay[pp], cOld * fEvap, dt);
                 c = mixedQual(c1, oldVol, w, qIn, dt);
-                if ((p.nNewVolume[i] <= 0.0353147 || p.nNewDepth[i] <= 0.003281) && qIn <= 1.E-10) c = 0.0;
+                if ((p.nNewVolume[i] <= 0.0353147 || depth <= 0.003281) && qIn <= 1.E-10) c = 0.0;
             } else if (qIn > 1.E-10) {
                 c = w / qIn;
             } else {
-                c = (p.nNewDepth[i] > 0.003281) ? cOld : 0.0;
+                c = (depth > 0.003281) ? cOld : 0.0;
             }
             p.nNewQual[ni] = c;
         }
@@ -1553,9 +1630,10 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
     const bool stats = !(aDate < c->statsStart);
     // convergence of this step (dynwave.c:242-257): nodes count non-convergence
     bool converged;
+    int steps = p.maxTrials < 1 ? 0 : 1;
     if (p.maxTrials <= 1) converged = false;
     else {
-        int steps = 2;
+        steps = 2;
         while (steps < p.maxTrials && c->unconv[steps - 1]) steps++;
         converged = (c->unconv[steps - 1] == 0);
     }
@@ -2640,6 +2718,15 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         p.dirty = devAlloc<unsigned char>(d, nN, &e);
         if (e == hipSuccess) e = hipMemset(p.dirty, 0, std::max<size_t>(nN, 1));
         if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+        p.frz = devAlloc<unsigned char>(d, nN, &e);
+        if (e == hipSuccess) e = hipMemset(p.frz, 0, std::max<size_t>(nN, 1));
+        if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+        // a frozen junction's later updates are pure relaxation steps whose
+        // change halves each iteration (freezable); a tolerance below a few
+        // ulps of a depth would not absorb their rounding.  SWMM5_NO_FREEZE
+        // disables it (comparison runs)
+        const char* nf = getenv("SWMM5_NO_FREEZE");
+        p.freeze = (prj.opt.headTol > 1e-12 && p.maxTrials > 2 && !(nf && atoi(nf))) ? 1 : 0;
     }
     UPD(p.dYdT, gn(st.dYdT), nN);
     UPI(p.conv, gni(st.converged), nN);

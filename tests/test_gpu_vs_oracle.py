@@ -200,6 +200,37 @@ def test_surcharge_regime_window_60x60(tmp_path):
 
 
 @pytest.mark.gpu
+def test_frozen_junctions_bitwise(tmp_path, monkeypatch):
+    """Frozen junctions (converged plain junctions whose conduits are all
+    bypassed are not visited; their depth is advanced by the same relaxation
+    steps when it is next read) change no bit of the result: the 60 x 60
+    surcharged variable-step run with and without freezing, every node and
+    link field and every counter compared bitwise over 300 steps."""
+    q, D = 0.3, 1.0
+    inp = str(tmp_path / "g.inp")
+    netgen.write_grid(inp, 60, 60, end_time="02:00:00", route_step=5.0, variable_step=0.75,
+                      diameter=D, q=q)
+    runs = []
+    for off in ("1", "0"):
+        monkeypatch.setenv("SWMM5_NO_FREEZE", off)
+        s = _engine(inp, tmp_path)
+        snaps = []
+        for _ in range(6):
+            assert s.run_steps(50)[0] == 0
+            snaps.append([s.get_array("node." + f) for f in NODE_F] +
+                         [s.get_array("link." + f) for f in LINK_F])
+        runs.append((snaps, s.counters()))
+        s.end()
+        s.close()
+    for a, b in zip(runs[0][0], runs[1][0]):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    c0, c1 = runs[0][1], runs[1][1]
+    assert c0["iterations"] == c1["iterations"] and c0["nonconverged"] == c1["nonconverged"]
+    assert c0["nonconverged"] > 5 and c0["iterations"] > 3 * c0["steps"], c0
+
+
+@pytest.mark.gpu
 def test_benchmark_regime_window_707(tmp_path):
     """bench.py's 1m_surcharge workload (BASELINE configs[2]) after its 400-step
     spin-up: the next 12 steps of the engine against the oracle continuing
