@@ -74,6 +74,21 @@ def make_inp(nx, route_step, variable_step, pollutants, diameter, q, rows=None):
     return path
 
 
+def pmc_record(workload):
+    """profiles/pmc_traffic.json entry for this workload (tools/pmc_summary.py),
+    only when it was measured on the kernel source being run"""
+    import hashlib
+    tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(tp):
+        return None
+    rec = json.load(open(tp)).get(workload)
+    src = os.path.join(PKG, "csrc", "dw_kernels.hip")
+    sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
+    if not rec or rec.get("src_sha") != sha:
+        return None
+    return rec
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -270,17 +285,24 @@ def main():
         regather = 100.0 * tw["timed_gathered"] / (tw["timed_gather_iters"] * tw["nodes"])
     traffic = args.traffic
     traffic_src = "--traffic" if traffic is not None else None
+    step_bytes = None
     if traffic is None:                    # PMC measurement committed for this workload
-        tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(tp):
-            rec = json.load(open(tp)).get(workload)
-            if rec:
-                traffic, traffic_src = rec["bytes_per_launch"], rec["source"]
+        rec = pmc_record(workload)
+        if rec:
+            traffic, traffic_src = rec["bytes_per_launch"], rec["source"]
+            step_bytes = rec.get("step_bytes")
     roof = {
         "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
         "traffic_source": traffic_src,
+        # whole step: PMC HBM bytes per routing step (same workload and kernel
+        # source) over the measured step time
+        "step_traffic": step_bytes,
+        "step_achieved": None if not step_bytes else
+        round(step_bytes / (elapsed / args.steps) / 1e9, 2),
+        "step_frac": None if not step_bytes else
+        round(step_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
         "kernel": "k_link<first> (Picard iteration 0 link momentum, dwflow_findConduitFlow, "
                   "every conduit)",
         "avg_launch_us": round(first_us, 2),

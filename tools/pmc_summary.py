@@ -1,0 +1,122 @@
+#!/usr/bin/env python3
+"""HBM traffic from rocprofv3 --pmc passes of bench.py (separate FETCH_SIZE and
+WRITE_SIZE runs) and the calibration kernel (tools/pmc_calib).
+
+usage: pmc_summary.py <out_dir> [tag]
+
+The workload, spin-up, warm-up, timed steps and iterations per step come from
+the bench.py JSON line in <out_dir>/pmc_fetch.log.
+
+<out_dir> holds pmc_fetch/, pmc_write/ (bench.py runs) and calib_fetch/,
+calib_write/ (tools/pmc_calib runs), each with run_counter_collection.csv.
+
+Calibration: pmc_calib's kernels move exactly 2^31 bytes per launch; the ratio
+counter-kB x 1024 / 2^31 is this box's factor for 8-byte-per-lane fp64 loads
+and stores.  The engine's counters are divided by it.
+
+Window: bench.py launches [spinup][warmup][timed steps][timing-mode steps]
+[kernel reps]; dispatches are ordered by Dispatch_Id, and a routing step ends
+at its k_finalize, so the timed window is the dispatches after the
+(spinup + warmup)-th k_finalize up to and including the (spinup + warmup +
+steps)-th.  Per-step bytes = window bytes / steps.
+
+Writes profiles/pmc_traffic.json (keyed by workload, stamped with the sha256
+of dw_kernels.hip so that bench.py ignores it for any other kernel source) and
+prints a markdown summary."""
+import csv
+import hashlib
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "stormwater-management-model_amd", "csrc", "dw_kernels.hip")
+
+
+def src_sha():
+    return hashlib.sha256(open(SRC, "rb").read()).hexdigest()[:16]
+
+
+def short(n):
+    n = re.sub(r"\(swx::Params.*", "", n).replace("void swx::", "")
+    return re.sub(r"\(.*", "", n)
+
+
+def load(path):
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    return [(short(r["Kernel_Name"]), float(r["Counter_Value"])) for r in rows]
+
+
+def calib(d):
+    out = {}
+    for c, f in (("FETCH_SIZE", "calib_fetch"), ("WRITE_SIZE", "calib_write")):
+        p = os.path.join(d, f, "run_counter_collection.csv")
+        vals = defaultdict(list)
+        for name, v in load(p):
+            vals[name].append(v)
+        key = "k_read8" if c == "FETCH_SIZE" else "k_write8"
+        kb = sum(vals[key]) / len(vals[key])
+        out[c] = (kb * 1024.0) / 2.0 ** 31         # counter bytes / true bytes
+    return out
+
+
+def window(disp, start, end):
+    """dispatches after the start-th k_finalize through the end-th"""
+    fin = [i for i, (n, _) in enumerate(disp) if n.startswith("k_finalize")]
+    lo = fin[start - 1] + 1 if start > 0 else 0
+    return disp[lo:fin[end - 1] + 1]
+
+
+def main():
+    d = sys.argv[1]
+    tag = sys.argv[2] if len(sys.argv) > 2 else ""
+    line = [l for l in open(os.path.join(d, "pmc_fetch.log")) if l.startswith('{"metric"')][-1]
+    b = json.loads(line)
+    workload = b["config"]["workload"]
+    spinup, warmup, steps = b["config"]["spinup_steps"], b["warmup"], b["steps"]
+    ips = b["config"]["iterations_per_step"]
+    cal = calib(d)
+    per = defaultdict(lambda: [0.0, 0.0, 0])    # name -> [fetch B, write B, launches]
+    for c, f, col in (("FETCH_SIZE", "pmc_fetch", 0), ("WRITE_SIZE", "pmc_write", 1)):
+        disp = load(os.path.join(d, f, "run_counter_collection.csv"))
+        for name, v in window(disp, spinup + warmup, spinup + warmup + steps):
+            per[name][col] += v * 1024.0 / cal[c]
+            if col == 0:
+                per[name][2] += 1
+    step_bytes = sum(a + b for a, b, _ in per.values()) / steps
+    first = per.get("k_link<true, 3, true>")
+    first_launch = (first[0] + first[1]) / first[2] if first else None
+    print("# PMC HBM traffic %s\n" % tag)
+    print("Workload `%s`; timed window of %d steps after %d spin-up + %d warm-up steps "
+          "(%.2f Picard iterations/step).\n" % (workload, steps, spinup, warmup, ips))
+    print("Calibration (tools/pmc_calib, 2^31 B per launch, 8-B lanes): FETCH_SIZE counts %.4f, "
+          "WRITE_SIZE %.4f of the true bytes; the engine's counters are divided by these.\n"
+          % (cal["FETCH_SIZE"], cal["WRITE_SIZE"]))
+    print("| kernel | launches/step | read MB/step | write MB/step | MB/launch |")
+    print("|---|---|---|---|---|")
+    for name, (fb, wb, n) in sorted(per.items(), key=lambda kv: -(kv[1][0] + kv[1][1])):
+        print("| `%s` | %.2f | %.2f | %.2f | %.2f |" % (name, n / steps, fb / steps / 1e6,
+                                                       wb / steps / 1e6, (fb + wb) / max(n, 1) / 1e6))
+    print("\nHBM bytes per step: %.1f MB; k_link<first> per launch: %.1f MB"
+          % (step_bytes / 1e6, (first_launch or 0) / 1e6))
+    tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    rec = json.load(open(tp)) if os.path.exists(tp) else {}
+    rec = {k: v for k, v in rec.items() if isinstance(v, dict) and "src_sha" in v}
+    rec[workload] = {
+        "bytes_per_launch": round(first_launch) if first_launch else None,
+        "step_bytes": round(step_bytes),
+        "iterations_per_step": ips,
+        "calibration": {k: round(v, 4) for k, v in cal.items()},
+        "src_sha": src_sha(),
+        "source": "profiles/%s_pmc_summary.md (rocprofv3 FETCH_SIZE and WRITE_SIZE passes, "
+                  "calibrated by tools/pmc_calib)" % (tag or "pmc"),
+    }
+    with open(tp, "w") as f:
+        json.dump(rec, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
