@@ -64,6 +64,7 @@ __host__ __device__ inline bool partialIsMin(int q) { return q == 5 || q == 6; }
 constexpr int kTimeLevels = 6;     // TIMELEVELS (objects.h:941)
 constexpr int kDtRing = 4;          // host-mapped per-step dt ring (k_finalize -> host)
 constexpr int kLinkWavesDefault = 3;   // measured best on MI355X
+constexpr double kTailIters = 2.5;     // auto mode: k_tail while steps average at most this many iterations
 
 // ---- packed per-link flags -------------------------------------------------
 enum : uint32_t {
@@ -125,6 +126,8 @@ struct StepCtl {
     unsigned long long linkWork[kMaxTrialsCap];   // timing mode: conduits updated per iteration
     unsigned long long nodeWork[kMaxTrialsCap];   // timing mode: nodes gathered per iteration
     int ucount[kMaxTrialsCap];    // unconverged nodes (+ outfalls) listed by k_node at iteration k
+    unsigned tailBar;             // k_tail's grid-barrier arrivals (zeroed by k_link<first>)
+    int tailErr;                  // k_tail gave up waiting at a barrier (never expected)
     double stepRed[kNumPartials];     // this step's reduced block partials (k_finalize)
     // run statistics (stats.c): report-period step count / span, max system
     // outfall flow, routing time-step statistics (stats_updateTimeStepStats)
@@ -255,7 +258,8 @@ struct Params {
     const int* sharedList;        // local indices of the shared nodes
     int nShared, xflag;
     double *xsend, *xrecv;
-    double* hostDt;               // host-mapped ring of per-step dt (Router::launchedDt)
+    double* hostDt;               // host-mapped rings: per-step dt (Router::launchedDt), then
+                                  // the Picard iterations each step ran (auto k_tail choice)
     int nCold, nOutLinks;
     const int* coldLinks;         // LF_COLD conduits, ascending
     const int* outLinks;          // conduits with an outfall end, ascending
@@ -732,23 +736,66 @@ __device__ __forceinline__ void stageTables(double* ct, const double* g, int nGe
 // end), one thread per conduit.  No calls, no root finders.
 // kWaves: minimum waves per SIMD the register allocator must allow (1 = no
 // constraint); selected at start-up (SWMM5_LINK_WAVES, default kLinkWavesDefault)
+// the step converged at iteration m (dynwave.c:249-251): the frozen junctions
+// take their depth at that last iteration (a step that runs all MaxTrials
+// iterations does this in its last node update)
+__device__ __forceinline__ void finalizeFrozen(const Params& p, int m, int tid, int nthr)
+{
+    for (int i = tid; i < p.nN; i += nthr) {
+        const int fz = p.frz[i];
+        if (fz) {
+            p.nNewDepth[i] = frozenDepth(p, i, fz, m);
+            p.frz[i] = 0;
+        }
+    }
+}
+
+// Iterations k >= 2: a conduit is updated unless both end nodes have
+// converged (findBypassedLinks dynwave.c:335-345), i.e. exactly the conduits
+// incident to the nodes the node update listed as unconverged in the previous
+// iteration (outfalls are always listed).  Four threads per listed node walk
+// its CSR row; a conduit whose ends are both listed is taken by the
+// lower-numbered end.  cnt = the number of listed nodes; ct = staged tables.
+template <bool kFast>
+__device__ __forceinline__ int linkListWalk(const Params& p, int k, int cnt, double dt, const double* ct,
+                                            int tid, int nthr)
+{
+    const int* list = p.ulist + (size_t)((k - 1) & 1) * p.nN;
+    const int slots = 4 * cnt;
+    int work = 0;
+    for (int t = tid; t < slots; t += nthr) {
+        int u = list[t >> 2];
+        int e1 = p.rowptr[u + 1];
+        for (int e = p.rowptr[u] + (t & 3); e < e1; e += 4) {
+            int l = p.csr[e] & 0x7FFFFFFF;
+            uint32_t f = p.lflags[l];
+            if (f & LF_COLD) continue;                // the cold conduits' loop
+            int2 nn = p.lnodes[l];
+            int v = (nn.x == u) ? nn.y : nn.x;
+            if (!p.conv[v] && v < u) continue;        // listed too: v takes it
+            double y1 = frozenDepth(p, nn.x, p.frz[nn.x], k - 1);
+            double y2 = frozenDepth(p, nn.y, p.frz[nn.y], k - 1);
+            conduitFlow<false, false, kFast>(p, l, f, nn, k, dt, ct, y1, y2);
+            p.dirty[nn.x] = 1;
+            p.dirty[nn.y] = 1;
+            work++;
+        }
+    }
+    return work;
+}
+
+// Streaming kernel: every conduit with LF_COLD clear (zero offsets, no outfall
+// end), one thread per conduit.  No calls, no root finders.
+// kWaves: minimum waves per SIMD the register allocator must allow (1 = no
+// constraint); selected at start-up (SWMM5_LINK_WAVES, default kLinkWavesDefault)
 template <bool kFirst, int kWaves, bool kFast>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves)))
 void k_link(Params p, int k)
 {
+    const int tid = blockIdx.x * kBlock + threadIdx.x, nthr = gridDim.x * kBlock;
     if (k >= 2 && p.ctl->unconv[k - 1] == 0) {            // converged: dynwave.c:249-251
-        // the first launch after the step converged (iteration k-1 ran): the
-        // frozen junctions take their depth at that last iteration (a step
-        // that runs all MaxTrials iterations does this in its last k_node)
-        if (p.freeze && (k == 2 || p.ctl->unconv[k - 2] != 0)) {
-            for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
-                const int fz = p.frz[i];
-                if (fz) {
-                    p.nNewDepth[i] = frozenDepth(p, i, fz, k - 1);
-                    p.frz[i] = 0;
-                }
-            }
-        }
+        // the first launch after the step converged (iteration k-1 ran)
+        if (p.freeze && (k == 2 || p.ctl->unconv[k - 2] != 0)) finalizeFrozen(p, k - 1, tid, nthr);
         return;
     }
     if (p.nShared && blockIdx.x == 0 && threadIdx.x == 0) p.xsend[p.xflag] = 0.0;   // k_node sets it
@@ -756,44 +803,20 @@ void k_link(Params p, int k)
     double dt = p.ctl->dt;
     int work = 0;
     if (kFirst && blockIdx.x == 0 && threadIdx.x < kMaxTrialsCap) p.ctl->ucount[threadIdx.x] = 0;
+    if (kFirst && blockIdx.x == 0 && threadIdx.x == 0) p.ctl->tailBar = 0;
     if (kFirst || k < 2) {
         stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
-        for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nL; j += gridDim.x * kBlock) {
+        for (int j = tid; j < p.nL; j += nthr) {
             uint32_t f = p.lflags[j];
             if (f & LF_COLD) continue;
             int2 nn = p.lnodes[j];
             conduitFlow<kFirst, false, kFast>(p, j, f, nn, k, dt, ct, p.nNewDepth[nn.x], p.nNewDepth[nn.y]);
         }
     } else {
-        // Later iterations: a conduit is updated unless both end nodes have
-        // converged (findBypassedLinks dynwave.c:335-345), i.e. exactly the
-        // conduits incident to the nodes k_node listed as unconverged in the
-        // previous iteration (outfalls are always listed).  Four threads per
-        // listed node walk its CSR row; a conduit whose ends are both listed
-        // is taken by the lower-numbered end.
         const int cnt = p.ctl->ucount[k - 1];
-        const int* list = p.ulist + (size_t)((k - 1) & 1) * p.nN;
-        const int slots = 4 * cnt;
-        if (blockIdx.x * kBlock < slots) {                  // uniform per block
+        if (blockIdx.x * kBlock < 4 * cnt) {                // uniform per block
             stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
-            for (int t = blockIdx.x * kBlock + threadIdx.x; t < slots; t += gridDim.x * kBlock) {
-                int u = list[t >> 2];
-                int e1 = p.rowptr[u + 1];
-                for (int e = p.rowptr[u] + (t & 3); e < e1; e += 4) {
-                    int l = p.csr[e] & 0x7FFFFFFF;
-                    uint32_t f = p.lflags[l];
-                    if (f & LF_COLD) continue;                // k_link_cold's
-                    int2 nn = p.lnodes[l];
-                    int v = (nn.x == u) ? nn.y : nn.x;
-                    if (!p.conv[v] && v < u) continue;        // listed too: v takes it
-                    double y1 = frozenDepth(p, nn.x, p.frz[nn.x], k - 1);
-                    double y2 = frozenDepth(p, nn.y, p.frz[nn.y], k - 1);
-                    conduitFlow<kFirst, false, kFast>(p, l, f, nn, k, dt, ct, y1, y2);
-                    p.dirty[nn.x] = 1;
-                    p.dirty[nn.y] = 1;
-                    work++;
-                }
-            }
+            work = linkListWalk<kFast>(p, k, cnt, dt, ct, tid, nthr);
         }
     }
     // measurement only (eager timing launches, iterations >= 2 where links can
@@ -884,13 +907,9 @@ __device__ __forceinline__ double outfallCombine(const Params& p, int i, uint32_
 // The few conduits with an invert offset or an outfall end (compacted list):
 // full flow classification with normal / critical depth.
 template <bool kFirst>
-__global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
+__device__ __forceinline__ void coldConduits(const Params& p, int k, double dt, const double* ct, int tid, int nthr)
 {
-    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
-    __shared__ double ct[5 * SWX_CIRC_N];
-    stageTables(ct, p.gTables);
-    double dt = p.ctl->dt;
-    for (int c = blockIdx.x * kBlock + threadIdx.x; c < p.nCold; c += gridDim.x * kBlock) {
+    for (int c = tid; c < p.nCold; c += nthr) {
         int j = p.coldLinks[c];
         uint32_t f = p.lflags[j];
         int2 nn = p.lnodes[j];
@@ -900,6 +919,14 @@ __global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
         conduitFlow<kFirst, true>(p, j, f, nn, k, dt, ct, y1, y2);
         if (k >= 2) { p.dirty[nn.x] = 1; p.dirty[nn.y] = 1; }
     }
+}
+template <bool kFirst>
+__global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
+{
+    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
+    __shared__ double ct[5 * SWX_CIRC_N];
+    stageTables(ct, p.gTables);
+    coldConduits<kFirst>(p, k, p.ctl->dt, ct, blockIdx.x * kBlock + threadIdx.x, gridDim.x * kBlock);
 }
 
 // storage unit i's area relation (node_getVolume / node_getSurfArea for
@@ -1034,49 +1061,45 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
 // area relations are out-of-line calls whose stack frames and registers would
 // give every node update a large scratch segment (and throttle its waves), so
 // the other networks use a node update without them.
+// prologue of the node update: outfall depths (link_setOutfallDepth,
+// findNodeDepths dynwave.c:605) from this iteration's link flows, on the
+// blocks with blockIdx.x * 64 < nOutLinks; ct = staged circular tables,
+// yc = 64 doubles of LDS
 template <bool kFirst, bool kGeneral>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_node(Params p, int k)
+__device__ __forceinline__ void outfallPrologue(const Params& p, const double* ct, double* yc)
+{
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int base = blockIdx.x * 64; base < p.nOutLinks; base += gridDim.x * 64) {
+        int c = base + lane;
+        int j = (c < p.nOutLinks) ? p.outLinks[c] : -1;
+        uint32_t f = (j >= 0) ? p.lflags[j] : 0u;
+        double yn = 0.0;                               // non-conduits: yNorm = yCrit = 0
+        if (j >= 0 && w == 0 && !(f & LF_NC)) yn = outfallPart<0, kGeneral>(p, j, f, ct);
+        if (j >= 0 && w == 1) yc[lane] = (f & LF_NC) ? 0.0 : outfallPart<1, kGeneral>(p, j, f, ct);
+        __syncthreads();
+        if (j >= 0 && w == 0) {
+            int2 nn = p.lnodes[j];
+            int o = (f & LF_N2_OUTFALL) ? nn.y : nn.x;    // link.c:743-753 (node2 first)
+            double prev = p.nNewDepth[o];
+            if (kFirst) p.nOldDepth[o] = prev;             // node_setOldHydState before the update
+            if (p.nNC) p.nPrevDepth[o] = prev;
+            p.nNewDepth[o] = outfallCombine(p, o, p.nflags[o], j, yn, yc[lane]);
+        }
+        __syncthreads();
+    }
+}
+
+// findNodeDepths (dynwave.c:593-626) over the node index space (tid, nthr),
+// plus the unconverged-node list of iteration k and its convergence flag
+template <bool kFirst, bool kGeneral>
+__device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nthr)
 {
     constexpr bool kStorage = kGeneral;
-    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
-    // prologue: outfall depths (link_setOutfallDepth, findNodeDepths
-    // dynwave.c:605) from this iteration's link flows.  Only the outfall's
-    // single link reads that depth (next iteration), and this kernel never
-    // reads an outfall's depth, so it can run alongside the node updates; it
-    // goes first because it is the long (iterative) part of the launch.  The
-    // outfall is never "converged" (dynwave.c:281, 340): its link is never
-    // bypassed and the depth is refreshed every iteration, as in the reference.
-    // 64 outfall conduits per block and round: wave 0 finds their normal
-    // depths while wave 1 finds their critical depths, then wave 0 combines.
-    if (blockIdx.x * 64 < p.nOutLinks) {
-        __shared__ double ct[5 * SWX_CIRC_N];
-        __shared__ double yc[64];
-        stageTables(ct, p.gTables);
-        const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        for (int base = blockIdx.x * 64; base < p.nOutLinks; base += gridDim.x * 64) {
-            int c = base + lane;
-            int j = (c < p.nOutLinks) ? p.outLinks[c] : -1;
-            uint32_t f = (j >= 0) ? p.lflags[j] : 0u;
-            double yn = 0.0;                               // non-conduits: yNorm = yCrit = 0
-            if (j >= 0 && w == 0 && !(f & LF_NC)) yn = outfallPart<0, kGeneral>(p, j, f, ct);
-            if (j >= 0 && w == 1) yc[lane] = (f & LF_NC) ? 0.0 : outfallPart<1, kGeneral>(p, j, f, ct);
-            __syncthreads();
-            if (j >= 0 && w == 0) {
-                int2 nn = p.lnodes[j];
-                int o = (f & LF_N2_OUTFALL) ? nn.y : nn.x;    // link.c:743-753 (node2 first)
-                double prev = p.nNewDepth[o];
-                if (kFirst) p.nOldDepth[o] = prev;             // node_setOldHydState before the update
-                if (p.nNC) p.nPrevDepth[o] = prev;
-                p.nNewDepth[o] = outfallCombine(p, o, p.nflags[o], j, yn, yc[lane]);
-            }
-            __syncthreads();
-        }
-    }
     const double dt = p.ctl->dt;
     bool anyUnconv = false;
     int gathered = 0;
     int* ulist = p.ulist + (size_t)(k & 1) * p.nN;
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
+    for (int i = tid; i < p.nN; i += nthr) {
         uint32_t nf = p.nflags[i];
         int type = (int)(nf & NF_TYPE);
         // an outfall's depth is written by the prologue above: not read here
@@ -1239,6 +1262,103 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     if (!kFirst && k >= 2 && p.countWork) {                // measurement only
         for (int off = 32; off > 0; off >>= 1) gathered += __shfl_down(gathered, off, 64);
         if ((threadIdx.x & 63) == 0 && gathered) atomicAdd(&p.ctl->nodeWork[k], (unsigned long long)gathered);
+    }
+}
+
+template <bool kFirst, bool kGeneral>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral ? 3 : 4))) void k_node(Params p, int k)
+{
+    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
+    // prologue: outfall depths (link_setOutfallDepth, findNodeDepths
+    // dynwave.c:605) from this iteration's link flows.  Only the outfall's
+    // single link reads that depth (next iteration), and this kernel never
+    // reads an outfall's depth, so it can run alongside the node updates; it
+    // goes first because it is the long (iterative) part of the launch.  The
+    // outfall is never "converged" (dynwave.c:281, 340): its link is never
+    // bypassed and the depth is refreshed every iteration, as in the reference.
+    // 64 outfall conduits per block and round: wave 0 finds their normal
+    // depths while wave 1 finds their critical depths, then wave 0 combines.
+    if (blockIdx.x * 64 < p.nOutLinks) {
+        __shared__ double ct[5 * SWX_CIRC_N];
+        __shared__ double yc[64];
+        stageTables(ct, p.gTables);
+        outfallPrologue<kFirst, kGeneral>(p, ct, yc);
+    }
+    nodePass<kFirst, kGeneral>(p, k, blockIdx.x * kBlock + threadIdx.x, gridDim.x * kBlock);
+}
+
+// ---------------------------------------------------------------------------
+// k_tail: Picard iterations k >= 2 of one routing step in ONE launch.  The
+// unrolled step graph launches a link and a node kernel for every possible
+// iteration; those after convergence exit at once but still cost a dispatch
+// each (about 5.5 us, 12 of them per step on a network that converges in two
+// iterations).  k_tail runs the same per-iteration code (linkListWalk /
+// coldConduits, outfallPrologue, nodePass) with a grid barrier between the
+// link and node phases, and stops when an iteration converged -- no launch
+// at all for the iterations that do not run.  Its workgroups must all be
+// resident (grid = CUs x blocks per CU the occupancy admits, host-checked).
+//
+// Barrier (cdna_hip_programming.md Guideline 16): every wave drains its
+// stores, the workgroup meets, lane 0 releases at agent scope and adds to one
+// arrival counter (zeroed by k_link<first> each step), polls it relaxed, and
+// acquires at agent scope before the workgroup goes on.  Control words
+// written inside the launch (unconv, ucount) are read with atomic loads (the
+// vector path: the acquire does not refresh the scalar cache).  The spin is
+// bounded: a barrier that never completes sets StepCtl::tailErr and the
+// launch ends (the step is then reported as failed by the host).
+__device__ __forceinline__ bool tailBarrier(const Params& p, unsigned target)
+{
+    __shared__ int ok;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(&p.ctl->tailBar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // about 1 s at most (an earlier timeout anywhere ends this one at once)
+        int good = __hip_atomic_load(&p.ctl->tailErr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+        for (unsigned spins = 0; good &&
+             __hip_atomic_load(&p.ctl->tailBar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 20)) good = 0;
+            else if ((spins & 1023) == 0 &&
+                     __hip_atomic_load(&p.ctl->tailErr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) good = 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (!good) __hip_atomic_store(&p.ctl->tailErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = good;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    return ok != 0;
+}
+
+template <bool kFast, bool kGeneral>
+__global__ __launch_bounds__(kBlock) void k_tail(Params p)
+{
+    __shared__ double ct[kFast ? kCtFast : 5 * SWX_CIRC_N];
+    __shared__ double yc[64];
+    stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
+    const int tid = blockIdx.x * kBlock + threadIdx.x, nthr = gridDim.x * kBlock;
+    const double dt = p.ctl->dt;
+    unsigned arrivals = 0;
+    for (int k = 2; k < p.maxTrials; k++) {
+        // dynwave.c:249-251: iteration k-1 converged -- the step is done
+        if (__hip_atomic_load(&p.ctl->unconv[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+            if (p.freeze) finalizeFrozen(p, k - 1, tid, nthr);
+            return;
+        }
+        coldConduits<false>(p, k, dt, ct, tid, nthr);
+        const int cnt = __hip_atomic_load(&p.ctl->ucount[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        (void)linkListWalk<kFast>(p, k, cnt, dt, ct, tid, nthr);
+        arrivals += gridDim.x;
+        if (!tailBarrier(p, arrivals)) return;
+        // the every-shape root finders (the cold conduits' callees): calling
+        // the lean ones would loosen their register budget, and k_node's
+        if (blockIdx.x * 64 < p.nOutLinks) outfallPrologue<false, true>(p, ct, yc);
+        nodePass<false, kGeneral>(p, k, tid, nthr);
+        arrivals += gridDim.x;
+        if (!tailBarrier(p, arrivals)) return;
     }
 }
 
@@ -1971,6 +2091,7 @@ __global__ void k_finalize(Params p)
     // next step's dt straight into host memory: the host clock advances
     // without a copy command in the step (totalSteps = index of that step)
     p.hostDt[c->totalSteps % kDtRing] = dtn;
+    p.hostDt[kDtRing + (c->totalSteps - 1) % kDtRing] = (double)steps;   // Picard iterations of this step
     __threadfence_system();
     }
     __syncthreads();
@@ -2067,6 +2188,13 @@ struct Router::Impl {
     float *resNHost = nullptr, *resLHost = nullptr;  // pinned copies
     hipEvent_t forkEv[kMaxTrialsCap] = {}, joinEv[kMaxTrialsCap] = {};
     hipGraphExec_t graph = nullptr;
+    // step graph whose iterations k >= 2 run in k_tail (Router::step picks
+    // it or the unrolled graph: SWMM5_TAIL = 0 never, 1 always, else auto)
+    hipGraphExec_t graphTail = nullptr;
+    int tailMode = 2;
+    int tailGrid = 0;
+    double itersAvg = 0.0;           // moving average of Picard iterations per step
+    long long itersSeen = -1;        // last step whose count was read from hostDt
     bool useGraph = true;
     bool timing = false;
     int gridL = 1, gridN = 1, gridEnd = 1, gridC = 1;
@@ -2117,6 +2245,7 @@ Router::~Router()
 {
     if (d_) {
         if (d_->graph) (void)hipGraphExecDestroy(d_->graph);
+        if (d_->graphTail) (void)hipGraphExecDestroy(d_->graphTail);
         for (auto& t : d_->tslots) {
             for (auto e : t.ev) (void)hipEventDestroy(e);
             for (auto e : t.evHot) (void)hipEventDestroy(e);
@@ -2229,10 +2358,24 @@ static void launchIteration(Router::Impl* d, int k)
     if (d->timing) (void)hipEventRecord(d->curEv[4 * k + 2], d->stream);
 }
 
-static void launchStep(Router::Impl* d)
+typedef void (*TailFn)(Params);
+static TailFn tailKernel(bool fast, bool general)
+{
+    if (fast) return general ? k_tail<true, true> : k_tail<true, false>;
+    return general ? k_tail<false, true> : k_tail<false, false>;
+}
+
+// tail: iterations k >= 2 in one k_tail launch (d->tailGrid > 0 only)
+static void launchStep(Router::Impl* d, bool tail = false)
 {
     Params& p = d->p;
-    for (int k = 0; k < p.maxTrials; k++) launchIteration(d, k);
+    if (tail) {
+        launchIteration(d, 0);
+        launchIteration(d, 1);
+        hipLaunchKernelGGL(tailKernel(d->fastLinks, d->general), dim3(d->tailGrid), dim3(kBlock), 0, d->stream, p);
+    } else {
+        for (int k = 0; k < p.maxTrials; k++) launchIteration(d, k);
+    }
     int base = 4 * p.maxTrials;
     if (d->timing) (void)hipEventRecord(d->curEv[base], d->stream);
     if (p.P > 0) {
@@ -2922,7 +3065,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     HIPCHECK(hipHostMalloc((void**)&d->hostPinned, d->pinnedSize * sizeof(double), hipHostMallocDefault));
     for (auto& ev : d->ringEv) { HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming)); HIPCHECK(hipEventRecord(ev, d->stream)); }
     for (auto& ev : d->clockEv) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    HIPCHECK(hipHostMalloc((void**)&d->hostDt, Impl::kRing * sizeof(double),
+    HIPCHECK(hipHostMalloc((void**)&d->hostDt, 2 * Impl::kRing * sizeof(double),
                            hipHostMallocMapped | hipHostMallocCoherent));
     {
         void* dp = nullptr;
@@ -2982,6 +3125,30 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     HIPCHECK(hipStreamEndCapture(d->stream, &g));
     HIPCHECK(hipGraphInstantiate(&d->graph, g, nullptr, nullptr, 0));
     (void)hipGraphDestroy(g);
+    // the k_tail variant: single GPU, no pumps/regulators (k_nc runs between
+    // the node update and the next link update), at least three iterations;
+    // one workgroup per CU (all resident: checked against the occupancy)
+    {
+        const char* tm = getenv("SWMM5_TAIL");
+        d->tailMode = tm ? atoi(tm) : 2;
+        int occ = 0, cus = 0;
+        bool ok = d->tailMode != 0 && !part.active() && !d->comm && p.nNC == 0 && p.maxTrials > 2;
+        if (ok && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+                   hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                       &occ, (const void*)tailKernel(d->fastLinks, d->general), kBlock, 0) != hipSuccess))
+            ok = false;
+        (void)hipGetLastError();
+        const char* tw = getenv("SWMM5_TAIL_PER_CU");
+        int perCU = std::max(1, std::min(tw ? atoi(tw) : 1, occ - 1 > 0 ? occ - 1 : 1));
+        d->tailGrid = (ok && occ >= 1 && cus > 0) ? perCU * cus : 0;
+    }
+    if (d->tailGrid > 0) {
+        HIPCHECK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
+        launchStep(d, true);
+        HIPCHECK(hipStreamEndCapture(d->stream, &g));
+        HIPCHECK(hipGraphInstantiate(&d->graphTail, g, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(g);
+    }
     HIPCHECK(hipStreamSynchronize(d->stream));
     ok_ = true;
     return 0;
@@ -3028,6 +3195,28 @@ static void flushTiming(Router::Impl* d)
         if (p.P) { d->kms[3] += msq; d->kcnt[3]++; d->kbytesSum[3] += d->kbytes[3]; }
     }
     d->tUsed = 0;
+}
+
+// Unrolled or k_tail graph for the next step.  Auto: k_tail while the recent
+// steps ran few Picard iterations (the unrolled graph's dispatches of the
+// iterations that do not run dominate), the unrolled graph otherwise.  The
+// iteration counts come from the host-mapped ring k_finalize writes (steps
+// already complete; no synchronisation).  Both graphs run the same code on
+// the same data: the choice changes no result.
+static bool useTail(Router::Impl* d)
+{
+    if (d->tailGrid <= 0) return false;
+    if (d->tailMode == 1) return true;
+    long long done = d->launched - 2;              // steps surely past their k_finalize?
+    while (d->itersSeen < done) {
+        long long n = d->itersSeen + 1;
+        if (n < 0) { d->itersSeen = n; continue; }
+        if (hipEventQuery(d->clockEv[n % Router::Impl::kRing]) != hipSuccess) break;
+        double it = d->hostDt[Router::Impl::kRing + n % Router::Impl::kRing];
+        d->itersAvg = (d->itersSeen < 0) ? it : 0.9 * d->itersAvg + 0.1 * it;
+        d->itersSeen = n;
+    }
+    return d->itersSeen < 0 || d->itersAvg <= kTailIters;
 }
 
 int Router::step(const double* latFlow, const double* qualLoad, const double tot[3])
@@ -3087,7 +3276,7 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
                                 hipMemcpyDeviceToHost, d->stream));
         HIPCHECK(hipMemsetAsync(d->ctl->linkWork, 0, 2 * kMaxTrialsCap * sizeof(unsigned long long), d->stream));
     } else if (d->useGraph) {
-        HIPCHECK(hipGraphLaunch(d->graph, d->stream));
+        HIPCHECK(hipGraphLaunch(useTail(d) ? d->graphTail : d->graph, d->stream));
     } else {
         launchStep(d);
     }
@@ -3423,6 +3612,10 @@ static void pullCtl(Router::Impl* d, int& err, std::string& msg)
     if (e != hipSuccess && !err) {
         err = 500;
         msg = std::string("ERROR 500: GPU router: ") + hipGetErrorString(e);
+    }
+    if (e == hipSuccess && d->hostCtl->tailErr && !err) {
+        err = 500;
+        msg = "ERROR 500: GPU router: k_tail grid barrier timed out (workgroups not co-resident)";
     }
 }
 

@@ -205,14 +205,18 @@ def test_frozen_junctions_bitwise(tmp_path, monkeypatch):
     bypassed are not visited; their depth is advanced by the same relaxation
     steps when it is next read) change no bit of the result: the 60 x 60
     surcharged variable-step run with and without freezing, every node and
-    link field and every counter compared bitwise over 300 steps."""
+    link field and every counter compared bitwise over 300 steps.  The same
+    for the step graph whose iterations k >= 2 run in one persistent k_tail
+    launch (grid barriers between the link and node phases) instead of one
+    launch per iteration."""
     q, D = 0.3, 1.0
     inp = str(tmp_path / "g.inp")
     netgen.write_grid(inp, 60, 60, end_time="02:00:00", route_step=5.0, variable_step=0.75,
                       diameter=D, q=q)
     runs = []
-    for off in ("1", "0"):
+    for off, tail in (("1", "0"), ("0", "0"), ("0", "1"), ("1", "1")):
         monkeypatch.setenv("SWMM5_NO_FREEZE", off)
+        monkeypatch.setenv("SWMM5_TAIL", tail)
         s = _engine(inp, tmp_path)
         snaps = []
         for _ in range(6):
@@ -222,11 +226,13 @@ def test_frozen_junctions_bitwise(tmp_path, monkeypatch):
         runs.append((snaps, s.counters()))
         s.end()
         s.close()
-    for a, b in zip(runs[0][0], runs[1][0]):
-        for x, y in zip(a, b):
-            np.testing.assert_array_equal(x, y)
-    c0, c1 = runs[0][1], runs[1][1]
-    assert c0["iterations"] == c1["iterations"] and c0["nonconverged"] == c1["nonconverged"]
+    for r in runs[1:]:
+        for a, b in zip(runs[0][0], r[0]):
+            for x, y in zip(a, b):
+                np.testing.assert_array_equal(x, y)
+    c0 = runs[0][1]
+    for _, c1 in runs[1:]:
+        assert c0["iterations"] == c1["iterations"] and c0["nonconverged"] == c1["nonconverged"]
     assert c0["nonconverged"] > 5 and c0["iterations"] > 3 * c0["steps"], c0
 
 

@@ -21,9 +21,12 @@ for s in $STEPS; do
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pytest) run pytest_gpu 900 python -m pytest tests -q -m gpu --maxfail=5 -p no:cacheprovider ;;
     bench)  run bench 600 python bench.py ;;
+    benchq)  run benchq 600 python bench.py --steps 200 --no-cpu ;;
+    tailab) for t in 0 1; do SWMM5_TAIL=$t run bench_tail$t 600 python bench.py --steps 200 --no-cpu; SWMM5_TAIL=$t run bench100k_tail$t 600 python bench.py --config 100k --steps 400 --no-cpu; done ;;
     bench100k) run bench100k 600 python bench.py --config 100k --steps 400 --no-cpu ;;
     benchall) for c in 100k 1m_fixed 1m_quality; do run bench_$c 600 python bench.py --config $c --no-cpu; done ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --no-cpu ;;
+    prof100k) run prof100k 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof100k -o run -- python3 bench.py --config 100k --steps 200 --no-cpu ;;
     probe)  run probe 120 ./tools/outfall_latency ;;
     mrehearse) run mrehearse 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 5 --grid 120 --spinup 50 --exchange host --no-cpu ;;
     gsweep) for g in ${GFACTORS:-0.34 0.67 2}; do SWMM5_GRID_FACTOR=$g run gsweep_$g 300 python bench.py --no-cpu; done ;;
