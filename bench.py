@@ -18,6 +18,10 @@ Workloads (--config; BASELINE.json configs):
   1m_quality (configs[3]) the same plus 3 pollutants (advection + decay).
   100k (configs[1]) 224 x 224 grid = 99,905 conduits, fixed 1 s step.
   1m_fixed  707 x 707, fixed 1 s step, 1.5-ft pipes (no surcharge).
+  4m (configs[4]) 1414 x 1414 grid = 3,995,965 conduits, the 1m_surcharge
+        hydraulics; the same grid at every rank count (strong scaling), one
+        row strip per rank.  The other presets scale weakly: N ranks route a
+        (707 N) x 707 grid, one 707-row strip each.
 
 Extra JSON objects:
   roofline      dominant kernel (link momentum) algorithmic bytes per launch
@@ -52,6 +56,10 @@ PRESETS = {
                  pollutants=0, spinup=0),
     "1m_fixed": dict(grid=707, route_step=1.0, variable_step=0.0, diameter=1.5, q=0.02,
                      pollutants=0, spinup=0),
+    # configs[4]: one 1414 x 1414 grid (3,995,965 conduits) whatever the rank
+    # count, link-partitioned into row strips (strong scaling)
+    "4m": dict(grid=1414, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.1,
+               pollutants=0, spinup=400, strong=True),
 }
 
 
@@ -166,8 +174,10 @@ def main():
 
     import swmm5
     # weak scaling: world row strips of grid x grid junctions (about 1M conduits
-    # per GPU), link-partitioned, one RCCL all-reduce per Picard iteration
-    rows = cfg["grid"] * world
+    # per GPU), link-partitioned, one RCCL all-reduce per Picard iteration;
+    # strong scaling (4m): one grid x grid network split into world strips
+    strong = cfg.get("strong", False)
+    rows = cfg["grid"] if strong else cfg["grid"] * world
     if rank == 0:
         inp = make_inp(cfg["grid"], cfg["route_step"], cfg["variable_step"], cfg["pollutants"],
                        cfg["diameter"], cfg["q"], rows=rows)
@@ -355,7 +365,7 @@ def main():
             "effective_value": None if eff is None else round(value * eff, 1),
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic",
             "config": {"workload": workload,
                        "conduits": nL, "nodes": nN, "pollutants": cfg["pollutants"],

@@ -55,8 +55,9 @@ def write_grid(path: str, nx: int, ny: int, *, diameter: float = 1.5,
                variable_step: float = 0.0, end_time: str = "06:00:00",
                report_step: str = "00:15:00", pollutants: int = 0,
                threads: int = 1, report_all: bool | None = None,
-               extra_options=()) -> tuple[int, int]:
-    """Write the SURVEY.md 8(d) Manhattan grid; returns (nodes, conduits)."""
+               extra_options=(), files: str = "") -> tuple[int, int]:
+    """Write the SURVEY.md 8(d) Manhattan grid; returns (nodes, conduits).
+    `files` is the body of an optional [FILES] section (hot start files)."""
     if report_all is None:
         report_all = nx * ny <= 2500
     slope_drop = 0.002 * 400.0
@@ -105,6 +106,8 @@ def write_grid(path: str, nx: int, ny: int, *, diameter: float = 1.5,
     if report_all:
         w("NODES ALL\nLINKS ALL\n")
     w("\n")
+    if files:
+        w("[FILES]\n" + files.rstrip("\n") + "\n\n")
     d = os.path.dirname(os.path.abspath(path))
     os.makedirs(d, exist_ok=True)
     with open(path, "w") as f:

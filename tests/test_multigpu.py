@@ -221,3 +221,39 @@ def test_rccl_single_rank_bitwise(tmp_path):
         if k.startswith(("node.", "link.")):
             np.testing.assert_array_equal(rc[k], one[k], err_msg=k)
     np.testing.assert_array_equal(rc["counters"], one["counters"])
+
+
+@pytest.mark.gpu
+def test_two_ranks_match_one_gpu_4m(tmp_path):
+    """BASELINE configs[4] at full size: bench.py's 4m preset, a 1414 x 1414
+    grid of 3,995,965 conduits, split into two row strips (host transport, both
+    ranks on this box's GPU) against one GPU, in the benchmark's regime.  One
+    GPU spins the network up for 2000 s and saves a hot start file; both runs
+    restart from it for 15 steps, which surcharge and do not all converge."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bench
+    cfg = bench.PRESETS["4m"]
+    n = cfg["grid"]
+    hs = str(tmp_path / "spin.hsf")
+    kw = dict(route_step=cfg["route_step"], variable_step=cfg["variable_step"],
+              diameter=cfg["diameter"], q=cfg["q"], report_all=False)
+    spin = str(tmp_path / "spin.inp")
+    netgen.write_grid(spin, n, n, end_time="00:33:20", files='SAVE HOTSTART "%s"' % hs, **kw)
+    _run_workers(spin, 100000, tmp_path, 1, "host", "spin")
+    assert os.path.getsize(hs) > 0
+    inp = str(tmp_path / "g4m.inp")
+    netgen.write_grid(inp, n, n, end_time="06:00:00", files='USE HOTSTART "%s"' % hs, **kw)
+    steps = 15
+    one = _run_workers(inp, steps, tmp_path, 1, "host", "one")[0]
+    st, its, nonconv = one["counters"]
+    assert one["link.newFlow"].size == 3995965
+    assert nonconv > 0 and its / st > 3.0, one["counters"]
+    assert (one["node.newDepth"][:-1] > cfg["diameter"]).sum() > 1000
+    parts = _run_workers(inp, steps, tmp_path, 2, "host", "two")
+    node, link = _merge(parts)
+    for k, v in node.items():
+        np.testing.assert_allclose(v, one[k], rtol=1e-9, atol=1e-12, err_msg=k)
+    for k, v in link.items():
+        np.testing.assert_allclose(v, one[k], rtol=1e-9, atol=1e-12, err_msg=k)
+    for part in parts:
+        np.testing.assert_array_equal(part["counters"], one["counters"])

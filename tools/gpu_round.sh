@@ -19,13 +19,15 @@ for s in $STEPS; do
   case $s in
     build)  run build 600 python -c "import __graft_entry__ as g; g.build()" ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) run pytest_gpu 900 python -m pytest tests -q -m gpu --maxfail=5 -p no:cacheprovider ;;
+    pytest) run pytest_gpu 900 python -u -m pytest tests -v -m gpu --maxfail=5 -p no:cacheprovider --timeout 600 --timeout-method thread ;;
     bench)  run bench 600 python bench.py ;;
     benchq)  run benchq 600 python bench.py --steps 200 --no-cpu ;;
     tailab) for t in 0 1; do SWMM5_TAIL=$t run bench_tail$t 600 python bench.py --steps 200 --no-cpu; SWMM5_TAIL=$t run bench100k_tail$t 600 python bench.py --config 100k --steps 400 --no-cpu; done ;;
     bench100k) run bench100k 600 python bench.py --config 100k --steps 400 --no-cpu ;;
     benchall) for c in 100k 1m_fixed 1m_quality; do run bench_$c 600 python bench.py --config $c --no-cpu; done ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --no-cpu ;;
+    bench4m) run bench4m 900 python bench.py --config 4m --steps 100 ;;
+    mrehearse4m) run mrehearse4m 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --config 4m --steps 10 --warmup 2 --spinup 20 --exchange host --no-cpu ;;
     prof100k) run prof100k 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof100k -o run -- python3 bench.py --config 100k --steps 200 --no-cpu ;;
     probe)  run probe 120 ./tools/outfall_latency ;;
     mrehearse) run mrehearse 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 5 --grid 120 --spinup 50 --exchange host --no-cpu ;;
