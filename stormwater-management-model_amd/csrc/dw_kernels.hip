@@ -13,7 +13,8 @@
 //                    outfall depth (link.c:728-766) and continuity/depth update
 //                    (setNodeDepth, dynwave.c:636-762); wave-level ballot of the
 //                    convergence test (dynwave.c:618) into one flag per iteration
-//   k_qual_node / k_qual_link   pollutant advection (qualrout.c:100-142)
+//   k_qual_node    pollutant advection at the nodes (qualrout.c:100-142); the
+//                  links' part runs in k_step_end's link pass (qualLink)
 //   k_step_end     capacity-limited links, outfall system outflow, flow totals
 //                  and Courant-step partials (dynwave.c:349-378, 799-921,
 //                  routing.c:841-925)
@@ -62,6 +63,7 @@ constexpr int kMaxTrialsCap = 32;
 constexpr int kNumPartials = 10;
 __host__ __device__ inline bool partialIsMin(int q) { return q == 5 || q == 6; }
 constexpr int kTimeLevels = 6;     // TIMELEVELS (objects.h:941)
+constexpr int kQualBatch = 4;      // pollutants whose node mass inflow k_qual_node sums in one link pass
 constexpr int kDtRing = 4;          // host-mapped per-step dt ring (k_finalize -> host)
 constexpr int kLinkWavesDefault = 3;   // measured best on MI355X
 constexpr double kTailIters = 2.5;     // auto mode: k_tail while steps average at most this many iterations
@@ -1630,19 +1632,29 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
             double vEvap = p.nEvapVol[i];
             if (vEvap > 0.0 && oldVol > 0.0353147) fEvap += vEvap / oldVol;
         }
-        for (int pp = 0; pp < p.P; pp++) {
+        // mass inflow of every pollutant in one pass over the node's links
+        // (each pollutant's sum in link order, as qualrout.c:162-174 adds it)
+        double wq[kQualBatch];
+        for (int p0 = 0; p0 < p.P; p0 += kQualBatch) {
+        const int np = (p.P - p0 < kQualBatch) ? p.P - p0 : kQualBatch;
+        for (int b = 0; b < np; b++) wq[b] = p.qualIn[(size_t)(p0 + b) * p.nN + i];
+        for (int e = e0; e < e1; e++) {
+            int ent = p.qcsr[e];
+            int l = ent & 0x7FFFFFFF;
+            bool isN2 = ent < 0;
+            double ql = p.lNewFlow[l];
+            bool down = isN2 ? !(ql < 0.0) : (ql < 0.0);
+            if (down) {
+                const double aq = fabs(ql);
+                for (int b = 0; b < np; b++) wq[b] += aq * p.lNewQual[(size_t)(p0 + b) * p.nL + l];
+            }
+        }
+        for (int b = 0; b < np; b++) {
+            const int pp = p0 + b;
             size_t ni = (size_t)pp * p.nN + i;
             double cOld = p.nNewQual[ni];           // node_setOldQualState
             p.nOldQual[ni] = cOld;
-            double w = p.qualIn[ni];
-            for (int e = e0; e < e1; e++) {
-                int ent = p.qcsr[e];
-                int l = ent & 0x7FFFFFFF;
-                bool isN2 = ent < 0;
-                double ql = p.lNewFlow[l];
-                bool down = isN2 ? !(ql < 0.0) : (ql < 0.0);
-                if (down) w += fabs(ql) * p.lNewQual[(size_t)pp * p.nL + l];
-            }
+            double w = wq[b];
             double c;
             if (isStorage || oldVol > 0.0353147) {
                 double c1 = reactedQual(p.kDecay[pp], cOld * fEvap, dt);
@@ -1655,25 +1667,26 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
             }
             p.nNewQual[ni] = c;
         }
+        }
     }
 }
 
-// qualrout.c:253-353 (DW) -- link quality; rotates link quality.
-__global__ __launch_bounds__(kBlock) void k_qual_link(Params p)
+// qualrout.c:253-353 (DW) -- quality of link j; rotates link quality.  Runs
+// in k_step_end's link pass (after k_qual_node), which reads the same link
+// state.
+__device__ __forceinline__ void qualLink(const Params& p, int j, uint32_t f, double dt)
 {
-    const double dt = p.ctl->dt;
-    for (int j = blockIdx.x * kBlock + threadIdx.x; j < p.nL; j += gridDim.x * kBlock) {
+    {
         int2 nn = p.lnodes[j];
         double nf = p.lNewFlow[j];
         int up = (nf < 0.0) ? nn.y : nn.x;
-        uint32_t f = p.lflags[j];
         if (f & LF_NC) {                      // non-conduit: upstream node's quality (qualrout.c:283-291)
             for (int pp = 0; pp < p.P; pp++) {
                 size_t li = (size_t)pp * p.nL + j;
                 p.lOldQual[li] = p.lNewQual[li];
                 p.lNewQual[li] = p.nNewQual[(size_t)pp * p.nN + up];
             }
-            continue;
+            return;
         }
         double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
         double qIn = fabs(p.q1[j]) * barrels;
@@ -1763,6 +1776,7 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
     // links (fixed order within a thread: j = tid, tid + n, ...)
     for (int j = tid; j < p.nL; j += n) {
         uint32_t f = p.lflags[j];
+        if (p.P > 0) qualLink(p, j, f, dt);                // qualrout_execute's link part
         if (f & LF_NC) {                                   // stats_updateLinkStats, non-conduits
             if (!stats) continue;
             double newFlow = p.lNewFlow[j], oldFlow = p.lOldFlow[j];
@@ -2378,10 +2392,8 @@ static void launchStep(Router::Impl* d, bool tail = false)
     }
     int base = 4 * p.maxTrials;
     if (d->timing) (void)hipEventRecord(d->curEv[base], d->stream);
-    if (p.P > 0) {
+    if (p.P > 0)                                   // the link part runs in k_step_end
         hipLaunchKernelGGL(k_qual_node, dim3(d->gridN), dim3(kBlock), 0, d->stream, p);
-        hipLaunchKernelGGL(k_qual_link, dim3(d->gridL), dim3(kBlock), 0, d->stream, p);
-    }
     if (d->timing) (void)hipEventRecord(d->curEv[base + 1], d->stream);
     hipLaunchKernelGGL(stepEndKernel(d->fastLinks, d->allShapes), dim3(d->gridEnd), dim3(kBlock), 0, d->stream, p);
     if (d->part.active() && p.varStep) {           // global Courant limits (min over ranks)

@@ -26,6 +26,7 @@ for s in $STEPS; do
     bench100k) run bench100k 600 python bench.py --config 100k --steps 400 --no-cpu ;;
     benchall) for c in 100k 1m_fixed 1m_quality; do run bench_$c 600 python bench.py --config $c --no-cpu; done ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --no-cpu ;;
+    benchqual) run benchqual 600 python bench.py --config 1m_quality --steps 200 --no-cpu ;;
     bench4m) run bench4m 900 python bench.py --config 4m --steps 100 ;;
     mrehearse4m) run mrehearse4m 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --config 4m --steps 10 --warmup 2 --spinup 20 --exchange host --no-cpu ;;
     prof100k) run prof100k 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof100k -o run -- python3 bench.py --config 100k --steps 200 --no-cpu ;;
