@@ -324,8 +324,11 @@ static void writeStatic(void)
 
 static char* ActText = NULL;
 
-static void applyActions(int step)
+/* returns the seconds of a swmm_stride call that replaces this step's
+   swmm_step (property -1), or 0 */
+static int applyActions(int step)
 {
+    int stride = 0;
     char buf[4096];
     char* save = NULL;
     char* tok;
@@ -339,6 +342,7 @@ static void applyActions(int step)
         double value = 0.0;
         if (sscanf(tok, "%d:%d:%255[^:]:%lf", &at, &prop, name, &value) != 4) continue;
         if (at != step) continue;
+        if (prop == -1) { stride = (int)value; continue; }
         if (strcmp(name, "-"))
         {
             idx = swmm_getIndex(prop >= 400 ? swmm_LINK : swmm_NODE, name);
@@ -346,6 +350,7 @@ static void applyActions(int step)
         }
         swmm_setValue(prop, idx, value);
     }
+    return stride;
 }
 
 int main(int argc, char** argv)
@@ -373,7 +378,9 @@ int main(int argc, char** argv)
     writeStatic();
     /* optional swmm_setValue calls between steps, for the API golden cases:
        REFDUMP_ACTIONS="afterStep:property:objectName:value;..." (objectName
-       "-" for system properties); applied once `afterStep` steps are done */
+       "-" for system properties); applied once `afterStep` steps are done.
+       Property -1: that call is swmm_stride(value seconds) instead of
+       swmm_step (one record, like a step) */
     {
         const char* env = getenv("REFDUMP_ACTIONS");
         if (env) ActText = strdup(env);
@@ -381,8 +388,11 @@ int main(int argc, char** argv)
     do
     {
         double told = NewRoutingTime;
-        applyActions(step);
-        swmm_step(&elapsed);
+        {
+            int stride = applyActions(step);
+            if (stride > 0) swmm_stride(stride, &elapsed);
+            else swmm_step(&elapsed);
+        }
         step++;
         if (step % every == 0 || elapsed <= 0.0)
         {

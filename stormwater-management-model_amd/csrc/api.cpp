@@ -280,19 +280,21 @@ int DLLEXPORT swmm_stride(int strideStep, double* elapsedTime)   // swmm5.c:466-
     if (!G->isStarted || G->hostOnly) return (G->errorCode = 502);
     Project& prj = *G->prj;
     double realRouteStep = prj.opt.routeStep;
+    const double durPrev = G->routingDuration;           // in force at the last step's end
     double dur = G->newRoutingTime + 1000.0 * strideStep;
     if (prj.opt.totalDuration < dur) dur = prj.opt.totalDuration;
     G->routingDuration = dur;
-    if (G->router->setDuration(dur)) return setErr(G->router->lastError(), G->router->lastErrorMsg());
-    if (strideStep < prj.opt.routeStep)
-        return setErr(500, "ERROR 500: swmm_stride shorter than the routing step is not supported by the MI355X engine");
+    if (strideStep < prj.opt.routeStep) prj.opt.routeStep = strideStep;   // RouteStep = strideStep meanwhile
+    if (G->router->repickStep(prj.opt.routeStep, durPrev, dur))
+        return setErr(G->router->lastError(), G->router->lastErrorMsg());
     double e = 0.0;
     do {
         swmm_step(&e);
     } while (e > 0.0 && !G->errorCode);
     prj.opt.routeStep = realRouteStep;
     G->routingDuration = prj.opt.totalDuration;
-    G->router->setDuration(G->routingDuration);
+    if (!G->errorCode && G->router->repickStep(realRouteStep, dur, G->routingDuration))
+        return setErr(G->router->lastError(), G->router->lastErrorMsg());
     if (G->newRoutingTime < prj.opt.totalDuration) G->elapsedTime = G->newRoutingTime / kMsecPerDay;
     else G->elapsedTime = 0.0;
     if (elapsedTime) *elapsedTime = G->elapsedTime;

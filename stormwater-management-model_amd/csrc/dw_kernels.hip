@@ -1713,6 +1713,23 @@ __device__ __forceinline__ void qualLink(const Params& p, int j, uint32_t f, dou
     }
 }
 
+// getVariableStep (dynwave.c:799-832) from the uncapped link and node
+// Courant minima: getLinkStep(maxStep) then getNodeStep(tMinLink), the
+// absolute minimum, then the millisecond floor of dynwave_getRoutingStep.
+// *crit: 2 = a node, 1 = a link set the step (stats_updateCriticalTimeCount),
+// 0 = the cap did
+__host__ __device__ inline double courantStep(double linkMin, double nodeMin, double maxStep,
+                                              double minStep, int* crit)
+{
+    double tMinLink = maxStep;
+    *crit = 0;
+    if (linkMin < tMinLink) { tMinLink = linkMin; *crit = 1; }
+    double tMin = tMinLink;
+    if (nodeMin < tMinLink) { tMin = nodeMin; *crit = 2; }
+    if (tMin < minStep) tMin = minStep;
+    return floor(1000.0 * tMin) / 1000.0;
+}
+
 // combine two partial vectors (sums; mins keep the first occurrence)
 __device__ __forceinline__ void combinePartials(double* a, const double* b)
 {
@@ -1752,8 +1769,10 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
     stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
     double acc[kNumPartials];
     for (int q = 0; q < kNumPartials; q++) acc[q] = 0.0;
-    acc[5] = p.routeStep; acc[8] = 1.0e300;
-    acc[6] = p.routeStep; acc[9] = 1.0e300;
+    // Courant limits uncapped: k_finalize caps them with the routing step in
+    // force when the next step begins (swmm_stride may lower it meanwhile)
+    acc[5] = 1.0e300; acc[8] = 1.0e300;
+    acc[6] = 1.0e300; acc[9] = 1.0e300;
     StepCtl* c = p.ctl;
     const double dt = c->dt;
     const double half = dt / 2.;
@@ -2084,16 +2103,15 @@ __global__ void k_finalize(Params p)
     // 799-832) then execRouting's end-of-run clamp (swmm5.c:538-546)
     double dtn = c->routeStep;
     if (p.varStep && !c->varStepOff) {
-        double tMin = tot[5];
-        if (tot[6] < tMin) tMin = tot[6];
+        int crit = 0;
+        double tMin = courantStep(tot[5], tot[6], c->routeStep, p.minRouteStep, &crit);
         // getVariableStep's critical element (dynwave.c:815-828) -- counted
         // when that next step will actually be routed (swmm5.c:531)
         if (!p.multi && c->newRoutingTime < c->routingDuration) {
-            if (tot[6] < tot[5]) p.st.timeCourant[(int)tot[9]] += 1.0;
-            else if (tot[8] < 1.0e299) p.st.lTimeCourant[(int)tot[8]] += 1.0;
+            if (crit == 2) p.st.timeCourant[(int)tot[9]] += 1.0;
+            else if (crit == 1) p.st.lTimeCourant[(int)tot[8]] += 1.0;
         }
-        if (tMin < p.minRouteStep) tMin = p.minRouteStep;
-        c->variableStep = floor(1000.0 * tMin) / 1000.0;
+        c->variableStep = tMin;
         dtn = c->variableStep;
     }
     c->dtNext = dtn;
@@ -3323,25 +3341,6 @@ int Router::readClock(double* t, double* lastDt, double* nextDt)
     return 0;
 }
 
-int Router::setDuration(double msec)
-{
-    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
-    Impl* d = d_;
-    HIPCHECK(hipStreamSynchronize(d->stream));
-    HIPCHECK(hipMemcpy(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost));
-    d->hostCtl->routingDuration = msec;
-    // re-apply the clamp for the step about to run
-    double dtn = d->hostCtl->dtNext > 0 ? d->hostCtl->dtNext : d->hostCtl->dt;
-    if (d->hostCtl->newRoutingTime + 1000.0 * dtn > msec) {
-        dtn = (msec - d->hostCtl->newRoutingTime) / 1000.0;
-        dtn = (dtn >= 1. / 1000.0) ? dtn : 1. / 1000.0;
-    }
-    d->hostCtl->dt = dtn;
-    HIPCHECK(hipMemcpy(d->ctl, d->hostCtl, sizeof(StepCtl), hipMemcpyHostToDevice));
-    d->hostDt[d->launched % Impl::kRing] = dtn;      // the next step's slot
-    return 0;
-}
-
 int Router::sync()
 {
     auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
@@ -3750,6 +3749,61 @@ int Router::setOutfallStage(int g, double stage)
     f = (int)(((uint32_t)f & ~(0x7u << NF_OTYPE_SHIFT)) | ((uint32_t)O_FIXED << NF_OTYPE_SHIFT));
     HIPCHECK(hipMemcpy((void*)(p.nflags + i), &f, sizeof(int), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy((void*)(p.fixedStage + i), &stage, sizeof(double), hipMemcpyHostToDevice));
+    return 0;
+}
+
+// swmm_stride (swmm5.c:466-510) ends the routing period at the stride's end
+// and lowers RouteStep to the stride for the steps it runs, then restores
+// both.  The reference takes each step's length at the start of that step
+// (routing_getRoutingStep(RouteStep), counting the Courant-critical element
+// if the step is routed at all); the engine chose the pending step's length
+// at the end of the previous one, under the cap and period end then in force
+// (durBefore).  It is chosen again here under `cap` and durAfter from the
+// same uncapped Courant minima (StepCtl::stepRed), the critical-element count
+// moved with it, and the end of the period re-applied.
+int Router::repickStep(double cap, double durBefore, double durAfter)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    const Params& p = d->p;
+    HIPCHECK(hipStreamSynchronize(d->stream));
+    HIPCHECK(hipMemcpy(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost));
+    StepCtl* h = d->hostCtl;
+    const double oldCap = h->routeStep;
+    h->routeStep = cap;
+    h->routingDuration = durAfter;
+    if (!p.varStep || h->varStepOff) {
+        h->dtNext = cap;                                   // fixed step
+    } else if (h->totalSteps > 0) {                        // the first step is MinRouteStep whatever the cap
+        int c0 = 0, c1 = 0;
+        (void)courantStep(h->stepRed[5], h->stepRed[6], oldCap, p.minRouteStep, &c0);
+        const double t = courantStep(h->stepRed[5], h->stepRed[6], cap, p.minRouteStep, &c1);
+        if (!(h->newRoutingTime < durBefore)) c0 = 0;     // k_finalize did not count it
+        if (!(h->newRoutingTime < durAfter)) c1 = 0;      // the reference will not
+        if (c0 != c1 && !p.multi) {
+            auto bump = [&](int crit, double by) -> int {
+                double* a = (crit == 2) ? p.st.timeCourant + (int)h->stepRed[9]
+                                        : p.st.lTimeCourant + (int)h->stepRed[8];
+                double v = 0.0;
+                HIPCHECK(hipMemcpy(&v, a, sizeof(double), hipMemcpyDeviceToHost));
+                v += by;
+                HIPCHECK(hipMemcpy(a, &v, sizeof(double), hipMemcpyHostToDevice));
+                return 0;
+            };
+            if (c0 && bump(c0, -1.0)) return err_;
+            if (c1 && bump(c1, 1.0)) return err_;
+        }
+        h->variableStep = t;
+        h->dtNext = t;
+    }
+    double dtn = h->dtNext > 0 ? h->dtNext : h->dt;
+    if (h->newRoutingTime + 1000.0 * dtn > durAfter) {
+        dtn = (durAfter - h->newRoutingTime) / 1000.0;
+        dtn = (dtn >= 1. / 1000.0) ? dtn : 1. / 1000.0;
+    }
+    h->dt = dtn;
+    HIPCHECK(hipMemcpy(d->ctl, d->hostCtl, sizeof(StepCtl), hipMemcpyHostToDevice));
+    d->hostDt[d->launched % Impl::kRing] = dtn;            // the next step's slot
     return 0;
 }
 

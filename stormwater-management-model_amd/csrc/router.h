@@ -53,7 +53,6 @@ public:
     // this rank's partition (whole network when running on one GPU)
     const Partition& partition() const;
     // Change the routing duration (msec) used for the end-of-run clamp.
-    int setDuration(double msec);
     // Copy device state into the host mirror (prj.st); synchronises.
     int download(Project& prj);
     // One state value of node / link g (global index) straight from HBM;
@@ -67,6 +66,9 @@ public:
     // swmm_setValue(ROUTESTEP) between steps (setRoutingStep, swmm5.c:1360-
     // 1370): fixed steps of `step` sec from now on, next step dtNext sec
     int setRouteStep(double step, double dtNext);
+    // swmm_stride: routing-step cap and end of the routing period for the
+    // following steps; the pending step's length is chosen again under them
+    int repickStep(double cap, double durBefore, double durAfter);
     // Results of one reporting period packed on the device in the .out
     // variable order (nodes: 6 + P floats each, links: 5 + P), interpolated
     // with weight f and converted with the unit factors; pointers to pinned

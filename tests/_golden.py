@@ -16,7 +16,8 @@ CASES = ["grid12", "grid12_var_qual", "grid10_surcharge", "example", "example_va
          "example_irregular", "example_irregular_var", "example_culverts", "example_culverts_var",
          "example_tidal", "example_tidal_var", "example_roadway", "example_dividers",
          "example_streets", "example_extfile", "example_branches", "example_branches_var",
-         "example_slot_pond", "example_options", "grid10_slot"]
+         "example_slot_pond", "example_options", "grid10_slot", "example_stride",
+         "example_stride_fixed"]
 # cases using objects outside the C restatement's scope (oracle/dw_oracle.c
 # covers junctions, outfalls and conduits): pinned by the GPU tests against the
 # reference's own fixtures only
@@ -25,7 +26,9 @@ BEYOND_ORACLE = {"example_storage", "example_storage_var", "example_storage_qual
                  "example_shapes_var", "example_irregular", "example_irregular_var",
                  "example_culverts", "example_culverts_var", "example_tidal", "example_tidal_var",
                  "example_roadway", "example_dividers", "example_streets", "example_branches",
-                 "example_branches_var"}
+                 "example_branches_var",
+                 # swmm_stride calls: an API driver the C restatement does not model
+                 "example_stride", "example_stride_fixed"}
 # cases whose input writes a file next to itself ([FILES] SAVE ...): they run
 # from a private copy so the fixtures directory is never written to
 SAVES = {"example_hotsave": "example_hotsave.hsf"}
@@ -126,13 +129,27 @@ def actions(d: dict) -> list:
     return out
 
 
-def apply_actions(s, acts: list, done: int) -> None:
-    """Make the same swmm_setValue calls on engine `s` once `done` steps ran."""
+def apply_actions(s, acts: list, done: int) -> int:
+    """Make the same swmm_setValue calls on engine `s` once `done` steps ran;
+    returns the seconds of a swmm_stride that replaces the next swmm_step
+    (property -1 in the fixture), else 0."""
+    stride = 0
     for at, prop, name, val in acts:
         if at != done:
+            continue
+        if prop == -1:
+            stride = int(val)
             continue
         idx = -1
         if name != "-":
             idx = s.getIndex(2 if prop < 400 else 3, name)
             assert idx >= 0, name
         s.setValue(prop, idx, val)
+    return stride
+
+
+def advance(s, acts: list, done: int):
+    """The reference run's next call after `done` calls: its setValue calls,
+    then swmm_step or swmm_stride; returns (error, elapsed days)."""
+    stride = apply_actions(s, acts, done)
+    return s.stride(stride) if stride > 0 else s.step()

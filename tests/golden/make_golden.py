@@ -142,10 +142,16 @@ CASES = {
     # swmm_setValue between steps: external inflow, outfall stage, routing step
     "example_api": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
                                                variable_step=0.75), 1),
+    # swmm_stride calls shorter and longer than the routing step (swmm5.c:466-510)
+    "example_stride": (netgen.write_example, dict(end_time="01:00:00", route_step=60.0,
+                                                  variable_step=0.75), 1),
+    "example_stride_fixed": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0), 1),
 }
 # REFDUMP_ACTIONS per case: "afterStep:property:object:value" (swmm5.h codes)
 ACTIONS = {
     "example_api": "40:306:N3:2.5;90:304:O1:104.2;150:3:-:4.0;200:306:N3:0.0;260:304:O2:104.5",
+    "example_stride": "10:-1:-:3;11:-1:-:7;12:-1:-:45;30:-1:-:25;31:-1:-:2;50:-1:-:1;51:-1:-:90",
+    "example_stride_fixed": "20:-1:-:3;21:-1:-:7;40:-1:-:25;41:-1:-:4",
 }
 
 

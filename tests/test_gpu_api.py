@@ -30,8 +30,7 @@ def test_getvalue_from_device_equals_mirror_and_reference(tmp_path):
     nn, nl = s.getCount(swmm5.NODE), s.getCount(swmm5.LINK)
     checked = 0
     for step in range(1, 301):
-        _golden.apply_actions(s, acts, step - 1)
-        err, t = s.step()
+        err, t = _golden.advance(s, acts, step - 1)
         assert err == 0, s.getError()
         if step % 37:
             continue

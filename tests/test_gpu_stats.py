@@ -33,8 +33,7 @@ def _run(name, tmp_path):
     assert s.start(True) == 0, s.getError()
     acts, done = _golden.actions(d), 0
     while True:
-        _golden.apply_actions(s, acts, done)
-        err, t = s.step()
+        err, t = _golden.advance(s, acts, done)
         done += 1
         assert err == 0, s.getError()
         if t == 0.0:
