@@ -296,6 +296,7 @@ def main():
     traffic = args.traffic
     traffic_src = "--traffic" if traffic is not None else None
     step_bytes = None
+    rec = None
     if traffic is None:                    # PMC measurement committed for this workload
         rec = pmc_record(workload)
         if rec:
@@ -309,6 +310,7 @@ def main():
         # whole step: PMC HBM bytes per routing step (same workload and kernel
         # source) over the measured step time
         "step_traffic": step_bytes,
+        "step_traffic_iterations_per_step": None if not step_bytes else rec.get("iterations_per_step"),
         "step_achieved": None if not step_bytes else
         round(step_bytes / (elapsed / args.steps) / 1e9, 2),
         "step_frac": None if not step_bytes else
