@@ -1340,7 +1340,6 @@ __global__ __launch_bounds__(kBlock) void k_tail(Params p)
 {
     __shared__ double ct[kFast ? kCtFast : 5 * SWX_CIRC_N];
     __shared__ double yc[64];
-    stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
     const int tid = blockIdx.x * kBlock + threadIdx.x, nthr = gridDim.x * kBlock;
     const double dt = p.ctl->dt;
     unsigned arrivals = 0;
@@ -1350,6 +1349,7 @@ __global__ __launch_bounds__(kBlock) void k_tail(Params p)
             if (p.freeze) finalizeFrozen(p, k - 1, tid, nthr);
             return;
         }
+        if (k == 2) stageTables(ct, p.gTables, kFast ? p.nGeom : 0);   // only when an iteration runs
         coldConduits<false>(p, k, dt, ct, tid, nthr);
         const int cnt = __hip_atomic_load(&p.ctl->ucount[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         (void)linkListWalk<kFast>(p, k, cnt, dt, ct, tid, nthr);
@@ -3141,8 +3141,18 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         d->kbytes[1] = N * (44 + 4 + 40 + 32 + 52) + E * (4 + 24 + 4);
         d->nodeFix = N * (44 + 40 + 52 - 16 + 1);
         d->nodeGather = 4 + 32 + (N > 0 ? (double)E / N * 32.0 : 0.0);
-        d->kbytes[2] = L * (4 + 8 + 8 + 8 + 8 + 8 + 4) + N * (4 + 8 * 6);
-        d->kbytes[3] = P ? (N * (24 + 16.0 * P) + E * (4 + 8 + 8.0 * P) + L * (72 + 24.0 * P)) : 0.0;
+        // step end: per conduit flags, state word (r+w), a1, aFull, newFlow,
+        //   froude, newVolume, modLength, length (48 + 4) and the run
+        //   statistics: oldFlow, maxFlow, newDepth, maxVeloc, maxDepth, the
+        //   flow-class time (r+w), qFull, turn sign (r+w) (96): 148; per node
+        //   flags, inflow, outflow, overflow, volumes, depths, crown, invert,
+        //   dYdT (84), the volume totals and pending rates (r+w, 80), the node
+        //   statistics avgDepth (r+w), maxDepth, newLat, oldLat, totLat (r+w),
+        //   maxLat, maxInflow, maxOverflow, conv (96): 260 (conditional
+        //   updates of maxima and times not counted); with pollutants the
+        //   links' quality update (qualLink) runs here too: 72 + 24 P
+        d->kbytes[2] = L * (148.0 + (P ? 72 + 24.0 * P : 0.0)) + N * 260.0;
+        d->kbytes[3] = P ? (N * (24 + 16.0 * P) + E * (4 + 8 + 8.0 * P)) : 0.0;
     }
 
     // ---- capture the step graph ----------------------------------------------
