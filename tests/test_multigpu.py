@@ -118,6 +118,13 @@ def _decompose_worker(rank, world, port, n1, n2, q, lat, node_owner, link_owner,
 
 
 def test_exchange_sums_gloo_world2(tmp_path):
+    """The per-iteration exchange's arithmetic as a world-size-2 gloo job on
+    the engine's own partition (node and link owners from partition.cpp,
+    through the host-only swmm_open of each rank): every rank sums its own
+    conduits and the owner's lateral inflow, the all-reduce combines them,
+    and every replica sees the whole network's sums.  The device side of the
+    exchange (k_node partials, k_node_shared) runs in the GPU tests
+    (test_two_ranks_match_one_gpu*, host transport, against one GPU)."""
     import torch.multiprocessing as mp
     inp = _grid(tmp_path)
     d = _topology(inp, tmp_path)
@@ -128,7 +135,11 @@ def test_exchange_sums_gloo_world2(tmp_path):
     q = rng.normal(0.0, 1.0, nL)
     lat = np.abs(rng.normal(0.0, 0.1, nN))
     world = 2
-    node_owner, link_owner = _ref_owners(n1, n2, ntype, nN, world)
+    node_owner, link_owner = _owners(inp, tmp_path, 0, world)
+    for r in range(1, world):                  # every rank computes the same owners
+        no, lo = _owners(inp, tmp_path, r, world)
+        np.testing.assert_array_equal(no, node_owner)
+        np.testing.assert_array_equal(lo, link_owner)
     ctx = mp.get_context("spawn")
     outq = ctx.Queue()
     port = _free_port()
