@@ -376,8 +376,10 @@ def main():
                        "nonconverged_steps": nonconv,
                        "surcharged_pct": round(surcharged, 2),
                        "sim_time_at_end_s": round(t_days * 86400.0, 1),
-                       "parallelism": ("link-partitioned x%d (row strips), RCCL all-reduce of "
-                                       "shared-node sums per Picard iteration" % world)
+                       "parallelism": ("link-partitioned x%d (row strips), %s all-reduce of "
+                                       "shared-node sums per Picard iteration"
+                                       % (world, "RCCL" if args.exchange == "rccl" else
+                                          "host-transport (gloo)"))
                                       if world > 1 else "single",
                        "backend": backend},
             "roofline": roof,
