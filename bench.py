@@ -169,8 +169,6 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo")
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")   # single-node RCCL bootstrap
-        if cfg["pollutants"]:
-            raise SystemExit("multi-GPU runs do not support pollutants yet")
 
     import swmm5
     # weak scaling: world row strips of grid x grid junctions (about 1M conduits
@@ -257,13 +255,13 @@ def main():
     err, _ = s.run_steps(args.timing_steps)
     kt = s.kernel_times()
     kb = s.kernel_bytes()
+    its = s.iteration_stats()
     tw = s.counters()
     s.set_timing(False)
     # dominant kernel alone: back-to-back launches between two HIP events on
     # the routing stream (per-launch dispatch gaps amortised); after the timed
     # run because it advances the state
-    first_us = s.time_kernel(0, args.kernel_reps)
-    node_us = s.time_kernel(1, args.kernel_reps)
+    b2b_us = s.time_kernel(0, args.kernel_reps) if args.kernel_reps > 0 else 0.0
     s.end()
     s.close()
 
@@ -282,6 +280,7 @@ def main():
         return kb[name] / (us * 1e-6) / 1e9 if us > 0 else 0.0
 
     first_bytes = kb["link_momentum_first"]
+    first_us = avg_us("link_momentum_first")          # in-step, kernel execution timestamps
     achieved = first_bytes / (first_us * 1e-6) / 1e9
     it_n = kt["link_momentum_iter"][0]
     n0 = kt["link_momentum_first"][0]
@@ -302,37 +301,62 @@ def main():
         if rec:
             traffic, traffic_src = rec["bytes_per_launch"], rec["source"]
             step_bytes = rec.get("step_bytes")
+            # the PMC pass must have measured this same window (same steps, same
+            # regime); otherwise its per-step bytes describe another workload
+            if rec.get("window") not in (None, [cfg["spinup"], args.warmup, args.steps]) or \
+                    abs(rec.get("iterations_per_step", 0) - iters / args.steps) > 1e-6:
+                step_bytes = None
+    step_s = elapsed / args.steps
     roof = {
         "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
         "traffic_source": traffic_src,
-        # whole step: PMC HBM bytes per routing step (same workload and kernel
-        # source) over the measured step time
+        # whole step: PMC HBM bytes per routing step of the same timed window
+        # (same workload, steps, iterations and kernel source) over the
+        # measured step time
         "step_traffic": step_bytes,
         "step_traffic_iterations_per_step": None if not step_bytes else rec.get("iterations_per_step"),
-        "step_achieved": None if not step_bytes else
-        round(step_bytes / (elapsed / args.steps) / 1e9, 2),
-        "step_frac": None if not step_bytes else
-        round(step_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+        "step_achieved": None if not step_bytes else round(step_bytes / step_s / 1e9, 2),
+        "step_frac": None if not step_bytes else round(step_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4),
         "kernel": "k_link<first> (Picard iteration 0 link momentum, dwflow_findConduitFlow, "
                   "every conduit)",
         "avg_launch_us": round(first_us, 2),
-        "timing": "%d back-to-back launches between HIP events on the routing stream" % args.kernel_reps,
+        "timing": ("in-step: %d routing steps launched eagerly, each kernel with "
+                   "hipExtLaunchKernelGGL start/stop events (the kernel's own execution "
+                   "timestamps, as rocprofv3's kernel trace)" % kt["link_momentum_first"][0]),
         "bytes_per_launch": first_bytes,
         "other_kernels": {
-            "k_link<first> in-step (event pair)": {"avg_launch_us": round(avg_us("link_momentum_first"), 2)},
-            "k_node<first> back-to-back": {"avg_launch_us": round(node_us, 2)},
+            "k_link<first> back-to-back": {
+                "avg_launch_us": round(b2b_us, 2),
+                "achieved_GBs": round(first_bytes / (b2b_us * 1e-6) / 1e9, 1) if b2b_us else None,
+                "note": "%d back-to-back launches of a separately named instantiation on the live "
+                        "state (caches warm from the previous launch); secondary" % args.kernel_reps},
+            "k_node<first>": {"avg_launch_us": round(avg_us("node_update_first"), 2),
+                              "achieved_GBs": round(gbs("node_update_first"), 1)},
             "k_link iterations>=1": {"avg_launch_us": round(avg_us("link_momentum_iter"), 2),
                                      "achieved_GBs": round(gbs("link_momentum_iter"), 1),
                                      "bypassed_pct": None if bypass is None else round(bypass, 2)},
-            "k_node": {"avg_launch_us": round(avg_us("node_update"), 2),
-                       "achieved_GBs": round(gbs("node_update"), 1),
-                       "regathered_pct_iter_ge2": None if regather is None else round(regather, 2)},
+            "k_node iteration 1": {"avg_launch_us": round(avg_us("node_update_iter1"), 2),
+                                   "achieved_GBs": round(gbs("node_update_iter1"), 1)},
+            "k_node iterations>=2": {"avg_launch_us": round(avg_us("node_update_iter2plus"), 2),
+                                     "achieved_GBs": round(gbs("node_update_iter2plus"), 1),
+                                     "regathered_pct": None if regather is None else round(regather, 2)},
             "k_step_end+k_finalize": {"avg_launch_us": round(avg_us("step_end"), 2),
                                       "achieved_GBs": round(gbs("step_end"), 1)},
         },
     }
+    # per Picard iteration of the timing-mode steps: how much work each one
+    # does and what its two launches cost
+    per_iter = []
+    for k, r in enumerate(its):
+        if r[0] > 0:
+            per_iter.append({"k": k, "runs": int(r[0]), "conduits_updated": round(r[1] / r[0]),
+                             "nodes_updated": round(r[3] / r[0]), "nodes_relax_only": round(r[4] / r[0]),
+                             "nodes_gathered": round(r[2] / r[0]),
+                             "k_link_us": round(1000.0 * r[5] / r[0], 2),
+                             "k_node_us": round(1000.0 * r[6] / r[0], 2)})
+    roof["per_iteration"] = per_iter
     if cfg["pollutants"]:
         roof["other_kernels"]["k_qual_node+k_qual_link"] = {
             "avg_launch_us": round(avg_us("quality"), 2), "achieved_GBs": round(gbs("quality"), 1)}
@@ -376,10 +400,11 @@ def main():
                        "nonconverged_steps": nonconv,
                        "surcharged_pct": round(surcharged, 2),
                        "sim_time_at_end_s": round(t_days * 86400.0, 1),
-                       "parallelism": ("link-partitioned x%d (row strips), %s all-reduce of "
-                                       "shared-node sums per Picard iteration"
-                                       % (world, "RCCL" if args.exchange == "rccl" else
-                                          "host-transport (gloo)"))
+                       "parallelism": ("link-partitioned x%d (row strips); per Picard iteration "
+                                       "%s of the strip neighbours' ghost-link values and an "
+                                       "all-reduce(max) of the convergence flag"
+                                       % (world, "RCCL ncclSend/ncclRecv" if args.exchange == "rccl"
+                                          else "host-transport (gloo) exchange"))
                                       if world > 1 else "single",
                        "backend": backend},
             "roofline": roof,

@@ -43,13 +43,17 @@ int    DLLEXPORT swmmx_runSteps(int n, double *elapsedTime);
  * iterations >= 2.  Synchronises with the device. */
 int    DLLEXPORT swmmx_getCounters(long long *out, int n);
 
-/* Device kernel timing (HIP events on the routing stream; steps run as eager
- * launches while enabled).  mode=1 enables, 0 disables; swmmx_getKernelTimes
- * returns, per kernel class, the number of timed launches and their total
+/* Device kernel timing (steps run as eager launches while enabled; each timed
+ * kernel is launched with hipExtLaunchKernelGGL, whose start/stop events carry
+ * the kernel's own execution timestamps -- the durations rocprofv3's kernel
+ * trace reports).  mode=1 enables, 0 disables; swmmx_getKernelTimes returns,
+ * per kernel class, the number of timed launches and their total
  * milliseconds:  out[2*k] = launches, out[2*k+1] = ms;
  *   k: 0 link momentum, Picard iteration 0 (k_link<first>: every conduit),
- *      1 node update, 2 step end, 3 quality,
- *      4 link momentum, executed iterations >= 1 (bypassed conduits skipped).
+ *      1 node update of iteration 0, 2 step end (k_step_end .. k_finalize),
+ *      3 quality, 4 link momentum, executed iterations >= 1 (bypassed
+ *      conduits skipped), 5 node update of iteration 1, 6 node updates of the
+ *      executed iterations >= 2.
  * Returns the number of classes written. */
 int    DLLEXPORT swmmx_setTiming(int mode);
 int    DLLEXPORT swmmx_getKernelTimes(double *out, int n);
@@ -60,10 +64,19 @@ int    DLLEXPORT swmmx_getKernelTimes(double *out, int n);
  * or the model value for a full launch when nothing has been timed. */
 int    DLLEXPORT swmmx_getKernelBytes(double *out, int n);
 
+/* Per Picard iteration k of the steps timed since swmmx_setTiming(1), seven
+ * values each (out[7k .. 7k+6]): iterations run, conduits updated (not
+ * bypassed), nodes that gathered their conduits, nodes updated (not frozen),
+ * relaxation-only node updates, k_link ms, k_node ms.  Returns the number of
+ * values available (7 x MAX_TRIALS once a step was timed). */
+int    DLLEXPORT swmmx_getIterationStats(double *out, int n);
+
 /* Average duration (microseconds) of `reps` back-to-back launches of one
  * kernel on the live state: which = 0 link momentum of Picard iteration 0,
- * 1 node update of iteration 0.  Measurement only: it advances the state, so
- * call it after the run being measured. */
+ * 1 node update of iteration 0.  The launches are of separate instantiations
+ * (k_link<..., probe = true>, k_node<..., probe = true>) so that a profiler's
+ * per-kernel statistics keep them apart from the routing steps'.  Measurement
+ * only: it advances the state, so call it after the run being measured. */
 int    DLLEXPORT swmmx_timeKernel(int which, int reps, double *avgUs);
 
 /* Name of the compute backend ("hip:gfx950:<device name>" or "none"). */
@@ -74,12 +87,15 @@ int    DLLEXPORT swmmx_setDevice(int ordinal);
 
 /* ---- multi-GPU (one process per GPU) ----------------
  * The network is split by node blocks (a conduit follows its node1, an
- * outfall its conduit); every Picard iteration all-reduces the partial
- * {inflow, outflow, surface area, dq/dh} sums of the nodes shared between
- * ranks over RCCL.  Call before swmm_start, on every rank:
+ * outfall its conduit; pumps / regulators keep their end nodes on one rank).
+ * A rank holds the nodes its links touch; the other ranks' links touching
+ * them are its ghost links, whose {flow, surface areas, dq/dh} the owners send
+ * every Picard iteration (RCCL ncclSend / ncclRecv between neighbours), so
+ * every held node is summed over all its links in the reference's order and
+ * the run is bitwise equal to one GPU.  Call before swmm_start, on every rank:
  *   rank 0: swmmx_ncclUniqueId(id, 128) and broadcast the id to the others;
  *   all:    swmmx_setPartition(rank, nranks, id, 128).
- * Water quality and the binary results file are single-GPU only for now. */
+ * The binary results file and hot start saving are single-GPU only for now. */
 int    DLLEXPORT swmmx_ncclUniqueId(void *out, int bytes);     /* returns bytes written */
 int    DLLEXPORT swmmx_setPartition(int rank, int nranks, const void *ncclId, int idBytes);
 
@@ -91,6 +107,16 @@ int    DLLEXPORT swmmx_setExchange(int (*fn)(double *buf, long n, int op, void *
 /* Owning rank of every node (objType swmm_NODE) or link (swmm_LINK) under the
  * current partition; returns the object count. */
 int    DLLEXPORT swmmx_getOwner(int objType, int *out, int n);
+
+/* This rank's part of the current partition (after swmm_open), by name:
+ * "lnode" held nodes (global indices), "llink" owned links, "lghost" ghost
+ * links, "nbr" neighbour ranks, "sendOff" / "sendLink" links sent to each
+ * neighbour (local owned indices), "recvOff" ghosts received from each,
+ * "hasGhost" per held node, "rowptr" / "csr" the node -> link incidence the
+ * node update sums (local link indices, ghosts after the owned links, bit 31
+ * = the node is the link's node2).  Copies at most n values; returns the
+ * array's length or -1. */
+long   DLLEXPORT swmmx_getPartition(const char *name, int *out, long n);
 
 /* Cross-section known-answer evaluation (test extension; needs no project).
  * Builds a section of reference shape code `type` from the four [XSECTIONS]

@@ -285,8 +285,11 @@ int DLLEXPORT swmm_stride(int strideStep, double* elapsedTime)   // swmm5.c:466-
     if (prj.opt.totalDuration < dur) dur = prj.opt.totalDuration;
     G->routingDuration = dur;
     if (strideStep < prj.opt.routeStep) prj.opt.routeStep = strideStep;   // RouteStep = strideStep meanwhile
-    if (G->router->repickStep(prj.opt.routeStep, durPrev, dur))
+    if (G->router->repickStep(prj.opt.routeStep, durPrev, dur)) {
+        prj.opt.routeStep = realRouteStep;               // leave the engine's step and duration as they were
+        G->routingDuration = durPrev;
         return setErr(G->router->lastError(), G->router->lastErrorMsg());
+    }
     double e = 0.0;
     do {
         swmm_step(&e);
@@ -964,6 +967,12 @@ int DLLEXPORT swmmx_getKernelTimes(double* out, int n)
     return G->router->kernelTimes(out, n);
 }
 
+int DLLEXPORT swmmx_getIterationStats(double* out, int n)
+{
+    if (!G || !G->router) return 0;
+    return G->router->iterationStats(out, n);
+}
+
 int DLLEXPORT swmmx_getKernelBytes(double* out, int n)
 {
     if (!G || !G->router) return 0;
@@ -1046,6 +1055,34 @@ int DLLEXPORT swmmx_getOwner(int objType, int* out, int n)
     int k = std::min(n, (int)v.size());
     for (int i = 0; i < k; i++) out[i] = v[i];
     return (int)v.size();
+}
+
+long DLLEXPORT swmmx_getPartition(const char* name, int* out, long n)
+{
+    if (!G || !G->prj || !name) return -1;
+    Partition p;
+    p.rank = gPart.rank;
+    p.nranks = gPart.nranks;
+    std::string m;
+    if (buildPartition(G->prj->net, p, &m)) return -1;
+    std::vector<int> rowptr, csr, hg;
+    const std::string nm = name;
+    const std::vector<int>* v = nullptr;
+    if (nm == "lnode") v = &p.lnode;
+    else if (nm == "llink") v = &p.llink;
+    else if (nm == "lghost") v = &p.lghost;
+    else if (nm == "nbr") v = &p.nbr;
+    else if (nm == "sendOff") v = &p.sendOff;
+    else if (nm == "sendLink") v = &p.sendLink;
+    else if (nm == "recvOff") v = &p.recvOff;
+    else if (nm == "hasGhost") { hg.assign(p.hasGhost.begin(), p.hasGhost.end()); v = &hg; }
+    else if (nm == "rowptr" || nm == "csr") {
+        buildLocalCsr(G->prj->net, p, true, rowptr, csr);
+        v = (nm == "rowptr") ? &rowptr : &csr;
+    } else return -1;
+    long k = std::min<long>(n, (long)v->size());
+    for (long i = 0; i < k && out; i++) out[i] = (*v)[i];
+    return (long)v->size();
 }
 
 int DLLEXPORT swmmx_setDevice(int ordinal)

@@ -25,6 +25,7 @@
 // glibc ulps in pow/exp/sqrt/sin/cos the arithmetic is the reference's.
 // No MFMA: the path is HBM-bandwidth bound (DESIGN.md has the byte model).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <array>
@@ -55,7 +56,6 @@ namespace swx {
     } while (0)
 
 constexpr int kBlock = 256;
-constexpr int kMaxTrialsCap = 32;
 // per-block partials written by k_step_end: [0] outflow [1] flooding [2] extra
 // external inflow [3] evap [4] seep (sums), [5] link Courant step [6] node
 // Courant step (min, with their first-occurrence indices in [8] [9]),
@@ -114,7 +114,6 @@ struct StepCtl {
     double dt;                    // step length used by the current step
     double dtNext;                // variable step computed at step end
     double variableStep;          // dynwave.c:84 VariableStep
-    int unconv[kMaxTrialsCap];    // per-iteration "some node not converged" flag
     int lastSteps;
     int varStepOff;               // swmm_setValue(ROUTESTEP) mid-run: CourantFactor = 0
     long long totalSteps, totalIters, nonConverge;
@@ -125,9 +124,6 @@ struct StepCtl {
     double newRoutingTime;            // msec (swmm5.c / routing.c clock mirror)
     double routingDuration;           // msec
     double routeStep;                 // fixed step (sec)
-    unsigned long long linkWork[kMaxTrialsCap];   // timing mode: conduits updated per iteration
-    unsigned long long nodeWork[kMaxTrialsCap];   // timing mode: nodes gathered per iteration
-    int ucount[kMaxTrialsCap];    // unconverged nodes (+ outfalls) listed by k_node at iteration k
     unsigned tailBar;             // k_tail's grid-barrier arrivals (zeroed by k_link<first>)
     int tailErr;                  // k_tail gave up waiting at a barrier (never expected)
     double stepRed[kNumPartials];     // this step's reduced block partials (k_finalize)
@@ -252,14 +248,24 @@ struct Params {
     StatsDev st;
     int multi;                    // partitioned (multi-GPU) run
     int countWork;                // timing mode: count updated conduits per iteration
-    // multi-GPU exchange (partition.h): per local node its global shared slot
-    // (-1 if interior); partial sums {inflow, outflow, surfArea, sumdqdh} of
-    // shared nodes go to xsend[4*slot..], the all-reduced sums come back in
-    // xrecv; xsend[xflag] = 1 when an interior node did not converge
-    const int* sharedSlot;
-    const int* sharedList;        // local indices of the shared nodes
-    int nShared, xflag;
+    // multi-GPU exchange (partition.h): link arrays hold this rank's owned
+    // links [0, nL) and its ghost links [nL, nLs) (other ranks' links touching
+    // a held node).  Each iteration k_xpack packs the owned links other ranks
+    // hold as ghosts (sendLink) into xsend, xF values each; the received
+    // values (xrecv, ghost order) are unpacked into the ghost slots by
+    // k_xunpack before k_node sums every held node over all its links
+    int nLs;                      // owned + ghost links (stride of [p][link] quality arrays)
+    int nSend, nGhost, xF;
+    const int* sendLink;
     double *xsend, *xrecv;
+    // per Picard iteration k < maxTrials (sized from MAX_TRIALS): unconv[k] =
+    // "some node did not converge in iteration k"; ucount[k] = nodes (and
+    // outfalls) k_node listed for the next iteration's link walk; work[4][k]
+    // timing-mode counters: conduits updated, nodes gathered, nodes updated
+    // (not frozen), relaxation-only node updates
+    int* unconv;
+    int* ucount;
+    unsigned long long* work;
     double* hostDt;               // host-mapped rings: per-step dt (Router::launchedDt), then
                                   // the Picard iterations each step ran (auto k_tail choice)
     int nCold, nOutLinks;
@@ -646,7 +652,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         (void)oldDepth;
         dq6 = conduitLossRate<kCold>(p, j, x, dt, &evapRate, &seepRate, ct) * 2.5 * dt * v / len0;
     } else {
-        dq6 = copysign(0.0, v);       // == 0.0 * 2.5 * dt * v / len0 (dt, len0 > 0)
+        dq6 = 0.0 * 2.5 * dt * v / len0;   // the loss rate is 0 (a non-finite v propagates, as in dwflow.c:236)
     }
 
     double denom = 1.0 + dq1 + dq5;
@@ -734,11 +740,7 @@ __device__ __forceinline__ void stageTables(double* ct, const double* g, int nGe
     __syncthreads();
 }
 
-// Streaming kernel: every conduit with LF_COLD clear (zero offsets, no outfall
-// end), one thread per conduit.  No calls, no root finders.
-// kWaves: minimum waves per SIMD the register allocator must allow (1 = no
-// constraint); selected at start-up (SWMM5_LINK_WAVES, default kLinkWavesDefault)
-// the step converged at iteration m (dynwave.c:249-251): the frozen junctions
+// The step converged at iteration m (dynwave.c:249-251): the frozen junctions
 // take their depth at that last iteration (a step that runs all MaxTrials
 // iterations does this in its last node update)
 __device__ __forceinline__ void finalizeFrozen(const Params& p, int m, int tid, int nthr)
@@ -790,21 +792,23 @@ __device__ __forceinline__ int linkListWalk(const Params& p, int k, int cnt, dou
 // end), one thread per conduit.  No calls, no root finders.
 // kWaves: minimum waves per SIMD the register allocator must allow (1 = no
 // constraint); selected at start-up (SWMM5_LINK_WAVES, default kLinkWavesDefault)
-template <bool kFirst, int kWaves, bool kFast>
+// kProbe: a separately named instantiation for swmmx_timeKernel's
+// back-to-back measurement launches (same code)
+template <bool kFirst, int kWaves, bool kFast, bool kProbe = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves)))
 void k_link(Params p, int k)
 {
     const int tid = blockIdx.x * kBlock + threadIdx.x, nthr = gridDim.x * kBlock;
-    if (k >= 2 && p.ctl->unconv[k - 1] == 0) {            // converged: dynwave.c:249-251
+    if (k >= 2 && p.unconv[k - 1] == 0) {            // converged: dynwave.c:249-251
         // the first launch after the step converged (iteration k-1 ran)
-        if (p.freeze && (k == 2 || p.ctl->unconv[k - 2] != 0)) finalizeFrozen(p, k - 1, tid, nthr);
+        if (p.freeze && (k == 2 || p.unconv[k - 2] != 0)) finalizeFrozen(p, k - 1, tid, nthr);
         return;
     }
-    if (p.nShared && blockIdx.x == 0 && threadIdx.x == 0) p.xsend[p.xflag] = 0.0;   // k_node sets it
     __shared__ double ct[kFast ? kCtFast : 5 * SWX_CIRC_N];
     double dt = p.ctl->dt;
     int work = 0;
-    if (kFirst && blockIdx.x == 0 && threadIdx.x < kMaxTrialsCap) p.ctl->ucount[threadIdx.x] = 0;
+    if (kFirst && blockIdx.x == 0)
+        for (int t = threadIdx.x; t < p.maxTrials; t += kBlock) p.ucount[t] = 0;
     if (kFirst && blockIdx.x == 0 && threadIdx.x == 0) p.ctl->tailBar = 0;
     if (kFirst || k < 2) {
         stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
@@ -815,7 +819,7 @@ void k_link(Params p, int k)
             conduitFlow<kFirst, false, kFast>(p, j, f, nn, k, dt, ct, p.nNewDepth[nn.x], p.nNewDepth[nn.y]);
         }
     } else {
-        const int cnt = p.ctl->ucount[k - 1];
+        const int cnt = p.ucount[k - 1];
         if (blockIdx.x * kBlock < 4 * cnt) {                // uniform per block
             stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
             work = linkListWalk<kFast>(p, k, cnt, dt, ct, tid, nthr);
@@ -831,7 +835,7 @@ void k_link(Params p, int k)
         if (threadIdx.x == 0) {
             int t = 0;
             for (int w = 0; w < kBlock / 64; w++) t += wsum[w];
-            if (t) atomicAdd(&p.ctl->linkWork[k], (unsigned long long)t);
+            if (t) atomicAdd(&p.work[k], (unsigned long long)t);
         }
     }
 }
@@ -925,7 +929,7 @@ __device__ __forceinline__ void coldConduits(const Params& p, int k, double dt, 
 template <bool kFirst>
 __global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
 {
-    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
+    if (k >= 2 && p.unconv[k - 1] == 0) return;
     __shared__ double ct[5 * SWX_CIRC_N];
     stageTables(ct, p.gTables);
     coldConduits<kFirst>(p, k, p.ctl->dt, ct, blockIdx.x * kBlock + threadIdx.x, gridDim.x * kBlock);
@@ -1099,7 +1103,7 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
     constexpr bool kStorage = kGeneral;
     const double dt = p.ctl->dt;
     bool anyUnconv = false;
-    int gathered = 0;
+    int gathered = 0, live = 0, fast = 0;          // measurement only (countWork)
     int* ulist = p.ulist + (size_t)(k & 1) * p.nN;
     for (int i = tid; i < p.nN; i += nthr) {
         uint32_t nf = p.nflags[i];
@@ -1108,7 +1112,7 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
         double yLast = 0.0;
         bool haveYLast = false;
         bool listMe = (type == OUTFALL);       // unconverged after this iteration
-        bool done = false;
+        bool done = false, isFast = false;
         if (!kFirst && k >= 2) {
             unsigned char cache = p.dirty[i];
             const int fz = p.frz[i];
@@ -1145,10 +1149,13 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
                         else if (p.freeze && k + 1 < p.maxTrials && freezable(p, yNew, yRaw, yMax, yCrown))
                             p.frz[i] = (unsigned char)(k + 1);
                         done = true;
+                        isFast = true;
                     }
                 }
             }
         }
+        if (!done || isFast) live++;
+        if (isFast) fast++;
         if (!done) {
         if (!haveYLast) yLast = (type == OUTFALL) ? 0.0 : p.nNewDepth[i];
         double yOld, lat;
@@ -1185,10 +1192,10 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
             bool canPond = (nf & NF_CANPOND) != 0;
             double fullDepth = p.fullDepth[i];
             surf = 0.0;
-            if (canPond && yLast > fullDepth && !(nf & NF_REPLICA)) surf = p.pondedArea[i];  // owner adds it
+            if (canPond && yLast > fullDepth) surf = p.pondedArea[i];
             inflow = 0.0;
             outflow = 0.0;                        // node losses are 0 for non-storage nodes
-            if (kStorage && type == STORAGE && !(nf & NF_REPLICA)) {
+            if (kStorage && type == STORAGE) {
                 surf = devStorageArea(p, i, yLast);
                 outflow = p.nLosses[i];
             }
@@ -1233,13 +1240,6 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
         } else if (nf & NF_DEFER) {
             // conduit sums written above; k_nc adds the non-conduit links
             // and updates the depth
-        } else if (nf & NF_SHARED) {                       // multi-GPU: partial sums out
-            int s4 = 4 * p.sharedSlot[i];
-            p.xsend[s4] = inflow;
-            p.xsend[s4 + 1] = outflow;
-            p.xsend[s4 + 2] = surf;
-            p.xsend[s4 + 3] = sumdqdh;
-            listMe = false;                                // k_node_shared lists it
         } else if (!nodeUpdate<kStorage>(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh)) {
             anyUnconv = true;
             listMe = true;
@@ -1250,27 +1250,32 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
             unsigned long long m = __ballot(listMe);
             if (m) {
                 int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1, base = 0;
-                if (lane == leader) base = atomicAdd(&p.ctl->ucount[k], __popcll(m));
+                if (lane == leader) base = atomicAdd(&p.ucount[k], __popcll(m));
                 base = __shfl(base, leader, 64);
                 if (listMe) ulist[base + __popcll(m & ((1ull << lane) - 1ull))] = i;
             }
         }
     }
     // one flag per iteration; any writer stores 1 (no atomics needed)
-    if (__any(anyUnconv) && (threadIdx.x & 63) == 0) {
-        p.ctl->unconv[k] = 1;
-        if (p.nShared) p.xsend[p.xflag] = 1.0;             // tell the other ranks
-    }
+    if (__any(anyUnconv) && (threadIdx.x & 63) == 0) p.unconv[k] = 1;   // all-reduced over the ranks
     if (!kFirst && k >= 2 && p.countWork) {                // measurement only
-        for (int off = 32; off > 0; off >>= 1) gathered += __shfl_down(gathered, off, 64);
-        if ((threadIdx.x & 63) == 0 && gathered) atomicAdd(&p.ctl->nodeWork[k], (unsigned long long)gathered);
+        for (int off = 32; off > 0; off >>= 1) {
+            gathered += __shfl_down(gathered, off, 64);
+            live += __shfl_down(live, off, 64);
+            fast += __shfl_down(fast, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            if (gathered) atomicAdd(&p.work[p.maxTrials + k], (unsigned long long)gathered);
+            if (live) atomicAdd(&p.work[2 * p.maxTrials + k], (unsigned long long)live);
+            if (fast) atomicAdd(&p.work[3 * p.maxTrials + k], (unsigned long long)fast);
+        }
     }
 }
 
-template <bool kFirst, bool kGeneral>
+template <bool kFirst, bool kGeneral, bool kProbe = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral ? 3 : 4))) void k_node(Params p, int k)
 {
-    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
+    if (k >= 2 && p.unconv[k - 1] == 0) return;
     // prologue: outfall depths (link_setOutfallDepth, findNodeDepths
     // dynwave.c:605) from this iteration's link flows.  Only the outfall's
     // single link reads that depth (next iteration), and this kernel never
@@ -1345,13 +1350,13 @@ __global__ __launch_bounds__(kBlock) void k_tail(Params p)
     unsigned arrivals = 0;
     for (int k = 2; k < p.maxTrials; k++) {
         // dynwave.c:249-251: iteration k-1 converged -- the step is done
-        if (__hip_atomic_load(&p.ctl->unconv[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        if (__hip_atomic_load(&p.unconv[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
             if (p.freeze) finalizeFrozen(p, k - 1, tid, nthr);
             return;
         }
         if (k == 2) stageTables(ct, p.gTables, kFast ? p.nGeom : 0);   // only when an iteration runs
         coldConduits<false>(p, k, dt, ct, tid, nthr);
-        const int cnt = __hip_atomic_load(&p.ctl->ucount[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int cnt = __hip_atomic_load(&p.ucount[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         (void)linkListWalk<kFast>(p, k, cnt, dt, ct, tid, nthr);
         arrivals += gridDim.x;
         if (!tailBarrier(p, arrivals)) return;
@@ -1364,40 +1369,57 @@ __global__ __launch_bounds__(kBlock) void k_tail(Params p)
     }
 }
 
-// Multi-GPU: shared nodes after the all-reduce of their partial sums.  Every
-// replica applies the same update to the same sums (identical results on all
-// ranks), and an unconverged interior node on any rank marks the iteration.
-template <bool kStorage>
-__global__ __launch_bounds__(kBlock) void k_node_shared(Params p, int k)
+// Multi-GPU neighbour exchange (partition.h).  k_xpack: the owned links
+// other ranks hold as ghosts, {newFlow, surfArea1, surfArea2, dqdh (, evap,
+// seep)} each, into the send buffer (neighbour-major, the receiver's ghost
+// order); k_xunpack: the received values into this rank's ghost slots.  The
+// node update then sums every held node over all its links in global link
+// order, exactly as on one GPU.  An iteration after convergence moves nothing.
+__global__ __launch_bounds__(kBlock) void k_xpack(Params p, int k)
 {
-    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
-    const double dt = p.ctl->dt;
-    bool anyUnconv = false;
-    for (int s = blockIdx.x * kBlock + threadIdx.x; s < p.nShared; s += gridDim.x * kBlock) {
-        int i = p.sharedList[s];
-        int s4 = 4 * p.sharedSlot[i];
-        uint32_t nf = p.nflags[i];
-        double inflow = p.xrecv[s4], outflow = p.xrecv[s4 + 1];
-        double surf = p.xrecv[s4 + 2], sumdqdh = p.xrecv[s4 + 3];
-        p.inflow[i] = inflow;
-        p.outflow[i] = outflow;
-        if ((int)(nf & NF_TYPE) == OUTFALL) continue;
-        double yLast = p.nNewDepth[i], yOld = p.nOldDepth[i];
-        bool listMe = false;
-        if (!nodeUpdate<kStorage>(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh)) {
-            anyUnconv = true;
-            listMe = true;
-        }
-        unsigned long long m = __ballot(listMe);          // next k_link's work list
-        if (m) {
-            int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1, base = 0;
-            if (lane == leader) base = atomicAdd(&p.ctl->ucount[k], __popcll(m));
-            base = __shfl(base, leader, 64);
-            if (listMe) p.ulist[(size_t)(k & 1) * p.nN + base + __popcll(m & ((1ull << lane) - 1ull))] = i;
+    if (k >= 2 && p.unconv[k - 1] == 0) return;
+    for (int e = blockIdx.x * kBlock + threadIdx.x; e < p.nSend; e += gridDim.x * kBlock) {
+        const int l = p.sendLink[e];
+        double* o = p.xsend + (size_t)p.xF * e;
+        o[0] = p.lNewFlow[l];
+        o[1] = p.sa1[l];
+        o[2] = p.sa2[l];
+        o[3] = p.dqdh[l];
+        if (p.xF > 4) {
+            o[4] = p.evapLoss[l];
+            o[5] = p.seepLoss[l];
         }
     }
-    if (__any(anyUnconv) && (threadIdx.x & 63) == 0) p.ctl->unconv[k] = 1;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && p.xrecv[p.xflag] > 0.0) p.ctl->unconv[k] = 1;
+}
+__global__ __launch_bounds__(kBlock) void k_xunpack(Params p, int k)
+{
+    if (k >= 2 && p.unconv[k - 1] == 0) return;
+    for (int g = blockIdx.x * kBlock + threadIdx.x; g < p.nGhost; g += gridDim.x * kBlock) {
+        const int l = p.nL + g;
+        const double* v = p.xrecv + (size_t)p.xF * g;
+        p.lNewFlow[l] = v[0];
+        p.sa1[l] = v[1];
+        p.sa2[l] = v[2];
+        p.dqdh[l] = v[3];
+        if (p.xF > 4) {
+            p.evapLoss[l] = v[4];
+            p.seepLoss[l] = v[5];
+        }
+    }
+}
+// once per step, before the node quality: the ghost links' concentrations
+// (the owners' qualLink of the previous step end), P values each
+__global__ __launch_bounds__(kBlock) void k_xpack_qual(Params p)
+{
+    for (int e = blockIdx.x * kBlock + threadIdx.x; e < p.nSend; e += gridDim.x * kBlock)
+        for (int q = 0; q < p.P; q++)
+            p.xsend[(size_t)p.P * e + q] = p.lNewQual[(size_t)q * p.nLs + p.sendLink[e]];
+}
+__global__ __launch_bounds__(kBlock) void k_xunpack_qual(Params p)
+{
+    for (int g = blockIdx.x * kBlock + threadIdx.x; g < p.nGhost; g += gridDim.x * kBlock)
+        for (int q = 0; q < p.P; q++)
+            p.lNewQual[(size_t)q * p.nLs + p.nL + g] = p.xrecv[(size_t)p.P * g + q];
 }
 
 // ---------------------------------------------------------------------------
@@ -1418,7 +1440,7 @@ __device__ __forceinline__ double ncDepth(const Params& p, int n)
 template <bool kFirst>
 __global__ __launch_bounds__(kBlock) void k_nc(Params p, int k)
 {
-    if (k >= 2 && p.ctl->unconv[k - 1] == 0) return;
+    if (k >= 2 && p.unconv[k - 1] == 0) return;
     __shared__ double ct[5 * SWX_CIRC_N];
     __shared__ int anyU;
     stageTables(ct, p.gTables);
@@ -1582,7 +1604,7 @@ __global__ __launch_bounds__(kBlock) void k_nc(Params p, int k)
             unsigned long long m = __ballot(listMe);
             if (m) {
                 int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1, b = 0;
-                if (lane == leader) b = atomicAdd(&p.ctl->ucount[k], __popcll(m));
+                if (lane == leader) b = atomicAdd(&p.ucount[k], __popcll(m));
                 b = __shfl(b, leader, 64);
                 if (listMe) ulist[b + __popcll(m & ((1ull << lane) - 1ull))] = p.defNodes[d];
             }
@@ -1590,7 +1612,7 @@ __global__ __launch_bounds__(kBlock) void k_nc(Params p, int k)
     }
     if (anyUnconv) anyU = 1;
     __syncthreads();
-    if (threadIdx.x == 0 && anyU) p.ctl->unconv[k] = 1;
+    if (threadIdx.x == 0 && anyU) p.unconv[k] = 1;
 }
 
 // qualrout.c:146-174, 498-518
@@ -1646,7 +1668,7 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
             bool down = isN2 ? !(ql < 0.0) : (ql < 0.0);
             if (down) {
                 const double aq = fabs(ql);
-                for (int b = 0; b < np; b++) wq[b] += aq * p.lNewQual[(size_t)(p0 + b) * p.nL + l];
+                for (int b = 0; b < np; b++) wq[b] += aq * p.lNewQual[(size_t)(p0 + b) * p.nLs + l];
             }
         }
         for (int b = 0; b < np; b++) {
@@ -1682,7 +1704,7 @@ __device__ __forceinline__ void qualLink(const Params& p, int j, uint32_t f, dou
         int up = (nf < 0.0) ? nn.y : nn.x;
         if (f & LF_NC) {                      // non-conduit: upstream node's quality (qualrout.c:283-291)
             for (int pp = 0; pp < p.P; pp++) {
-                size_t li = (size_t)pp * p.nL + j;
+                size_t li = (size_t)pp * p.nLs + j;
                 p.lOldQual[li] = p.lNewQual[li];
                 p.lNewQual[li] = p.nNewQual[(size_t)pp * p.nN + up];
             }
@@ -1700,7 +1722,7 @@ __device__ __forceinline__ void qualLink(const Params& p, int j, uint32_t f, dou
         qIn = gmax(qIn, 0.0);
         bool dry = (v2 < 0.0353147 || p.lNewDepth[j] <= 0.003281);
         for (int pp = 0; pp < p.P; pp++) {
-            size_t li = (size_t)pp * p.nL + j;
+            size_t li = (size_t)pp * p.nLs + j;
             double c1 = p.lNewQual[li];
             p.lOldQual[li] = c1;
             c1 *= fEvap;
@@ -1786,8 +1808,8 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
     if (p.maxTrials <= 1) converged = false;
     else {
         steps = 2;
-        while (steps < p.maxTrials && c->unconv[steps - 1]) steps++;
-        converged = (c->unconv[steps - 1] == 0);
+        while (steps < p.maxTrials && p.unconv[steps - 1]) steps++;
+        converged = (p.unconv[steps - 1] == 0);
     }
     const StatsDev& S = p.st;
     int n = gridDim.x * kBlock;
@@ -2059,14 +2081,13 @@ __global__ void k_finalize(Params p)
     if (p.maxTrials <= 1) { steps = p.maxTrials < 1 ? 0 : 1; converged = false; }
     else {
         steps = 2;
-        while (steps < p.maxTrials && c->unconv[steps - 1]) steps++;
-        converged = (c->unconv[steps - 1] == 0);
+        while (steps < p.maxTrials && p.unconv[steps - 1]) steps++;
+        converged = (p.unconv[steps - 1] == 0);
     }
     c->lastSteps = steps;
     c->totalSteps += 1;
     c->totalIters += steps;
     if (!converged) c->nonConverge += 1;
-    for (int k = 0; k < kMaxTrialsCap; k++) c->unconv[k] = 0;
     // mass balance: massbal_updateRoutingTotals(dt/2) at both ends of the step
     double half = c->dt / 2.;
     double step[kNumPartials] = {c->latTot[0], c->latTot[1] + tot[2], tot[1], c->latTot[2] + tot[0],
@@ -2124,9 +2145,16 @@ __global__ void k_finalize(Params p)
     // without a copy command in the step (totalSteps = index of that step)
     p.hostDt[c->totalSteps % kDtRing] = dtn;
     p.hostDt[kDtRing + (c->totalSteps - 1) % kDtRing] = (double)steps;   // Picard iterations of this step
+    // a k_tail grid barrier that timed out (never expected: its workgroups
+    // are co-resident by construction) is reported to the host at once
+    p.hostDt[2 * kDtRing] = (double)c->tailErr;
     __threadfence_system();
     }
+    if (c->tailErr)                                // leave no junction frozen in a failed step
+        for (int i = t; i < p.nN; i += kBlock) p.frz[i] = 0;
     __syncthreads();
+    if (kPhase != 1)                               // the next step's convergence flags
+        for (int k = t; k < p.maxTrials; k += kBlock) p.unconv[k] = 0;
     unsigned long long* g = (unsigned long long*)p.ctl;
     for (int w = t; w < nw; w += kBlock) g[w] = cw[w];
 }
@@ -2198,7 +2226,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_results(Params p, double f, dou
         x[3] = (float)v;
         x[4] = (float)c;
         for (int qq = 0; qq < p.P; qq++) {
-            size_t k = (size_t)qq * p.nL + j;
+            size_t k = (size_t)qq * p.nLs + j;
             c = f1 * p.lOldQual[k] + f * p.lNewQual[k];
             x[5 + qq] = (float)c;
         }
@@ -2214,11 +2242,13 @@ struct Router::Impl {
     hipStream_t side = nullptr;      // fork/join branch for the cold conduits
     Partition part;                  // this rank's part of the network (whole net on one GPU)
     ncclComm_t comm = nullptr;       // RCCL communicator (multi-GPU, RCCL transport)
-    int gridS = 1;                   // k_node_shared grid
+    int gridX = 1;                   // k_xpack / k_xunpack grid
     double* hostX = nullptr;         // host staging for the test transport
+    std::vector<double> slotBuf;     // host transport: global ghost-slot buffer
+    std::string xerrMsg;             // last failed collective / transfer
     float *resN = nullptr, *resL = nullptr;          // packed period results (device)
     float *resNHost = nullptr, *resLHost = nullptr;  // pinned copies
-    hipEvent_t forkEv[kMaxTrialsCap] = {}, joinEv[kMaxTrialsCap] = {};
+    std::vector<hipEvent_t> forkEv, joinEv;   // per Picard iteration (cold-conduit fork / join)
     hipGraphExec_t graph = nullptr;
     // step graph whose iterations k >= 2 run in k_tail (Router::step picks
     // it or the unrolled graph: SWMM5_TAIL = 0 never, 1 always, else auto)
@@ -2250,15 +2280,25 @@ struct Router::Impl {
     int tUsed = 0;
     hipEvent_t* curEv = nullptr;     // event set of the step being launched
     hipEvent_t* curHot = nullptr;
-    static constexpr int kClasses = 5;
+    // kernel classes: 0 k_link<first>, 1 k_node<first>, 2 step end (k_step_end +
+    // k_finalize), 3 quality, 4 k_link iterations >= 1, 5 k_node iteration 1,
+    // 6 k_node iterations >= 2
+    static constexpr int kClasses = 7;
     double kms[kClasses] = {};
     long long kcnt[kClasses] = {};
     double kbytes[kClasses] = {};     // byte model per launch (class 4: per updated conduit)
     double kbytesSum[kClasses] = {};  // algorithmic bytes of the timed launches
-    double nodeFix = 0, nodeGather = 0;   // node byte model at iterations >= 2
+    // node byte model: iteration 1 per launch; iterations >= 2 per scanned node,
+    // per relaxation-only update, per full update and per gathering node
+    double nodeIter1 = 0, nodeScan = 0, nodeFastB = 0, nodeUpdB = 0, nodeGather = 0;
     double gatherSum = 0, gatherCnt = 0;  // nodes gathered at iterations >= 2
     double nHot = 0, nColdD = 0;
     double workSum = 0;               // conduits updated in timed iterations >= 1
+    // per Picard iteration k of the timed steps: [0] launches, [1] conduits
+    // updated, [2] nodes gathered, [3] nodes updated (not frozen), [4]
+    // relaxation-only node updates, [5] k_link ms, [6] k_node ms
+    static constexpr int kIterCols = 7;
+    std::vector<double> iterStats;
     int nE = 0;
     bool tableShapes = true;
     static constexpr int kRing = kDtRing;
@@ -2293,10 +2333,8 @@ Router::~Router()
         if (d_->comm) (void)ncclCommDestroy(d_->comm);
         for (auto e : d_->clockEv) if (e) (void)hipEventDestroy(e);
         for (auto e : d_->ringEv) if (e) (void)hipEventDestroy(e);
-        for (int k = 0; k < kMaxTrialsCap; k++) {
-            if (d_->forkEv[k]) (void)hipEventDestroy(d_->forkEv[k]);
-            if (d_->joinEv[k]) (void)hipEventDestroy(d_->joinEv[k]);
-        }
+        for (auto e : d_->forkEv) if (e) (void)hipEventDestroy(e);
+        for (auto e : d_->joinEv) if (e) (void)hipEventDestroy(e);
         if (d_->side) (void)hipStreamDestroy(d_->side);
         if (d_->stream) (void)hipStreamDestroy(d_->stream);
         delete d_;
@@ -2338,6 +2376,132 @@ static LinkKernelFn nodeKernel(bool first, bool storage)
     return first ? k_node<true, false> : k_node<false, false>;
 }
 
+// ---- multi-GPU collectives ------------------------------------------------
+// Every call returns 0 or 500 with d->xerrMsg set.  On the RCCL transport the
+// calls are enqueued on the routing stream (captured into the step graph at
+// init, where a failing call fails Router::init); the host transport (tests:
+// gloo through a callback) runs them synchronously.
+static int xfail(Router::Impl* d, const std::string& what)
+{
+    d->xerrMsg = what;
+    return 500;
+}
+static int ncclCheck(Router::Impl* d, ncclResult_t r, const char* what)
+{
+    if (r == ncclSuccess) return 0;
+    return xfail(d, std::string(what) + ": " + ncclGetErrorString(r));
+}
+static int hipCheckX(Router::Impl* d, hipError_t e, const char* what)
+{
+    if (e == hipSuccess) return 0;
+    return xfail(d, std::string(what) + ": " + hipGetErrorString(e));
+}
+// host transport: in-place reduction of n doubles over the ranks
+static int hostReduce(Router::Impl* d, double* buf, long n, int op)
+{
+    if (!d->part.xchg) return xfail(d, "host exchange callback missing");
+    if (d->part.xchg(buf, n, op, d->part.xuser)) return xfail(d, "host exchange callback failed");
+    return 0;
+}
+
+// In-place all-reduce of n doubles (op 0 sum, 1 min) -- the Courant limits.
+static int exchange(Router::Impl* d, const double* send, double* recv, size_t n, int op)
+{
+    if (d->part.transport == XCHG_RCCL)
+        return ncclCheck(d, ncclAllReduce(send, recv, n, ncclDouble, op ? ncclMin : ncclSum, d->comm, d->stream),
+                         "ncclAllReduce");
+    if (int r = hipCheckX(d, hipMemcpyAsync(d->hostX, send, n * sizeof(double), hipMemcpyDeviceToHost, d->stream),
+                          "exchange D2H")) return r;
+    if (int r = hipCheckX(d, hipStreamSynchronize(d->stream), "exchange sync")) return r;
+    if (int r = hostReduce(d, d->hostX, (long)n, op)) return r;
+    return hipCheckX(d, hipMemcpyAsync(recv, d->hostX, n * sizeof(double), hipMemcpyHostToDevice, d->stream),
+                     "exchange H2D");
+}
+
+// Neighbour exchange of f doubles per link: xsend (packed, neighbour-major)
+// to the ranks holding them as ghosts, xrecv (ghost order) from them.  RCCL:
+// one grouped ncclSend / ncclRecv per neighbour (strip neighbours for the
+// grids), no collective.  Host transport: every sent link has one global
+// slot; each rank writes its links' slots and a sum over the ranks leaves
+// every slot holding its owner's values exactly (x + 0.0 == x; a -0.0 becomes
+// +0.0, which no node sum can tell apart).
+static int neighbourExchange(Router::Impl* d, int f)
+{
+    const Partition& part = d->part;
+    const Params& p = d->p;
+    if (part.transport == XCHG_RCCL) {
+        if (int r = ncclCheck(d, ncclGroupStart(), "ncclGroupStart")) return r;
+        for (size_t k = 0; k < part.nbr.size(); k++) {
+            const int ns = part.sendOff[k + 1] - part.sendOff[k], nr = part.recvOff[k + 1] - part.recvOff[k];
+            if (ns > 0 && ncclCheck(d, ncclSend(p.xsend + (size_t)f * part.sendOff[k], (size_t)f * ns, ncclDouble,
+                                                part.nbr[k], d->comm, d->stream), "ncclSend")) {
+                (void)ncclGroupEnd();
+                return 500;
+            }
+            if (nr > 0 && ncclCheck(d, ncclRecv(p.xrecv + (size_t)f * part.recvOff[k], (size_t)f * nr, ncclDouble,
+                                                part.nbr[k], d->comm, d->stream), "ncclRecv")) {
+                (void)ncclGroupEnd();
+                return 500;
+            }
+        }
+        return ncclCheck(d, ncclGroupEnd(), "ncclGroupEnd");
+    }
+    const size_t ns = part.sendLink.size(), ng = part.lghost.size(), slots = (size_t)f * part.nSlotGlobal;
+    std::vector<double>& g = d->slotBuf;
+    g.assign(slots, 0.0);
+    if (ns) {
+        if (int r = hipCheckX(d, hipMemcpyAsync(d->hostX, p.xsend, (size_t)f * ns * sizeof(double),
+                                                hipMemcpyDeviceToHost, d->stream), "neighbour D2H")) return r;
+        if (int r = hipCheckX(d, hipStreamSynchronize(d->stream), "neighbour sync")) return r;
+        for (size_t e = 0; e < ns; e++)
+            for (int q = 0; q < f; q++) g[(size_t)f * part.sendSlot[e] + q] = d->hostX[(size_t)f * e + q];
+    }
+    if (slots && hostReduce(d, g.data(), (long)slots, 0)) return 500;
+    if (ng) {
+        for (size_t e = 0; e < ng; e++)
+            for (int q = 0; q < f; q++) d->hostX[(size_t)f * e + q] = g[(size_t)f * part.recvSlot[e] + q];
+        if (int r = hipCheckX(d, hipMemcpyAsync(p.xrecv, d->hostX, (size_t)f * ng * sizeof(double),
+                                                hipMemcpyHostToDevice, d->stream), "neighbour H2D")) return r;
+        if (int r = hipCheckX(d, hipStreamSynchronize(d->stream), "neighbour sync")) return r;
+    }
+    return 0;
+}
+
+// Iteration k's "some node did not converge" flag, max over the ranks (in
+// place in the per-iteration flags), so every rank runs the same iterations.
+static int flagExchange(Router::Impl* d, int k)
+{
+    int* flag = d->p.unconv + k;
+    if (d->part.transport == XCHG_RCCL)
+        return ncclCheck(d, ncclAllReduce(flag, flag, 1, ncclInt32, ncclMax, d->comm, d->stream), "ncclAllReduce");
+    int v = 0;
+    if (int r = hipCheckX(d, hipMemcpyAsync(&v, flag, sizeof(int), hipMemcpyDeviceToHost, d->stream), "flag D2H"))
+        return r;
+    if (int r = hipCheckX(d, hipStreamSynchronize(d->stream), "flag sync")) return r;
+    double x = v ? 1.0 : 0.0;
+    if (int r = hostReduce(d, &x, 1, 0)) return r;
+    v = x > 0.0 ? 1 : 0;
+    if (int r = hipCheckX(d, hipMemcpyAsync(flag, &v, sizeof(int), hipMemcpyHostToDevice, d->stream), "flag H2D"))
+        return r;
+    return hipCheckX(d, hipStreamSynchronize(d->stream), "flag sync");
+}
+
+// Timing mode (eager launches, Router::setTiming): the link and node kernels
+// of iteration k, the quality kernel and the step-end pair are launched with
+// hipExtLaunchKernelGGL, whose start/stop events carry the kernels' own
+// execution timestamps (the durations rocprofv3's kernel trace reports), not
+// the dispatch gaps around them.  Events per step: [4k] / hot[k] k_link(k),
+// [4k+1] / [4k+2] k_node(k), [base] / [base+1] quality, [base+2] / [base+3]
+// k_step_end .. k_finalize (base = 4 MaxTrials).
+template <typename F, typename... A>
+static void launchTimed(Router::Impl* d, F kernel, dim3 grid, hipEvent_t start, hipEvent_t stop, A... args)
+{
+    if (d->timing)
+        hipExtLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, d->stream, start, stop, 0, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, d->stream, args...);
+}
+
 // One Picard iteration k.  Conduits with an invert offset (k_link_cold) run on
 // a side stream, concurrently with the streaming kernel, and are joined before
 // the node update; without such conduits the iteration is two kernels on one
@@ -2345,25 +2509,12 @@ static LinkKernelFn nodeKernel(bool first, bool storage)
 // cold work it would hide):
 //   main:  [fork k] k_link(k) ─wait join k─ k_node(k)
 //   side:  wait fork k ─ k_link_cold(k) ─[join k]
-// In-place all-reduce of n doubles across the ranks (op 0 sum, 1 min):
-// ncclAllReduce on the routing stream (graph-capturable), or, for the test
-// transport, a synchronous round trip through the host callback.
-static void exchange(Router::Impl* d, const double* send, double* recv, size_t n, int op)
-{
-    if (d->part.transport == XCHG_RCCL) {
-        (void)ncclAllReduce(send, recv, n, ncclDouble, op ? ncclMin : ncclSum, d->comm, d->stream);
-        return;
-    }
-    (void)hipMemcpyAsync(d->hostX, send, n * sizeof(double), hipMemcpyDeviceToHost, d->stream);
-    (void)hipStreamSynchronize(d->stream);
-    if (d->part.xchg) d->part.xchg(d->hostX, (long)n, op, d->part.xuser);
-    (void)hipMemcpyAsync(recv, d->hostX, n * sizeof(double), hipMemcpyHostToDevice, d->stream);
-}
-
-static void launchIteration(Router::Impl* d, int k)
+// Multi-GPU: k_link ─ k_xpack ─ neighbour send/recv ─ k_xunpack ─ k_node ─
+// [k_nc] ─ all-reduce(max) of the iteration's convergence flag.
+static int launchIteration(Router::Impl* d, int k)
 {
     Params& p = d->p;
-    if (d->timing) (void)hipEventRecord(d->curEv[4 * k], d->stream);
+    const bool multi = d->part.active();
     if (p.nCold) {
         (void)hipEventRecord(d->forkEv[k], d->stream);
         (void)hipStreamWaitEvent(d->side, d->forkEv[k], 0);
@@ -2373,21 +2524,23 @@ static void launchIteration(Router::Impl* d, int k)
             hipLaunchKernelGGL(k_link_cold<false>, dim3(d->gridC), dim3(kBlock), 0, d->side, p, k);
         (void)hipEventRecord(d->joinEv[k], d->side);
     }
-    hipLaunchKernelGGL(linkKernel(k == 0, d->linkWaves, d->fastLinks), dim3(d->gridL), dim3(kBlock), 0, d->stream, p, k);
-    if (d->timing) (void)hipEventRecord(d->curHot[k], d->stream);
+    hipEvent_t e0 = d->timing ? d->curEv[4 * k] : nullptr, e1 = d->timing ? d->curHot[k] : nullptr;
+    launchTimed(d, linkKernel(k == 0, d->linkWaves, d->fastLinks), dim3(d->gridL), e0, e1, p, k);
     if (p.nCold) (void)hipStreamWaitEvent(d->stream, d->joinEv[k], 0);
-    if (d->timing) (void)hipEventRecord(d->curEv[4 * k + 1], d->stream);
-    hipLaunchKernelGGL(nodeKernel(k == 0, d->general), dim3(d->gridN), dim3(kBlock), 0, d->stream, p, k);
-    if (d->part.active()) {                        // interface sums + convergence flag
-        exchange(d, p.xsend, p.xrecv, (size_t)p.xflag + 1, 0);
-        hipLaunchKernelGGL(d->general ? k_node_shared<true> : k_node_shared<false>, dim3(d->gridS),
-                           dim3(kBlock), 0, d->stream, p, k);
+    if (multi) {                                   // ghost links' values from their owners
+        if (p.nSend) hipLaunchKernelGGL(k_xpack, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
+        if (int r = neighbourExchange(d, p.xF)) return r;
+        if (p.nGhost) hipLaunchKernelGGL(k_xunpack, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
     }
+    e0 = d->timing ? d->curEv[4 * k + 1] : nullptr;
+    e1 = d->timing ? d->curEv[4 * k + 2] : nullptr;
+    launchTimed(d, nodeKernel(k == 0, d->general), dim3(d->gridN), e0, e1, p, k);
     if (p.nNC > 0) {                               // pumps / regulators, their end nodes
         if (k == 0) hipLaunchKernelGGL(k_nc<true>, dim3(1), dim3(kBlock), 0, d->stream, p, k);
         else hipLaunchKernelGGL(k_nc<false>, dim3(1), dim3(kBlock), 0, d->stream, p, k);
     }
-    if (d->timing) (void)hipEventRecord(d->curEv[4 * k + 2], d->stream);
+    if (multi) return flagExchange(d, k);
+    return 0;
 }
 
 typedef void (*TailFn)(Params);
@@ -2398,30 +2551,38 @@ static TailFn tailKernel(bool fast, bool general)
 }
 
 // tail: iterations k >= 2 in one k_tail launch (d->tailGrid > 0 only)
-static void launchStep(Router::Impl* d, bool tail = false)
+static int launchStep(Router::Impl* d, bool tail = false)
 {
     Params& p = d->p;
+    const bool multi = d->part.active();
     if (tail) {
-        launchIteration(d, 0);
-        launchIteration(d, 1);
+        for (int k = 0; k < 2; k++)
+            if (int r = launchIteration(d, k)) return r;
         hipLaunchKernelGGL(tailKernel(d->fastLinks, d->general), dim3(d->tailGrid), dim3(kBlock), 0, d->stream, p);
     } else {
-        for (int k = 0; k < p.maxTrials; k++) launchIteration(d, k);
+        for (int k = 0; k < p.maxTrials; k++)
+            if (int r = launchIteration(d, k)) return r;
     }
-    int base = 4 * p.maxTrials;
-    if (d->timing) (void)hipEventRecord(d->curEv[base], d->stream);
-    if (p.P > 0)                                   // the link part runs in k_step_end
-        hipLaunchKernelGGL(k_qual_node, dim3(d->gridN), dim3(kBlock), 0, d->stream, p);
-    if (d->timing) (void)hipEventRecord(d->curEv[base + 1], d->stream);
-    hipLaunchKernelGGL(stepEndKernel(d->fastLinks, d->allShapes), dim3(d->gridEnd), dim3(kBlock), 0, d->stream, p);
-    if (d->part.active() && p.varStep) {           // global Courant limits (min over ranks)
+    const int base = 4 * p.maxTrials;
+    hipEvent_t* ev = d->timing ? d->curEv : nullptr;
+    if (p.P > 0) {                                 // the link part runs in k_step_end
+        if (multi) {                               // ghost links' concentrations (previous step end)
+            if (p.nSend) hipLaunchKernelGGL(k_xpack_qual, dim3(d->gridX), dim3(kBlock), 0, d->stream, p);
+            if (int r = neighbourExchange(d, p.P)) return r;
+            if (p.nGhost) hipLaunchKernelGGL(k_xunpack_qual, dim3(d->gridX), dim3(kBlock), 0, d->stream, p);
+        }
+        launchTimed(d, k_qual_node, dim3(d->gridN), ev ? ev[base] : nullptr, ev ? ev[base + 1] : nullptr, p);
+    }
+    launchTimed(d, stepEndKernel(d->fastLinks, d->allShapes), dim3(d->gridEnd), ev ? ev[base + 2] : nullptr,
+                (hipEvent_t) nullptr, p);
+    if (multi && p.varStep) {                      // global Courant limits (min over ranks)
         hipLaunchKernelGGL(k_finalize<1>, dim3(1), dim3(kBlock), 0, d->stream, p);
-        exchange(d, &p.ctl->stepRed[5], &p.ctl->stepRed[5], 2, 1);
-        hipLaunchKernelGGL(k_finalize<2>, dim3(1), dim3(kBlock), 0, d->stream, p);
+        if (int r = exchange(d, &p.ctl->stepRed[5], &p.ctl->stepRed[5], 2, 1)) return r;
+        launchTimed(d, k_finalize<2>, dim3(1), (hipEvent_t) nullptr, ev ? ev[base + 3] : nullptr, p);
     } else {
-        hipLaunchKernelGGL(k_finalize<0>, dim3(1), dim3(kBlock), 0, d->stream, p);
+        launchTimed(d, k_finalize<0>, dim3(1), (hipEvent_t) nullptr, ev ? ev[base + 3] : nullptr, p);
     }
-    if (d->timing) (void)hipEventRecord(d->curEv[base + 2], d->stream);
+    return 0;
 }
 
 int Router::init(Project& prj, int device, const Partition* partIn)
@@ -2439,9 +2600,12 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (buildPartition(net, d->part, &m)) { fail(m); return err_; }
     }
     const Partition& part = d->part;
-    const std::vector<int>& LL = part.llink;
+    // local links: this rank's owned links, then its ghost links (other
+    // ranks' links touching a held node; values received every iteration)
+    std::vector<int> LL = part.llink;
+    LL.insert(LL.end(), part.lghost.begin(), part.lghost.end());
     const std::vector<int>& LN = part.lnode;
-    if (part.active() && P > 0) { fail("water quality is not yet supported with more than one GPU"); return err_; }
+    const int nOwn = (int)part.llink.size();
     nN = (int)LN.size();
     nL = (int)LL.size();
     auto gl = [&](const std::vector<double>& v) {
@@ -2478,17 +2642,18 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     devName_ = std::string("hip:") + prop.gcnArchName + ":" + prop.name;
     HIPCHECK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking));
-    for (int k = 0; k < kMaxTrialsCap; k++) {
-        HIPCHECK(hipEventCreateWithFlags(&d->forkEv[k], hipEventDisableTiming));
-        HIPCHECK(hipEventCreateWithFlags(&d->joinEv[k], hipEventDisableTiming));
+    {
+        const int m = std::max(prj.opt.maxTrials, 1);
+        d->forkEv.assign(m, nullptr);
+        d->joinEv.assign(m, nullptr);
+        for (int k = 0; k < m; k++) {
+            HIPCHECK(hipEventCreateWithFlags(&d->forkEv[k], hipEventDisableTiming));
+            HIPCHECK(hipEventCreateWithFlags(&d->joinEv[k], hipEventDisableTiming));
+        }
     }
 
     Params& p = d->p;
-    p.nN = nN; p.nL = nL; p.P = P;
-    if (prj.opt.maxTrials > kMaxTrialsCap) {        // one flag per iteration in StepCtl
-        fail("MAX_TRIALS above " + std::to_string(kMaxTrialsCap) + " is not supported");
-        return err_;
-    }
+    p.nN = nN; p.nL = nOwn; p.nLs = nL; p.P = P;
     p.maxTrials = prj.opt.maxTrials;
     p.surchargeMethod = prj.opt.surchargeMethod;
     p.forceMainEqn = prj.opt.forceMainEqn;
@@ -2523,10 +2688,6 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     std::vector<int> lflags(nL), coldLinks, outLinks;
     std::vector<double> inv1(nL), inv2(nL), xd[11];
     for (auto& v : xd) v.resize(nL);
-    if (net.nNC > 0 && part.active()) {
-        fail("pumps / regulators are not yet supported with more than one GPU");
-        return err_;
-    }
     for (int jj = 0; jj < gL; jj++)
         if (net.linkType[jj] == CONDUIT && net.xsect[jj].type == X_DUMMY) {
             fail("dummy conduits are not supported yet");
@@ -2549,7 +2710,9 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (net.seepRate[g] > 0.0 || (prj.opt.evapRate > 0.0 && isOpen(x.type))) f |= LF_SEEP;
         if (net.qLimit[g] > 0.0) f |= LF_QLIMIT;
         if (net.direction[g] < 0) f |= LF_DIRNEG;
-        if (net.linkType[g] != CONDUIT) {
+        if (j >= nOwn) {
+            f |= LF_COLD;                           // ghost: computed by its owner, never here
+        } else if (net.linkType[g] != CONDUIT) {
             f |= LF_NC | LF_COLD;                   // k_nc, not the conduit kernels
             if (net.linkType[g] == PUMP) f |= LF_PUMP;
         } else if (net.offset1[g] > 0.0 || net.offset2[g] > 0.0 || !isBasicShape(x.type) ||
@@ -2668,7 +2831,6 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     // ---- node static ------------------------------------------------------
     std::vector<int> nflags(nN), outLink(nN, -1);
     std::vector<double> yCrown(nN);
-    std::vector<int> sharedNodes;
     for (int i = 0; i < nN; i++) {
         const int g = LN[i];                        // global node index
         uint32_t f = (uint32_t)net.nodeType[g] & NF_TYPE;
@@ -2676,7 +2838,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (net.degree[g] < 0) f |= NF_DEGNEG;
         if (prj.opt.allowPonding && net.pondedArea[g] > 0.0) f |= NF_CANPOND;
         if (net.degree[g] == 0) f |= NF_DEG0;
-        if (part.sharedSlot[i] >= 0) { f |= NF_SHARED; sharedNodes.push_back(i); }
+        if (part.hasGhost[i]) f |= NF_SHARED;      // sums include received ghost values
         if (!part.owned[i]) f |= NF_REPLICA;
         nflags[i] = (int)f;
         yCrown[i] = net.crownElev[g] - net.invertElev[g];
@@ -2711,29 +2873,12 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     // Pumps / regulators are not in it: their flows join the node sums after
     // all conduits (dynwave.c:398-412), in k_nc.  The quality CSR keeps every
     // link in link order (findLinkMassFlow, qualrout.c:111).
-    auto buildCsr = [&](bool all, std::vector<int>& rowptr, std::vector<int>& csr) {
-        rowptr.assign(nN + 1, 0);
-        for (int j = 0; j < nL; j++) {
-            if (!all && (lflags[j] & LF_NC)) continue;
-            rowptr[nodes2[2 * j] + 1]++;
-            rowptr[nodes2[2 * j + 1] + 1]++;
-        }
-        for (int i = 0; i < nN; i++) rowptr[i + 1] += rowptr[i];
-        csr.resize(rowptr[nN]);
-        std::vector<int> fillp(rowptr.begin(), rowptr.end() - 1);
-        for (int j = 0; j < nL; j++) {
-            if (!all && (lflags[j] & LF_NC)) continue;
-            int a = nodes2[2 * j], b = nodes2[2 * j + 1];
-            csr[fillp[a]++] = j;
-            csr[fillp[b]++] = (int)((unsigned)j | 0x80000000u);
-        }
-    };
     std::vector<int> rowptr, csr, qrowptr, qcsr;
-    buildCsr(false, rowptr, csr);
-    if (net.nNC > 0) buildCsr(true, qrowptr, qcsr);
+    buildLocalCsr(net, part, true, rowptr, csr);
+    if (net.nNC > 0) buildLocalCsr(net, part, false, qrowptr, qcsr);
     // the reference's link_setOutfallDepth loop (findNodeDepths): the last
     // link touching an outfall sets its depth
-    for (int j = 0; j < nL; j++) {
+    for (int j = 0; j < nOwn; j++) {
         int a = nodes2[2 * j], b = nodes2[2 * j + 1];
         if (net.nodeType[LN[b]] == OUTFALL) outLink[b] = j;
         else if (net.nodeType[LN[a]] == OUTFALL) outLink[a] = j;
@@ -2751,7 +2896,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     std::vector<int> defNodes;
     {
         std::vector<char> isDef(nN, 0);
-        for (int j = 0; j < nL; j++)
+        for (int j = 0; j < nOwn; j++)
             if (lflags[j] & LF_NC) { isDef[nodes2[2 * j]] = 1; isDef[nodes2[2 * j + 1]] = 1; }
         for (int i = 0; i < nN; i++)
             if (isDef[i]) { defNodes.push_back(i); nflags[i] = (int)((uint32_t)nflags[i] | NF_DEFER); }
@@ -2821,7 +2966,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
             std::vector<int> ncl;
             std::vector<NcLink> ncs;
             std::vector<double> coef, target, zero;
-            for (int j = 0; j < nL; j++) {
+            for (int j = 0; j < nOwn; j++) {
                 const int g = LL[j];
                 if (net.linkType[g] == CONDUIT) continue;
                 ncl.push_back(j);
@@ -2913,8 +3058,8 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         // is added by its owner only (replicas start their sums from 0)
         if (part.rank != 0) tot[0] = tot[1] = tot[2] = 0.0;
         d->latTot0[0] = tot[0]; d->latTot0[1] = tot[1]; d->latTot0[2] = tot[2];
-        std::vector<double> latL(nN);
-        for (int i = 0; i < nN; i++) latL[i] = part.owned[i] ? lat[LN[i]] : 0.0;
+        std::vector<double> latL(nN);                   // every replica adds the node's own inflow
+        for (int i = 0; i < nN; i++) latL[i] = lat[LN[i]];
         UPD(d->latBase, latL, nN);
         if (P) {
             UPD(d->qualBase, gq(qual, gN, LN), (size_t)P * nN);
@@ -3026,34 +3171,46 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         UPD(S.mbPendOut, pout, pout.size());
     }
     // ---- multi-GPU exchange ----------------------------------------------------
-    p.nShared = (int)sharedNodes.size();
-    p.xflag = 4 * part.nSharedGlobal;
+    p.nSend = (int)part.sendLink.size();
+    p.nGhost = (int)part.lghost.size();
     {
-        std::vector<int> slots(part.sharedSlot.begin(), part.sharedSlot.end());
+        bool seep = false;                          // evaporation / seepage values travel too
+        for (int j = 0; j < nL; j++) seep = seep || (lflags[j] & LF_SEEP);
+        p.xF = seep ? 6 : 4;
+        const int w = std::max(p.xF, P);
         int* ip;
-        UPI(ip, slots, nN); p.sharedSlot = ip;
-        UPI(ip, sharedNodes, sharedNodes.size()); p.sharedList = ip;
-        std::vector<double> z((size_t)p.xflag + 1, 0.0);
-        UPD(p.xsend, z, z.size());
-        UPD(p.xrecv, z, z.size());
-    }
-    d->gridS = std::max(1, std::min((p.nShared + kBlock - 1) / kBlock, maxBlocks));
-    if (part.active()) {
-        if (part.transport == XCHG_RCCL) {
-            if (part.ncclId.size() != sizeof(ncclUniqueId)) { fail("RCCL unique id missing"); return err_; }
-            ncclUniqueId id;
-            memcpy(&id, part.ncclId.data(), sizeof id);
-            ncclResult_t r = ncclCommInitRank(&d->comm, part.nranks, id, part.rank);
-            if (r != ncclSuccess) { fail(std::string("ncclCommInitRank: ") + ncclGetErrorString(r)); return err_; }
-        } else {
-            if (!part.xchg) { fail("host exchange callback missing"); return err_; }
-            HIPCHECK(hipHostMalloc((void**)&d->hostX, ((size_t)p.xflag + 8) * sizeof(double), hipHostMallocDefault));
+        UPI(ip, part.sendLink, part.sendLink.size()); p.sendLink = ip;
+        std::vector<double> zs((size_t)w * std::max(p.nSend, 1), 0.0), zg((size_t)w * std::max(p.nGhost, 1), 0.0);
+        UPD(p.xsend, zs, zs.size());
+        UPD(p.xrecv, zg, zg.size());
+        d->gridX = std::max(1, std::min((std::max(p.nSend, p.nGhost) + kBlock - 1) / kBlock, maxBlocks));
+        if (part.active()) {
+            if (part.transport == XCHG_RCCL) {
+                if (part.ncclId.size() != sizeof(ncclUniqueId)) { fail("RCCL unique id missing"); return err_; }
+                ncclUniqueId id;
+                memcpy(&id, part.ncclId.data(), sizeof id);
+                ncclResult_t r = ncclCommInitRank(&d->comm, part.nranks, id, part.rank);
+                if (r != ncclSuccess) { fail(std::string("ncclCommInitRank: ") + ncclGetErrorString(r)); return err_; }
+            } else {
+                if (!part.xchg) { fail("host exchange callback missing"); return err_; }
+                size_t nx = (size_t)w * std::max(p.nSend, p.nGhost) + 8;
+                HIPCHECK(hipHostMalloc((void**)&d->hostX, nx * sizeof(double), hipHostMallocDefault));
+            }
         }
     }
     p.partials = devAlloc<double>(d, (size_t)d->gridEnd * kNumPartials, &e);
     if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
     p.ctl = devAlloc<StepCtl>(d, 1, &e);
     if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+    {   // per-iteration flags and counters, sized from MAX_TRIALS (any value the reference accepts)
+        const size_t M = (size_t)std::max(p.maxTrials, 1);
+        std::vector<int> zi(M, 0);
+        UPI(p.unconv, zi, M);
+        UPI(p.ucount, zi, M);
+        p.work = devAlloc<unsigned long long>(d, 4 * M, &e);
+        if (e == hipSuccess) e = hipMemset(p.work, 0, 4 * M * sizeof(unsigned long long));
+        if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+    }
     d->ctl = p.ctl;
     HIPCHECK(hipHostMalloc((void**)&d->hostCtl, sizeof(StepCtl), hipHostMallocDefault));
     memset(d->hostCtl, 0, sizeof(StepCtl));
@@ -3095,13 +3252,14 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     HIPCHECK(hipHostMalloc((void**)&d->hostPinned, d->pinnedSize * sizeof(double), hipHostMallocDefault));
     for (auto& ev : d->ringEv) { HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming)); HIPCHECK(hipEventRecord(ev, d->stream)); }
     for (auto& ev : d->clockEv) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    HIPCHECK(hipHostMalloc((void**)&d->hostDt, 2 * Impl::kRing * sizeof(double),
+    HIPCHECK(hipHostMalloc((void**)&d->hostDt, (2 * Impl::kRing + 1) * sizeof(double),
                            hipHostMallocMapped | hipHostMallocCoherent));
     {
         void* dp = nullptr;
         HIPCHECK(hipHostGetDevicePointer(&dp, d->hostDt, 0));
         p.hostDt = (double*)dp;
         for (int r = 0; r < Impl::kRing; r++) d->hostDt[r] = d->hostCtl->dt;
+        d->hostDt[2 * Impl::kRing] = 0.0;          // k_tail barrier timeout flag
     }
 
     // algorithmic bytes per launch (DESIGN.md byte model; per kernel class)
@@ -3129,18 +3287,35 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         const double stat = d->fastLinks ? 60 : 116;
         d->kbytes[0] = d->nHot * (stat + 16 + 76 + 84) + nSeepHot * 16 + d->nColdD * 4;
         d->kbytes[4] = stat + 16 + 76 + 36 + (d->nHot > 0 ? 16.0 * nSeepHot / d->nHot : 0.0);
-        // node update: per node static (flags, fullDepth, surDepth, yCrown,
-        //   fullVolume, ponded: 4+5x8) + rowptr 4 + dynamic reads (newDepth,
-        //   oldDepth, oldNetInflow, newLat, oldSurfArea: 40) + writes (inflow,
-        //   outflow, newDepth, newVolume, overflow, dYdT, oldSurfArea, conv:
-        //   7x8+4) ; per CSR entry: index 4 + newFlow, sa, dqdh 24 + flags 4
-        // iterations >= 2 also read the node's "conduit updated" flag 1; a node
-        //   whose conduits were all bypassed reads its previous sums (inflow,
-        //   outflow, surface area, sum dq/dh: 32) instead of rowptr + CSR;
-        //   a gathering node writes those 4 sums (32), dYdT moved to step end
-        d->kbytes[1] = N * (44 + 4 + 40 + 32 + 52) + E * (4 + 24 + 4);
-        d->nodeFix = N * (44 + 40 + 52 - 16 + 1);
-        d->nodeGather = 4 + 32 + (N > 0 ? (double)E / N * 32.0 : 0.0);
+        // node update (k_node), per node, iteration 0: reads flags 4, yLast 8,
+        //   rowptr 4 (+ the neighbour's), fullDepth yCrown surDepth fullVolume
+        //   32 and the step-begin rotation's inflow outflow newVolume newLat
+        //   latIn 40 = 88; writes the rotation's oldDepth oldVolume
+        //   oldFlowInflow oldNetInflow oldLat newLat 48, the sums inflow
+        //   outflow surfArea sumdqdh 32, oldSurfArea newVolume overflow
+        //   newDepth 32 and conv 4 = 116; per CSR entry: index 4 + the link's
+        //   newFlow 8, flags 4, surfArea at that end 8, dqdh 8 = 32
+        //   iteration 1: no rotation; reads yOld lat oldNetInflow instead
+        //   (72), writes the sums, oldSurfArea newVolume overflow newDepth
+        //   conv, the cached unrelaxed depth yRaw and the dirty byte (77)
+        //   iterations >= 2: every node's flags, frozen and dirty bytes are
+        //   scanned (6); a relaxation-only update reads newDepth yCrown yRaw
+        //   yMaxNP and writes newDepth conv (44); a full update reads yLast
+        //   yOld lat oldNetInflow fullDepth yCrown surDepth fullVolume (64),
+        //   writes oldSurfArea newVolume overflow newDepth conv dirty yRaw
+        //   (45) and reads or writes the four sums (32); a gathering node
+        //   adds rowptr 8 and its CSR entries (32 each).  The counts of each
+        //   kind come from the timing-mode counters (StepCtl nodeLive /
+        //   nodeFast / nodeWork), so frozen nodes are not charged bytes they
+        //   never fetch.
+        d->kbytes[1] = N * (88 + 116) + E * 32;
+        d->nodeIter1 = N * (72 + 77) + E * 32;
+        d->nodeScan = 6;
+        d->nodeFastB = 44;
+        d->nodeUpdB = 64 + 45 + 32;
+        d->nodeGather = 8 + (N > 0 ? (double)E / N * 32.0 : 0.0);
+        d->kbytes[5] = d->nodeIter1;
+        d->kbytes[6] = N * (6 + 141) + E * 32;    // every node updated and gathering (no timing data)
         // step end: per conduit flags, state word (r+w), a1, aFull, newFlow,
         //   froude, newVolume, modLength, length (48 + 4) and the run
         //   statistics: oldFlow, maxFlow, newDepth, maxVeloc, maxDepth, the
@@ -3161,7 +3336,11 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     if (!d->useGraph) { ok_ = true; return 0; }
     hipGraph_t g;
     HIPCHECK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
-    launchStep(d);
+    if (launchStep(d)) {                           // a collective refused at capture
+        (void)hipStreamEndCapture(d->stream, &g);
+        fail(d->xerrMsg);
+        return err_;
+    }
     HIPCHECK(hipStreamEndCapture(d->stream, &g));
     HIPCHECK(hipGraphInstantiate(&d->graph, g, nullptr, nullptr, 0));
     (void)hipGraphDestroy(g);
@@ -3184,7 +3363,11 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     }
     if (d->tailGrid > 0) {
         HIPCHECK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
-        launchStep(d, true);
+        if (launchStep(d, true)) {
+            (void)hipStreamEndCapture(d->stream, &g);
+            fail(d->xerrMsg);
+            return err_;
+        }
         HIPCHECK(hipStreamEndCapture(d->stream, &g));
         HIPCHECK(hipGraphInstantiate(&d->graphTail, g, nullptr, nullptr, 0));
         (void)hipGraphDestroy(g);
@@ -3205,11 +3388,24 @@ static void flushTiming(Router::Impl* d)
     for (int s = 0; s < d->tUsed; s++) {
         Router::Impl::TimingSlot& t = d->tslots[s];
         int ran = (int)(t.pinned[0] & 0xFFFFFFFFull);
-        const unsigned long long* work = t.pinned + 1;
+        const unsigned long long* work = t.pinned + 1;       // linkWork, nodeWork, nodeLive, nodeFast
+        if ((int)d->iterStats.size() < Router::Impl::kIterCols * p.maxTrials)
+            d->iterStats.assign((size_t)Router::Impl::kIterCols * p.maxTrials, 0.0);
         for (int k = 0; k < ran; k++) {    // early-exited iterations are not counted
             float ms1 = 0, ms2 = 0;
             (void)hipEventElapsedTime(&ms1, t.ev[4 * k], t.evHot[k]);
             (void)hipEventElapsedTime(&ms2, t.ev[4 * k + 1], t.ev[4 * k + 2]);
+            {
+                const int M = p.maxTrials;
+                double* it = d->iterStats.data() + (size_t)Router::Impl::kIterCols * k;
+                it[0] += 1;
+                it[1] += (k >= 2) ? (double)work[k] : d->nHot;
+                it[2] += (k >= 2) ? (double)work[M + k] : (double)p.nN;
+                it[3] += (k >= 2) ? (double)work[2 * M + k] : (double)p.nN;
+                it[4] += (k >= 2) ? (double)work[3 * M + k] : 0.0;
+                it[5] += ms1;
+                it[6] += ms2;
+            }
             int c = (k == 0) ? 0 : 4;
             d->kms[c] += ms1; d->kcnt[c]++;
             if (k == 0) d->kbytesSum[0] += d->kbytes[0];
@@ -3218,21 +3414,28 @@ static void flushTiming(Router::Impl* d)
                 d->workSum += w;
                 d->kbytesSum[4] += w * d->kbytes[4] + (d->nHot - w) * 20.0 + d->nColdD * 4.0;
             }
-            d->kms[1] += ms2; d->kcnt[1]++;
-            if (k < 2) d->kbytesSum[1] += d->kbytes[1];
+            const int cn = (k == 0) ? 1 : (k == 1 ? 5 : 6);
+            d->kms[cn] += ms2; d->kcnt[cn]++;
+            if (k == 0) d->kbytesSum[1] += d->kbytes[1];
+            else if (k == 1) d->kbytesSum[5] += d->nodeIter1;
             else {
-                double g = (double)work[kMaxTrialsCap + k];
-                d->kbytesSum[1] += d->nodeFix + g * d->nodeGather + ((double)p.nN - g) * 32.0;
+                const int M = p.maxTrials;
+                double g = (double)work[M + k];
+                double live = (double)work[2 * M + k], fast = (double)work[3 * M + k];
+                d->kbytesSum[6] += d->nodeScan * (double)p.nN + fast * d->nodeFastB +
+                                   (live - fast) * d->nodeUpdB + g * d->nodeGather;
                 d->gatherSum += g; d->gatherCnt += 1;
             }
         }
         int base = 4 * p.maxTrials;
         float ms3 = 0, msq = 0;
-        (void)hipEventElapsedTime(&ms3, t.ev[base + 1], t.ev[base + 2]);
-        (void)hipEventElapsedTime(&msq, t.ev[base], t.ev[base + 1]);
+        (void)hipEventElapsedTime(&ms3, t.ev[base + 2], t.ev[base + 3]);
         d->kms[2] += ms3; d->kcnt[2]++;
         d->kbytesSum[2] += d->kbytes[2];
-        if (p.P) { d->kms[3] += msq; d->kcnt[3]++; d->kbytesSum[3] += d->kbytes[3]; }
+        if (p.P) {
+            (void)hipEventElapsedTime(&msq, t.ev[base], t.ev[base + 1]);
+            d->kms[3] += msq; d->kcnt[3]++; d->kbytesSum[3] += d->kbytes[3];
+        }
     }
     d->tUsed = 0;
 }
@@ -3259,11 +3462,25 @@ static bool useTail(Router::Impl* d)
     return d->itersSeen < 0 || d->itersAvg <= kTailIters;
 }
 
+// A k_tail launch whose grid barrier timed out left its step incomplete; the
+// flag arrives through the host-mapped ring (k_finalize), so the next
+// swmm_step fails at once and k_tail is not used again.
+static bool tailFailed(Router::Impl* d)
+{
+    if (d->hostDt[2 * Router::Impl::kRing] == 0.0) return false;
+    d->tailGrid = 0;
+    return true;
+}
+
 int Router::step(const double* latFlow, const double* qualLoad, const double tot[3])
 {
     auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
     Impl* d = d_;
     Params& p = d->p;
+    if (tailFailed(d)) {
+        fail("k_tail grid barrier timed out (workgroups not co-resident); the step it ran is incomplete");
+        return err_;
+    }
     if (latFlow) {
         // pinned ring slot: wait until the DMA that last read this slot is done
         int s = d->ringNext;
@@ -3272,14 +3489,19 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
         double* slot = d->hostPinned + (size_t)s * d->slotDoubles;
         size_t nN = p.nN, nq = (size_t)p.P * nN;
         const Partition& part = d->part;
-        if (part.active()) {                       // this rank's nodes; owners add inflow
-            for (size_t i = 0; i < nN; i++) slot[i] = part.owned[i] ? latFlow[part.lnode[i]] : 0.0;
+        if (part.active()) {                       // this rank's held nodes (every replica adds them)
+            for (size_t i = 0; i < nN; i++) slot[i] = latFlow[part.lnode[i]];
         } else {
             memcpy(slot, latFlow, nN * sizeof(double));
         }
         if (nq) {
-            if (qualLoad) memcpy(slot + nN, qualLoad, nq * sizeof(double));
-            else memset(slot + nN, 0, nq * sizeof(double));
+            if (!qualLoad) memset(slot + nN, 0, nq * sizeof(double));
+            else if (!part.active()) memcpy(slot + nN, qualLoad, nq * sizeof(double));
+            else {                                 // [p][global node] -> [p][held node]
+                const size_t gN = part.nodeOwner.size();
+                for (size_t q = 0; q < (size_t)p.P; q++)
+                    for (size_t i = 0; i < nN; i++) slot[nN + q * nN + i] = qualLoad[q * gN + part.lnode[i]];
+            }
         }
         bool countTotals = part.rank == 0;         // system totals counted once
         slot[nN + nq + 0] = countTotals ? tot[0] : 0.0;
@@ -3299,26 +3521,28 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
         if (d->tUsed == (int)d->tslots.size()) {
             d->tslots.emplace_back();
             Impl::TimingSlot& t = d->tslots.back();
-            t.ev.resize(4 * kMaxTrialsCap + 4);
-            t.evHot.resize(kMaxTrialsCap);
+            const int M = std::max(p.maxTrials, 1);
+            t.ev.resize(4 * M + 6);
+            t.evHot.resize(M);
             for (auto& ev : t.ev) HIPCHECK(hipEventCreate(&ev));
             for (auto& ev : t.evHot) HIPCHECK(hipEventCreate(&ev));
-            HIPCHECK(hipHostMalloc((void**)&t.pinned, (1 + 2 * kMaxTrialsCap) * sizeof(unsigned long long),
+            HIPCHECK(hipHostMalloc((void**)&t.pinned, (1 + 4 * (size_t)M) * sizeof(unsigned long long),
                                    hipHostMallocDefault));
         }
         Impl::TimingSlot& t = d->tslots[d->tUsed++];
         d->curEv = t.ev.data();
         d->curHot = t.evHot.data();
-        launchStep(d);
+        if (launchStep(d)) { fail(d->xerrMsg); return err_; }
         HIPCHECK(hipMemcpyAsync(t.pinned, &d->ctl->lastSteps, sizeof(int), hipMemcpyDeviceToHost,
                                 d->stream));
-        HIPCHECK(hipMemcpyAsync(t.pinned + 1, d->ctl->linkWork, 2 * kMaxTrialsCap * sizeof(unsigned long long),
-                                hipMemcpyDeviceToHost, d->stream));
-        HIPCHECK(hipMemsetAsync(d->ctl->linkWork, 0, 2 * kMaxTrialsCap * sizeof(unsigned long long), d->stream));
+        const size_t wb = 4 * (size_t)std::max(p.maxTrials, 1) * sizeof(unsigned long long);
+        HIPCHECK(hipMemcpyAsync(t.pinned + 1, p.work, wb, hipMemcpyDeviceToHost, d->stream));
+        HIPCHECK(hipMemsetAsync(p.work, 0, wb, d->stream));
     } else if (d->useGraph) {
         HIPCHECK(hipGraphLaunch(useTail(d) ? d->graphTail : d->graph, d->stream));
-    } else {
-        launchStep(d);
+    } else if (launchStep(d)) {                   // eager (host-transport exchange)
+        fail(d->xerrMsg);
+        return err_;
     }
     // completion marker of this step: k_finalize has by then written the next
     // step's dt into the host-mapped ring (Router::launchedDt)
@@ -3335,6 +3559,10 @@ int Router::launchedDt(double* dt)
     // k_finalize into slot (L-1) % kRing (slot 0 holds the initial step)
     long long L = d->launched;
     if (L >= 2) HIPCHECK(hipEventSynchronize(d->clockEv[(L - 2) % Impl::kRing]));
+    if (tailFailed(d)) {
+        fail("k_tail grid barrier timed out (workgroups not co-resident); the step it ran is incomplete");
+        return err_;
+    }
     *dt = d->hostDt[(L - 1) % Impl::kRing];
     return 0;
 }
@@ -3421,8 +3649,8 @@ int Router::download(Project& prj)
     HIPCHECK(dnL(st.evapLossRate, p.evapLoss));
     HIPCHECK(dnL(st.seepLossRate, p.seepLoss));
     HIPCHECK(dnL(st.setting, p.setting));
-    size_t P = p.P;                                 // (quality: one GPU only)
-    if (P) {
+    size_t P = p.P;
+    if (P && !multi) {
         auto dn = [&](std::vector<double>& v, const double* src, size_t n) {
             v.resize(n);
             return hipMemcpyAsync(v.data(), src, n * sizeof(double), hipMemcpyDeviceToHost, d->stream);
@@ -3431,6 +3659,29 @@ int Router::download(Project& prj)
         HIPCHECK(dn(st.nNewQual, p.nNewQual, P * nN));
         HIPCHECK(dn(st.lOldQual, p.lOldQual, P * nL));
         HIPCHECK(dn(st.lNewQual, p.lNewQual, P * nL));
+    } else if (P) {                                 // owned nodes / links to their global slots
+        const size_t gN = prj.net.nNodes(), gL = prj.net.nLinks(), nLs = p.nLs;
+        auto qn = [&](std::vector<double>& v, const double* src) -> hipError_t {
+            v.resize(P * gN);
+            tmp.resize(P * nN);
+            hipError_t r = hipMemcpy(tmp.data(), src, P * nN * sizeof(double), hipMemcpyDeviceToHost);
+            for (size_t q = 0; q < P; q++)
+                for (size_t i = 0; i < nN; i++)
+                    if (part.owned[i]) v[q * gN + part.lnode[i]] = tmp[q * nN + i];
+            return r;
+        };
+        auto ql = [&](std::vector<double>& v, const double* src) -> hipError_t {
+            v.resize(P * gL);
+            tmp.resize(P * nLs);
+            hipError_t r = hipMemcpy(tmp.data(), src, P * nLs * sizeof(double), hipMemcpyDeviceToHost);
+            for (size_t q = 0; q < P; q++)
+                for (size_t j = 0; j < nL; j++) v[q * gL + part.llink[j]] = tmp[q * nLs + j];
+            return r;
+        };
+        HIPCHECK(qn(st.nOldQual, p.nOldQual));
+        HIPCHECK(qn(st.nNewQual, p.nNewQual));
+        HIPCHECK(ql(st.lOldQual, p.lOldQual));
+        HIPCHECK(ql(st.lNewQual, p.lNewQual));
     }
     std::vector<int> ls(nL), cv(nN);
     HIPCHECK(hipMemcpyAsync(ls.data(), p.lstate, nL * sizeof(int), hipMemcpyDeviceToHost, d->stream));
@@ -3670,6 +3921,7 @@ void Router::setTiming(bool on)
     d_->p.countWork = on ? 1 : 0;                  // eager launches only; the graph keeps 0
     for (int k = 0; k < Impl::kClasses; k++) { d_->kms[k] = 0; d_->kcnt[k] = 0; d_->kbytesSum[k] = 0; }
     d_->workSum = 0;
+    d_->iterStats.clear();
     d_->gatherSum = 0;
     d_->gatherCnt = 0;
 }
@@ -3688,12 +3940,19 @@ int Router::timeKernel(int which, int reps, double* avgUs)
     HIPCHECK(hipEventCreate(&b));
     HIPCHECK(hipStreamSynchronize(d->stream));
     HIPCHECK(hipEventRecord(a, d->stream));
+    // the probe instantiations (distinct kernel names, same code)
+    LinkKernelFn lk = nullptr;
+    switch (d->linkWaves) {
+    case 3: lk = d->fastLinks ? k_link<true, 3, true, true> : k_link<true, 3, false, true>; break;
+    case 4: lk = d->fastLinks ? k_link<true, 4, true, true> : k_link<true, 4, false, true>; break;
+    default: lk = d->fastLinks ? k_link<true, 1, true, true> : k_link<true, 1, false, true>; break;
+    }
+    LinkKernelFn nk = d->general ? k_node<true, true, true> : k_node<true, false, true>;
     for (int r = 0; r < reps; r++) {
         if (which == 0)
-            hipLaunchKernelGGL(linkKernel(true, d->linkWaves, d->fastLinks), dim3(d->gridL), dim3(kBlock), 0,
-                               d->stream, p, 0);
+            hipLaunchKernelGGL(lk, dim3(d->gridL), dim3(kBlock), 0, d->stream, p, 0);
         else
-            hipLaunchKernelGGL(nodeKernel(true, d->general), dim3(d->gridN), dim3(kBlock), 0, d->stream, p, 0);
+            hipLaunchKernelGGL(nk, dim3(d->gridN), dim3(kBlock), 0, d->stream, p, 0);
     }
     HIPCHECK(hipEventRecord(b, d->stream));
     HIPCHECK(hipEventSynchronize(b));
@@ -3905,6 +4164,14 @@ int Router::kernelTimes(double* out, int n)
         out[2 * k + 1] = d_->kms[k];
     }
     return m;
+}
+
+int Router::iterationStats(double* out, int n)
+{
+    flushTiming(d_);
+    const int m = std::min(n, (int)d_->iterStats.size());
+    for (int k = 0; k < m; k++) out[k] = d_->iterStats[k];
+    return (int)d_->iterStats.size();
 }
 
 int Router::kernelBytes(double* out, int n)

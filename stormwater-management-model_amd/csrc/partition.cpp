@@ -1,9 +1,27 @@
-// partition.cpp -- owner assignment and local index maps (see partition.h).
+// partition.cpp -- owner assignment, ghost links, neighbour lists and the
+// local node -> link incidence (see partition.h).
 #include "partition.h"
 
+#include <algorithm>
+#include <numeric>
 #include <string>
+#include <unordered_map>
 
 namespace swx {
+
+namespace {
+
+// smallest-index root union-find (deferred-node groups)
+int findRoot(std::vector<int>& up, int a)
+{
+    while (up[a] != a) {
+        up[a] = up[up[a]];
+        a = up[a];
+    }
+    return a;
+}
+
+}  // namespace
 
 int buildPartition(const Network& net, Partition& part, std::string* msg)
 {
@@ -12,61 +30,190 @@ int buildPartition(const Network& net, Partition& part, std::string* msg)
         if (msg) *msg = "invalid rank / number of ranks";
         return 500;
     }
+    const int me = part.rank;
     // nodes: contiguous blocks of the node index
     part.nodeOwner.assign(nN, 0);
     for (int i = 0; i < nN; i++) part.nodeOwner[i] = (int)((long long)i * R / nN);
-    // conduits: owner of node1; outfalls: owner of their conduit
+    // pumps / regulators: their end nodes ("deferred": updated by k_nc from
+    // running link-order totals) and every link touching one stay on one rank,
+    // the owner of the group's smallest node
+    std::vector<char> deferred(nN, 0);
+    for (int j = 0; j < nL; j++)
+        if (net.linkType[j] != CONDUIT) deferred[net.node1[j]] = deferred[net.node2[j]] = 1;
+    {
+        std::vector<int> up(nN);
+        std::iota(up.begin(), up.end(), 0);
+        for (int j = 0; j < nL; j++) {
+            int a = net.node1[j], b = net.node2[j];
+            if (!deferred[a] || !deferred[b]) continue;
+            a = findRoot(up, a);
+            b = findRoot(up, b);
+            if (a != b) up[std::max(a, b)] = std::min(a, b);
+        }
+        for (int i = 0; i < nN; i++)
+            if (deferred[i]) part.nodeOwner[i] = part.nodeOwner[findRoot(up, i)];
+    }
+    // conduits: owner of node1 (of the deferred end, if one end is deferred);
+    // outfalls: owner of their conduit
     part.linkOwner.assign(nL, 0);
-    for (int j = 0; j < nL; j++) part.linkOwner[j] = part.nodeOwner[net.node1[j]];
+    for (int j = 0; j < nL; j++) {
+        int n1 = net.node1[j], n2 = net.node2[j];
+        part.linkOwner[j] = part.nodeOwner[(deferred[n2] && !deferred[n1]) ? n2 : n1];
+    }
     for (int j = 0; j < nL; j++) {
         int n1 = net.node1[j], n2 = net.node2[j];
         if (net.nodeType[n2] == OUTFALL) part.nodeOwner[n2] = part.linkOwner[j];
         else if (net.nodeType[n1] == OUTFALL) part.nodeOwner[n1] = part.linkOwner[j];
     }
-    // ranks touching each node: its owner and the owners of its conduits.
-    // A node is shared when that set has more than one rank.
-    std::vector<int> firstRank(nN), shared(nN, 0);
-    for (int i = 0; i < nN; i++) firstRank[i] = part.nodeOwner[i];
+    // holders of each node: its owner and the owners of the links touching it
+    // (a rank holds a node it owns or that one of its links touches); the
+    // nodes with more than one holder are few (strip boundaries)
+    std::unordered_map<int, std::vector<int>> extra;
+    auto addHolder = [&](int n, int r) {
+        if (r == part.nodeOwner[n]) return;
+        std::vector<int>& v = extra[n];
+        if (std::find(v.begin(), v.end(), r) == v.end()) v.push_back(r);
+    };
     for (int j = 0; j < nL; j++) {
-        int r = part.linkOwner[j];
-        for (int n : {net.node1[j], net.node2[j]})
-            if (r != firstRank[n]) shared[n] = 1;
+        addHolder(net.node1[j], part.linkOwner[j]);
+        addHolder(net.node2[j], part.linkOwner[j]);
     }
-    // present on this rank: owned nodes and both ends of owned conduits
-    std::vector<char> here(nN, 0);
-    for (int i = 0; i < nN; i++)
-        if (part.nodeOwner[i] == part.rank) here[i] = 1;
-    for (int j = 0; j < nL; j++)
-        if (part.linkOwner[j] == part.rank) here[net.node1[j]] = here[net.node2[j]] = 1;
+    auto holds = [&](int n, int r) {
+        if (part.nodeOwner[n] == r) return true;
+        auto it = extra.find(n);
+        return it != extra.end() && std::find(it->second.begin(), it->second.end(), r) != it->second.end();
+    };
+    // a link is a ghost on every rank other than its owner that holds one of
+    // its end nodes; deferred nodes must not be held by two ranks (k_nc runs
+    // on one rank)
+    for (const auto& kv : extra)
+        if (deferred[kv.first]) {
+            if (msg) *msg = "a pump / regulator end node is shared between ranks";
+            return 500;
+        }
+    // ghost sets: (receiver, sender, link); global slots: links that are a
+    // ghost anywhere
+    struct G { int to, from, link; };
+    std::vector<G> ghosts;
+    std::vector<int> slotLinks;
+    for (int j = 0; j < nL; j++) {
+        const int s = part.linkOwner[j];
+        int rs[8], nr = 0;
+        for (int n : {net.node1[j], net.node2[j]}) {
+            auto add = [&](int r) {
+                if (r == s) return;
+                for (int q = 0; q < nr; q++) if (rs[q] == r) return;
+                if (nr < 8) rs[nr++] = r;
+            };
+            add(part.nodeOwner[n]);
+            auto it = extra.find(n);
+            if (it != extra.end()) for (int r : it->second) add(r);
+        }
+        if (nr == 0) continue;
+        slotLinks.push_back(j);
+        for (int q = 0; q < nr; q++) ghosts.push_back({rs[q], s, j});
+    }
+    part.nSlotGlobal = (int)slotLinks.size();
+    std::unordered_map<int, int> slotOf;
+    slotOf.reserve(slotLinks.size() * 2 + 1);
+    for (size_t k = 0; k < slotLinks.size(); k++) slotOf[slotLinks[k]] = (int)k;
 
+    // ---- this rank's held nodes and owned links --------------------------
     part.lnode.clear();
     part.gnode.assign(nN, -1);
-    std::vector<int> slotOf(nN, -1);
-    int slot = 0;
-    for (int i = 0; i < nN; i++) {
-        if (shared[i]) slotOf[i] = slot++;
-        if (here[i]) {
+    for (int i = 0; i < nN; i++)
+        if (holds(i, me)) {
             part.gnode[i] = (int)part.lnode.size();
             part.lnode.push_back(i);
         }
-    }
-    part.nSharedGlobal = slot;
     part.llink.clear();
     part.glink.assign(nL, -1);
     for (int j = 0; j < nL; j++)
-        if (part.linkOwner[j] == part.rank) {
+        if (part.linkOwner[j] == me) {
             part.glink[j] = (int)part.llink.size();
             part.llink.push_back(j);
         }
     const int n = (int)part.lnode.size();
-    part.sharedSlot.assign(n, -1);
     part.owned.assign(n, 0);
-    for (int k = 0; k < n; k++) {
-        int g = part.lnode[k];
-        part.sharedSlot[k] = slotOf[g];
-        part.owned[k] = part.nodeOwner[g] == part.rank;
+    for (int k = 0; k < n; k++) part.owned[k] = part.nodeOwner[part.lnode[k]] == me;
+
+    // ---- ghosts received (sender ascending, link ascending) and links sent
+    std::vector<G> in, out;
+    for (const G& g : ghosts) {
+        if (g.to == me) in.push_back(g);
+        if (g.from == me) out.push_back(g);
     }
+    auto bySender = [](const G& a, const G& b) { return a.from != b.from ? a.from < b.from : a.link < b.link; };
+    auto byReceiver = [](const G& a, const G& b) { return a.to != b.to ? a.to < b.to : a.link < b.link; };
+    std::sort(in.begin(), in.end(), bySender);
+    std::sort(out.begin(), out.end(), byReceiver);
+    part.lghost.clear();
+    part.recvSlot.clear();
+    for (const G& g : in) {
+        part.lghost.push_back(g.link);
+        part.recvSlot.push_back(slotOf[g.link]);
+    }
+    part.sendLink.clear();
+    part.sendSlot.clear();
+    for (const G& g : out) {
+        part.sendLink.push_back(part.glink[g.link]);
+        part.sendSlot.push_back(slotOf[g.link]);
+    }
+    part.nbr.clear();
+    for (const G& g : in) part.nbr.push_back(g.from);
+    for (const G& g : out) part.nbr.push_back(g.to);
+    std::sort(part.nbr.begin(), part.nbr.end());
+    part.nbr.erase(std::unique(part.nbr.begin(), part.nbr.end()), part.nbr.end());
+    const int nb = (int)part.nbr.size();
+    part.sendOff.assign(nb + 1, 0);
+    part.recvOff.assign(nb + 1, 0);
+    for (int k = 0; k < nb; k++) {
+        const int r = part.nbr[k];
+        part.sendOff[k + 1] = part.sendOff[k] + (int)std::count_if(out.begin(), out.end(),
+                                                                   [r](const G& g) { return g.to == r; });
+        part.recvOff[k + 1] = part.recvOff[k] + (int)std::count_if(in.begin(), in.end(),
+                                                                   [r](const G& g) { return g.from == r; });
+    }
+    // held nodes touched by a ghost link: their sums include received values
+    // (never reused across iterations, never frozen: see k_node)
+    part.hasGhost.assign(n, 0);
+    for (int g : part.lghost)
+        for (int e : {net.node1[g], net.node2[g]})
+            if (part.gnode[e] >= 0) part.hasGhost[part.gnode[e]] = 1;
     return 0;
+}
+
+void buildLocalCsr(const Network& net, const Partition& part, bool conduitsOnly, std::vector<int>& rowptr,
+                   std::vector<int>& csr)
+{
+    const int n = (int)part.lnode.size();
+    const int nOwned = (int)part.llink.size();
+    const int nLoc = nOwned + (int)part.lghost.size();
+    auto global = [&](int l) { return l < nOwned ? part.llink[l] : part.lghost[l - nOwned]; };
+    rowptr.assign(n + 1, 0);
+    for (int l = 0; l < nLoc; l++) {
+        const int g = global(l);
+        if (conduitsOnly && net.linkType[g] != CONDUIT) continue;
+        for (int e : {net.node1[g], net.node2[g]})
+            if (part.gnode[e] >= 0) rowptr[part.gnode[e] + 1]++;
+    }
+    for (int i = 0; i < n; i++) rowptr[i + 1] += rowptr[i];
+    csr.assign(rowptr[n], 0);
+    std::vector<int> fill(rowptr.begin(), rowptr.end() - 1);
+    for (int l = 0; l < nLoc; l++) {
+        const int g = global(l);
+        if (conduitsOnly && net.linkType[g] != CONDUIT) continue;
+        const int a = part.gnode[net.node1[g]], b = part.gnode[net.node2[g]];
+        if (a >= 0) csr[fill[a]++] = l;
+        if (b >= 0) csr[fill[b]++] = (int)((unsigned)l | 0x80000000u);
+    }
+    // ascending global link index within each row (owned links come first in
+    // local order, so a row that mixes in ghosts needs sorting)
+    for (int i = 0; i < n; i++) {
+        auto key = [&](int ent) { return global(ent & 0x7FFFFFFF); };
+        std::stable_sort(csr.begin() + rowptr[i], csr.begin() + rowptr[i + 1],
+                         [&](int x, int y) { return key(x) < key(y); });
+    }
 }
 
 }  // namespace swx

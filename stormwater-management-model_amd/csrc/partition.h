@@ -3,18 +3,24 @@
 // One process per GPU.  Nodes are split into contiguous blocks of the
 // reference's node index (row strips for the row-major synthetic grids); a
 // conduit belongs to the rank that owns its node1, an outfall to the rank that
-// owns its (single) conduit.  A node is *shared* when the conduits touching it
-// belong to more than one rank, or to a rank other than the node's owner.
-// Every rank touching a shared node keeps a replica of it.  Each Picard
-// iteration, every rank sums the contributions of its own conduits (plus, on
-// the owner, the node's own inflow and ponded area) for its shared nodes and
-// one all-reduce adds the partial sums; every replica then applies the same
-// depth update to the same sums, so the replicas stay identical without a
-// second exchange.  Interior nodes and all conduits are computed exactly as on
-// one GPU (same arithmetic, same summation order); only a shared node's sums
-// are reassociated (partial sums per rank).
+// owns its (single) conduit.  Pumps and regulators (routed by k_nc, whose node
+// sums need the running totals of their end nodes) keep their end nodes and
+// every link touching those nodes on one rank.
+//
+// A rank holds its *owned* links and every node they touch (owned nodes plus
+// replicas of nodes owned elsewhere).  For every held node it also needs the
+// contributions of the links of other ranks that touch the node: those are
+// its *ghost* links.  Each Picard iteration the owner of a ghost link sends
+// its {flow, surface areas, dq/dh (, evaporation, seepage)} to the ranks that
+// hold it as a ghost (strip neighbours for the grids), and every held node is
+// then summed over all its links in global link order -- the reference's
+// serial scatter order (dynwave.c:398-411, 528-589).  Every replica of a node
+// therefore computes exactly the single-GPU update: the partitioned run is
+// bitwise equal to one GPU.  A small all-reduce (max) of the per-iteration
+// "some node did not converge" flag keeps the ranks' Picard loops in step.
 #pragma once
 
+#include <string>
 #include <vector>
 
 #include "model.h"
@@ -36,18 +42,38 @@ struct Partition {
 
     // ---- derived by buildPartition (identical on every rank) -------------
     std::vector<int> nodeOwner, linkOwner;  // global object -> rank
-    std::vector<int> lnode, llink;          // local -> global, ascending global index
-    std::vector<int> gnode, glink;          // global -> local, -1 when not present here
-    std::vector<int> sharedSlot;            // per local node: global shared slot or -1
+    std::vector<int> lnode, llink;          // local -> global, ascending global index (llink: owned)
+    std::vector<int> gnode, glink;          // global -> local, -1 when not held (glink: owned only)
     std::vector<char> owned;                // per local node: this rank owns it
-    int nSharedGlobal = 0;
+    std::vector<char> hasGhost;             // per local node: a ghost link touches it
+    // ghost links: local link index nOwned + g holds global link lghost[g];
+    // grouped by the sending rank (ascending), ascending global index within
+    std::vector<int> lghost;
+    // neighbour exchange: nbr[k] = k-th rank this one exchanges with
+    // (ascending); the links sent to it are sendLink[sendOff[k] .. sendOff[k+1])
+    // (local owned indices, in the receiver's ghost order); the ghosts received
+    // from it are lghost[recvOff[k] .. recvOff[k+1])
+    std::vector<int> nbr, sendOff, sendLink, recvOff;
+    // host transport: one global slot per link that is a ghost anywhere
+    // (ascending global index); sendSlot / recvSlot per send / ghost entry
+    std::vector<int> sendSlot, recvSlot;
+    int nSlotGlobal = 0;
 
     bool forced = false;                    // partitioned code path with one rank (tests)
     bool active() const { return nranks > 1 || forced; }
+    int nOwnedLinks() const { return (int)llink.size(); }
 };
 
 // Fills the derived fields of `part` for `net`.  Returns 0, or an error code
 // (and message) when the network cannot be partitioned.
 int buildPartition(const Network& net, Partition& part, std::string* msg);
+
+// Node -> link incidence of this rank's held nodes over its owned and ghost
+// links, each row in ascending GLOBAL link index (the reference's summation
+// order).  Entries are local link indices (ghosts: nOwned + g) with bit 31 set
+// when the node is the link's node2.  conduitsOnly drops pumps and regulators
+// from the rows (their flows join the node sums after all conduits, in k_nc).
+void buildLocalCsr(const Network& net, const Partition& part, bool conduitsOnly,
+                   std::vector<int>& rowptr, std::vector<int>& csr);
 
 }  // namespace swx

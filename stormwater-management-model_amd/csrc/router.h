@@ -88,6 +88,10 @@ public:
     void setTiming(bool on);
     int kernelTimes(double* out, int n);
     int kernelBytes(double* out, int n);
+    // per Picard iteration k of the timed steps, 7 values each: launches,
+    // conduits updated, nodes gathered, nodes updated, relaxation-only node
+    // updates, k_link ms, k_node ms; returns the number of values available
+    int iterationStats(double* out, int n);
     std::string deviceName() const { return devName_; }
     bool ok() const { return ok_; }
     int lastError() const { return err_; }

@@ -39,7 +39,8 @@ class EngineMissing(RuntimeError):
 
 
 # kernel classes of swmmx_getKernelTimes / swmmx_getKernelBytes
-KERNEL_CLASSES = ["link_momentum_first", "node_update", "step_end", "quality", "link_momentum_iter"]
+KERNEL_CLASSES = ["link_momentum_first", "node_update_first", "step_end", "quality", "link_momentum_iter",
+                  "node_update_iter1", "node_update_iter2plus"]
 
 
 def load_library(path: str | None = None):
@@ -84,6 +85,7 @@ def load_library(path: str | None = None):
         "swmmx_setTiming": (c_int, [c_int]),
         "swmmx_getKernelTimes": (c_int, [P(c_dbl), c_int]),
         "swmmx_getKernelBytes": (c_int, [P(c_dbl), c_int]),
+        "swmmx_getIterationStats": (c_int, [P(c_dbl), c_int]),
         "swmmx_getBackend": (c_int, [ctypes.c_char_p, c_int]),
         "swmmx_setDevice": (c_int, [c_int]),
         "swmmx_timeKernel": (c_int, [c_int, c_int, P(c_dbl)]),
@@ -91,6 +93,7 @@ def load_library(path: str | None = None):
         "swmmx_setPartition": (c_int, [c_int, c_int, ctypes.c_void_p, c_int]),
         "swmmx_setExchange": (c_int, [ctypes.c_void_p, ctypes.c_void_p]),
         "swmmx_getOwner": (c_int, [c_int, P(c_int), c_int]),
+        "swmmx_getPartition": (ctypes.c_long, [c_char_p, P(c_int), ctypes.c_long]),
         "swmmx_xsect": (c_int, [c_int, P(c_dbl), c_dbl, c_int, P(c_dbl), P(c_dbl), c_int, c_int]),
     }
     for name, (res, args) in sig.items():
@@ -254,16 +257,26 @@ class SWMM:
         return self.L.swmmx_setTiming(1 if on else 0)
 
     def kernel_times(self):
-        a = (ctypes.c_double * 10)()
-        n = self.L.swmmx_getKernelTimes(a, 10)
+        a = (ctypes.c_double * (2 * len(KERNEL_CLASSES)))()
+        n = self.L.swmmx_getKernelTimes(a, 2 * len(KERNEL_CLASSES))
         names = KERNEL_CLASSES
         return {names[k]: (a[2 * k], a[2 * k + 1]) for k in range(n)}
 
     def kernel_bytes(self):
-        a = (ctypes.c_double * 5)()
-        n = self.L.swmmx_getKernelBytes(a, 5)
+        a = (ctypes.c_double * len(KERNEL_CLASSES))()
+        n = self.L.swmmx_getKernelBytes(a, len(KERNEL_CLASSES))
         names = KERNEL_CLASSES
         return {names[k]: a[k] for k in range(n)}
+
+    def iteration_stats(self):
+        """Per Picard iteration of the timed steps (swmmx_getIterationStats):
+        rows of (runs, conduits updated, nodes gathered, nodes updated,
+        relaxation-only updates, k_link ms, k_node ms)."""
+        import numpy as np
+        n = self.L.swmmx_getIterationStats(None, 0)
+        a = (ctypes.c_double * max(n, 1))()
+        self.L.swmmx_getIterationStats(a, n)
+        return np.array(a[:n]).reshape(-1, 7)
 
     def backend(self):
         buf = ctypes.create_string_buffer(256)
@@ -313,6 +326,16 @@ class SWMM:
                 return 1
         self._xchg = CB(tramp)
         return self.L.swmmx_setExchange(ctypes.cast(self._xchg, ctypes.c_void_p), None)
+
+    def partition_array(self, name: str):
+        """This rank's part of the partition (swmmx_getPartition)."""
+        import numpy as np
+        n = self.L.swmmx_getPartition(self._b(name), None, 0)
+        if n < 0:
+            raise KeyError(name)
+        a = (ctypes.c_int * max(n, 1))()
+        self.L.swmmx_getPartition(self._b(name), a, n)
+        return np.array(a[:n], dtype=np.int64)
 
     def owners(self, obj_type: int):
         import numpy as np

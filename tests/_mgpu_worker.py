@@ -4,7 +4,7 @@ Runs the engine on one rank of a partitioned network.  Transport:
   host  -- swmmx_setExchange with a gloo all-reduce callback (works with all
            ranks on one GPU, which RCCL refuses)
   rccl  -- RCCL (one rank only on a one-GPU box: exercises the captured
-           ncclAllReduce path)
+           ncclSend / ncclRecv and flag all-reduce path)
 Writes the owned part of the final state to an .npz.
 
 usage: python _mgpu_worker.py INP STEPS OUT.npz TRANSPORT     (env: RANK, WORLD_SIZE, MASTER_*)
@@ -52,8 +52,13 @@ def main():
     }
     for f in ("newDepth", "newVolume", "inflow", "outflow", "overflow"):
         res["node." + f] = s.get_array("node." + f)
-    for f in ("newFlow", "newDepth", "newVolume", "froude", "a1", "q1"):
+    for f in ("newFlow", "newDepth", "newVolume", "froude", "a1", "q1", "dqdh", "surfArea1", "surfArea2"):
         res["link." + f] = s.get_array("link." + f)
+    nN, nL = s.getCount(swmm5.NODE), s.getCount(swmm5.LINK)
+    P = s.get_array("node.newQual").size // max(nN, 1)
+    for q in range(P):                  # pollutant concentrations, one array per pollutant
+        res["node.qual%d" % q] = s.get_array("node.newQual").reshape(P, nN)[q].copy()
+        res["link.qual%d" % q] = s.get_array("link.newQual").reshape(P, nL)[q].copy()
     s.end()
     _, ferr, _ = s.getMassBalErr()
     res["flow_error"] = np.array([ferr])

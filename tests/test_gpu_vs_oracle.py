@@ -52,10 +52,28 @@ def _set_lat(o, q):
     lat = np.full(o.nN, q)
     lat[-1] = 0.0                     # netgen: DWF at every junction, none at the outfall
     o.d("node.latIn")[:] = lat
+    if o.nP:                          # netgen's pollutant DWF loads (concentrations 5, 10, 15, ...)
+        _set_loads(o, lat)
     return lat
 
 
+def _set_loads(o, lat):
+    """Pollutant mass loads of the grid's DWF in addDryWeatherInflows'
+    arithmetic order (routing.c:540-572): w = q*cDWF; w += q*c; w -= q*cDWF."""
+    conc = [5.0, 10.0, 15.0, 20.0, 25.0, 30.0]
+    qi = o.d("node.qualIn").reshape(o.nP, o.nN)
+    for p in range(o.nP):
+        w = np.where(lat > 0, lat * conc[p], 0.0)
+        w = np.where(lat > 0, w + lat * conc[p], 0.0)
+        w = np.where(lat > 0, w - lat * conc[p], 0.0)
+        qi[p] = w
+
+
 def _compare(s, o, what):
+    if o.nP:                          # pollutant concentrations (qualrout.c:100-142)
+        for f in ("node.newQual", "link.newQual"):
+            np.testing.assert_allclose(s.get_array(f), o.d(f), rtol=RTOL, atol=ATOL,
+                                       err_msg="%s %s" % (what, f))
     for f in NODE_F:
         np.testing.assert_allclose(s.get_array("node." + f), o.d("node." + f), rtol=RTOL, atol=ATOL,
                                    err_msg="%s node.%s" % (what, f))
@@ -81,16 +99,8 @@ def test_gpu_matches_oracle(nx, steps, kw, tmp_path):
     assert s.export_state(dump) == 0
     d = read_dump(dump)
     o = oracle_from_dump(d)
-    lat = _set_lat(o, kw.get("q", 0.02))
+    _set_lat(o, kw.get("q", 0.02))
     P = kw.get("pollutants", 0)
-    if P:
-        conc = [5.0, 10.0, 15.0]
-        qi = o.d("node.qualIn").reshape(P, o.nN)
-        for p in range(P):
-            w = np.where(lat > 0, lat * conc[p], 0.0)
-            w = np.where(lat > 0, w + lat * conc[p], 0.0)
-            w = np.where(lat > 0, w - lat * conc[p], 0.0)
-            qi[p] = w
     for k in range(steps):
         dt = o.routing_step(d["opt.d"][0])
         o.step(dt)
@@ -200,6 +210,25 @@ def test_surcharge_regime_window_60x60(tmp_path):
 
 
 @pytest.mark.gpu
+def test_max_trials_above_32(tmp_path):
+    """MAX_TRIALS is any non-negative integer in the reference (project.c:
+    724-727); the engine sizes its per-iteration flags from it.  A surcharged
+    60 x 60 grid with MAX_TRIALS 40 in a window against the oracle: steps run
+    more than 32 Picard iterations and every step matches at 1e-6."""
+    q, D = 0.3, 1.0
+    inp = str(tmp_path / "g.inp")
+    netgen.write_grid(inp, 60, 60, end_time="02:00:00", route_step=5.0, variable_step=0.75,
+                      diameter=D, q=q, extra_options=("MAX_TRIALS 40", "HEAD_TOLERANCE 0.0001"))
+    s = _engine(inp, tmp_path)
+    err, _ = s.run_steps(250)
+    assert err == 0
+    iters, sur, nonconv = _window(s, tmp_path, q, D, 20, 5.0)
+    assert iters.max() > 32 and sur.min() > 100, (iters, sur.min())
+    s.end()
+    s.close()
+
+
+@pytest.mark.gpu
 def test_frozen_junctions_bitwise(tmp_path, monkeypatch):
     """Frozen junctions (converged plain junctions whose conduits are all
     bypassed are not visited; their depth is advanced by the same relaxation
@@ -250,6 +279,61 @@ def test_benchmark_regime_window_707(tmp_path):
     assert err == 0
     iters, sur, nonconv = _window(s, tmp_path, cfg["q"], cfg["diameter"], 12, cfg["route_step"])
     assert sur.min() > 1000 and iters.mean() > 3.0, (sur.min(), iters)
+    s.end()
+    s.close()
+
+
+@pytest.mark.gpu
+def test_config1_100k_fixed_step_from_start(tmp_path):
+    """BASELINE configs[1] at its own size: bench.py's 100k workload (224 x 224
+    grid, 99,905 conduits, fixed 1 s routing step) from the initial state, 120
+    steps in lockstep with the oracle: the Picard iteration count of every step
+    equal, every node and link field compared at 1e-6 every step."""
+    import bench
+    cfg = bench.PRESETS["100k"]
+    inp = bench.make_inp(cfg["grid"], cfg["route_step"], cfg["variable_step"], cfg["pollutants"],
+                         cfg["diameter"], cfg["q"])
+    s = _engine(inp, tmp_path)
+    dump = str(tmp_path / "init.bin")
+    assert s.export_state(dump) == 0
+    d = read_dump(dump)
+    o = oracle_from_dump(d)
+    assert o.nL == 99905 and o.nN == 50177
+    _set_lat(o, cfg["q"])
+    iters = []
+    for k in range(120):
+        it = o.step(o.routing_step(cfg["route_step"]))
+        err, _ = s.step()
+        assert err == 0, s.getError()
+        c = s.counters()
+        assert c["last_iterations"] == it, (k, c["last_iterations"], it)
+        _compare(s, o, "100k step %d" % (k + 1))
+        iters.append(it)
+    assert c["nonconverged"] == o.get("nonConverge")
+    assert min(iters) >= 2 and np.mean(iters) >= 2.0, iters        # the configuration's regime
+    s.end()
+    s.close()
+
+
+@pytest.mark.gpu
+def test_config3_1m_quality_window(tmp_path):
+    """BASELINE configs[3] at its own size: bench.py's 1m_quality workload
+    (707 x 707 grid, 998,285 conduits, 3 pollutants with first-order decay,
+    variable step) after its 400-step spin-up: the next 12 steps of the engine
+    against the oracle continuing from the engine's own state (quality
+    included, qualrout.c:100-142), every step compared at 1e-6 -- pollutant
+    concentrations of every node and link included."""
+    import bench
+    cfg = bench.PRESETS["1m_quality"]
+    inp = bench.make_inp(cfg["grid"], cfg["route_step"], cfg["variable_step"], cfg["pollutants"],
+                         cfg["diameter"], cfg["q"])
+    s = _engine(inp, tmp_path)
+    err, _ = s.run_steps(cfg["spinup"])
+    assert err == 0
+    iters, sur, nonconv = _window(s, tmp_path, cfg["q"], cfg["diameter"], 12, cfg["route_step"])
+    assert sur.min() > 1000 and iters.mean() > 3.0, (sur.min(), iters)
+    c = s.get_array("node.newQual").reshape(3, -1)
+    assert (c > 1.0).mean() > 0.5, (c > 1.0).mean()                     # the loads have spread
     s.end()
     s.close()
 

@@ -25,7 +25,7 @@ for s in $STEPS; do
     tailab) for t in 0 1; do SWMM5_TAIL=$t run bench_tail$t 600 python bench.py --steps 200 --no-cpu; SWMM5_TAIL=$t run bench100k_tail$t 600 python bench.py --config 100k --steps 400 --no-cpu; done ;;
     bench100k) run bench100k 600 python bench.py --config 100k --steps 400 --no-cpu ;;
     benchall) for c in 100k 1m_fixed 1m_quality; do run bench_$c 600 python bench.py --config $c --no-cpu; done ;;
-    prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --no-cpu ;;
+    prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu ;;
     benchqual) run benchqual 600 python bench.py --config 1m_quality --steps 200 --no-cpu ;;
     bench4m) run bench4m 900 python bench.py --config 4m --steps 100 ;;
     mrehearse4m) run mrehearse4m 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --config 4m --steps 10 --warmup 2 --spinup 20 --exchange host --no-cpu ;;
@@ -35,8 +35,8 @@ for s in $STEPS; do
     gsweep) for g in ${GFACTORS:-0.34 0.67 2}; do SWMM5_GRID_FACTOR=$g run gsweep_$g 300 python bench.py --no-cpu; done ;;
     nsweep) for g in ${NFACTORS:-1 2 3}; do SWMM5_NODE_GRID_FACTOR=$g run nsweep_$g 300 python bench.py --no-cpu; done ;;
     sweep)  for w in 1 3 4 5; do SWMM5_LINK_WAVES=$w run sweep_w$w 300 python bench.py --steps 200 --no-cpu; done ;;
-    pmc)    run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 50 --warmup 20 --no-cpu \
-              && run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 50 --warmup 20 --no-cpu ;;
+    pmc)    run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --no-cpu \
+              && run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --no-cpu ;;
     calib)  run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/calib_fetch -o run -- ./tools/pmc_calib \
               && run calib_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/calib_write -o run -- ./tools/pmc_calib ;;
     sq)     run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD --output-format csv -d gpurun_out/pmc_sq -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu ;;

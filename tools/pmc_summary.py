@@ -87,7 +87,7 @@ def main():
             if col == 0:
                 per[name][2] += 1
     step_bytes = sum(a + b for a, b, _ in per.values()) / steps
-    first = per.get("k_link<true, 3, true>")
+    first = per.get("k_link<true, 3, true, false>") or per.get("k_link<true, 3, true>")
     first_launch = (first[0] + first[1]) / first[2] if first else None
     print("# PMC HBM traffic %s\n" % tag)
     print("Workload `%s`; timed window of %d steps after %d spin-up + %d warm-up steps "
@@ -109,6 +109,7 @@ def main():
         "bytes_per_launch": round(first_launch) if first_launch else None,
         "step_bytes": round(step_bytes),
         "iterations_per_step": ips,
+        "window": [spinup, warmup, steps],
         "calibration": {k: round(v, 4) for k, v in cal.items()},
         "src_sha": src_sha(),
         "source": "profiles/%s_pmc_summary.md (rocprofv3 FETCH_SIZE and WRITE_SIZE passes, "
