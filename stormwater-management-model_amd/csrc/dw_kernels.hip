@@ -13,8 +13,8 @@
 //                    outfall depth (link.c:728-766) and continuity/depth update
 //                    (setNodeDepth, dynwave.c:636-762); wave-level ballot of the
 //                    convergence test (dynwave.c:618) into one flag per iteration
-//   k_qual_node    pollutant advection at the nodes (qualrout.c:100-142); the
-//                  links' part runs in k_step_end's link pass (qualLink)
+//   k_qual_node    pollutant advection (qualrout.c:100-142): node mixing, then
+//                  each link updated by the thread of its upstream node
 //   k_step_end     capacity-limited links, outfall system outflow, flow totals
 //                  and Courant-step partials (dynwave.c:349-378, 799-921,
 //                  routing.c:841-925)
@@ -126,6 +126,7 @@ struct StepCtl {
     double routeStep;                 // fixed step (sec)
     unsigned tailBar;             // k_tail's grid-barrier arrivals (zeroed by k_link<first>)
     int tailErr;                  // k_tail gave up waiting at a barrier (never expected)
+    int qualPar;                  // quality buffer holding the latest concentrations (Params::nQual)
     double stepRed[kNumPartials];     // this step's reduced block partials (k_finalize)
     // run statistics (stats.c): report-period step count / span, max system
     // outfall flow, routing time-step statistics (stats_updateTimeStepStats)
@@ -180,6 +181,7 @@ struct Params {
     const double *crownElev;
     const int* rowptr;
     const int* csr;               // link index | (1<<31 if node is the link's node2)
+    const int* csrOther;          // per CSR entry: the link's other end node (-1: not held here)
     const int* outfallLink;       // per node: its single link (outfalls) or -1
     // node dynamic
     double *nNewDepth, *nOldDepth, *nNewVolume, *nOldVolume, *inflow, *outflow, *overflow;
@@ -228,8 +230,12 @@ struct Params {
     double *pUtil, *pAvg, *pVol, *pEnergy, *pOffLow, *pOffHigh, *pMin, *pMax;   // PumpStats, per link
     int *pStarts, *pPeriods;
     const double* latIn;          // lateral inflow for this step
-    // quality [p][object]
-    double *nOldQual, *nNewQual, *lOldQual, *lNewQual;
+    // quality [p][object], two buffers per object kind: during a step the
+    // previous step's concentrations are read from [qualPar] and the new ones
+    // written to [qualPar ^ 1]; k_finalize flips StepCtl::qualPar, so the
+    // reference's old <- new rotation (node_setOldQualState etc.) is free
+    double* nQual[2];
+    double* lQual[2];
     const double* qualIn;         // mass loads for this step [p][node]
     const double* kDecay;
     // misc
@@ -742,7 +748,8 @@ __device__ __forceinline__ void stageTables(double* ct, const double* g, int nGe
 
 // The step converged at iteration m (dynwave.c:249-251): the frozen junctions
 // take their depth at that last iteration (a step that runs all MaxTrials
-// iterations does this in its last node update)
+// iterations does this in its last node update).  Run by the first launch
+// after convergence.
 __device__ __forceinline__ void finalizeFrozen(const Params& p, int m, int tid, int nthr)
 {
     for (int i = tid; i < p.nN; i += nthr) {
@@ -753,6 +760,16 @@ __device__ __forceinline__ void finalizeFrozen(const Params& p, int m, int tid, 
         }
     }
 }
+// iterations run in this step (dynwave.c:242-257), from the per-iteration flags
+__device__ __forceinline__ int stepIterations(const Params& p, bool* converged)
+{
+    if (p.maxTrials <= 1) { *converged = false; return p.maxTrials < 1 ? 0 : 1; }
+    int steps = 2;
+    while (steps < p.maxTrials && p.unconv[steps - 1]) steps++;
+    *converged = (p.unconv[steps - 1] == 0);
+    return steps;
+}
+
 
 // Iterations k >= 2: a conduit is updated unless both end nodes have
 // converged (findBypassedLinks dynwave.c:335-345), i.e. exactly the conduits
@@ -771,16 +788,21 @@ __device__ __forceinline__ int linkListWalk(const Params& p, int k, int cnt, dou
         int u = list[t >> 2];
         int e1 = p.rowptr[u + 1];
         for (int e = p.rowptr[u] + (t & 3); e < e1; e += 4) {
-            int l = p.csr[e] & 0x7FFFFFFF;
+            // the entry names the link and (csrOther) its other end, so the
+            // end nodes' state loads in parallel with the link's own
+            const int ent = p.csr[e], v = p.csrOther[e];
+            const int l = ent & 0x7FFFFFFF;
+            if (v < 0) continue;                      // a ghost link (multi-GPU): its owner updates it
             uint32_t f = p.lflags[l];
+            const int2 nn = (ent < 0) ? make_int2(v, u) : make_int2(u, v);
+            const int f1 = p.frz[nn.x], f2 = p.frz[nn.y];
+            const int cv = p.conv[v];
             if (f & LF_COLD) continue;                // the cold conduits' loop
-            int2 nn = p.lnodes[l];
-            int v = (nn.x == u) ? nn.y : nn.x;
-            if (!p.conv[v] && v < u) continue;        // listed too: v takes it
-            double y1 = frozenDepth(p, nn.x, p.frz[nn.x], k - 1);
-            double y2 = frozenDepth(p, nn.y, p.frz[nn.y], k - 1);
+            if (!cv && v < u) continue;               // listed too: v takes it
+            double y1 = frozenDepth(p, nn.x, f1, k - 1);
+            double y2 = frozenDepth(p, nn.y, f2, k - 1);
             conduitFlow<false, false, kFast>(p, l, f, nn, k, dt, ct, y1, y2);
-            p.dirty[nn.x] = 1;
+            p.dirty[nn.x] = 1;                        // their sums are stale
             p.dirty[nn.y] = 1;
             work++;
         }
@@ -788,10 +810,6 @@ __device__ __forceinline__ int linkListWalk(const Params& p, int k, int cnt, dou
     return work;
 }
 
-// Streaming kernel: every conduit with LF_COLD clear (zero offsets, no outfall
-// end), one thread per conduit.  No calls, no root finders.
-// kWaves: minimum waves per SIMD the register allocator must allow (1 = no
-// constraint); selected at start-up (SWMM5_LINK_WAVES, default kLinkWavesDefault)
 // kProbe: a separately named instantiation for swmmx_timeKernel's
 // back-to-back measurement launches (same code)
 template <bool kFirst, int kWaves, bool kFast, bool kProbe = false>
@@ -920,8 +938,9 @@ __device__ __forceinline__ void coldConduits(const Params& p, int k, double dt, 
         uint32_t f = p.lflags[j];
         int2 nn = p.lnodes[j];
         if (k >= 2 && p.conv[nn.x] && p.conv[nn.y]) continue;
-        double y1 = frozenDepth(p, nn.x, (k >= 2) ? p.frz[nn.x] : 0, k - 1);
-        double y2 = frozenDepth(p, nn.y, (k >= 2) ? p.frz[nn.y] : 0, k - 1);
+        const int f1 = (k >= 2) ? p.frz[nn.x] : 0, f2 = (k >= 2) ? p.frz[nn.y] : 0;
+        double y1 = frozenDepth(p, nn.x, f1, k - 1);
+        double y2 = frozenDepth(p, nn.y, f2, k - 1);
         conduitFlow<kFirst, true>(p, j, f, nn, k, dt, ct, y1, y2);
         if (k >= 2) { p.dirty[nn.x] = 1; p.dirty[nn.y] = 1; }
     }
@@ -1069,19 +1088,55 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
 // the other networks use a node update without them.
 // prologue of the node update: outfall depths (link_setOutfallDepth,
 // findNodeDepths dynwave.c:605) from this iteration's link flows, on the
-// blocks with blockIdx.x * 64 < nOutLinks; ct = staged circular tables,
-// yc = 64 doubles of LDS
+// blocks with blockIdx.x * 64 < nOutLinks, 64 outfall conduits per block and
+// round.  Wave 0 finds their normal depths (one lane per conduit; the
+// small-flow circular case is an inherently serial Newton solve).  Waves 1-3
+// find their critical depths in groups of 32 lanes, one conduit per group:
+// the 26 critical flows of getYcritEnum's depth increments are evaluated one
+// per lane and the group's first lane runs the enumeration's search on them
+// (yCritEnumScan: the same values and operations as the serial search, which
+// evaluates up to 25 of them one after another).  Wave 0 then combines.
+// ct = staged circular tables; sh = OutfallLds scratch.
+struct OutfallLds {
+    double yc[64];
+    double qcs[6][32];
+};
 template <bool kFirst, bool kGeneral>
-__device__ __forceinline__ void outfallPrologue(const Params& p, const double* ct, double* yc)
+__device__ __forceinline__ void outfallPrologue(const Params& p, const double* ct, OutfallLds* sh)
 {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int base = blockIdx.x * 64; base < p.nOutLinks; base += gridDim.x * 64) {
+        const int nHere = (p.nOutLinks - base < 64) ? p.nOutLinks - base : 64;
         int c = base + lane;
         int j = (c < p.nOutLinks) ? p.outLinks[c] : -1;
         uint32_t f = (j >= 0) ? p.lflags[j] : 0u;
         double yn = 0.0;                               // non-conduits: yNorm = yCrit = 0
         if (j >= 0 && w == 0 && !(f & LF_NC)) yn = outfallPart<0, kGeneral>(p, j, f, ct);
-        if (j >= 0 && w == 1) yc[lane] = (f & LF_NC) ? 0.0 : outfallPart<1, kGeneral>(p, j, f, ct);
+        if (w >= 1) {
+            const int g = (threadIdx.x - 64) >> 5, gl = threadIdx.x & 31;    // 6 groups of 32 lanes
+            for (int m = g; m < nHere; m += 6) {
+                const int jj = p.outLinks[base + m];
+                const uint32_t ff = p.lflags[jj];
+                double ycv = 0.0;
+                if (!(ff & LF_NC)) {
+                    Geom x = loadGeom(p, jj, ff);
+                    double barrels = (double)((ff >> LF_BARREL_SHIFT) & 0xFF);
+                    double q = fabs(p.lNewFlow[jj] / barrels);
+                    double y0 = 0.0;
+                    if (yCritByEnum(x, q, &y0)) {
+                        if (gl <= 25) sh->qcs[g][gl] = qCritical<kGeneral>(x, gl * (x.yFull / 25.), 0.0, ct);
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        if (gl == 0) ycv = gmin(yCritEnumScan(x, q, y0, sh->qcs[g]), x.yFull);
+                        __builtin_amdgcn_wave_barrier();
+                    } else if (gl == 0) {
+                        ycv = getYcrit<kGeneral>(x, q, ct);
+                    }
+                }
+                if (gl == 0) sh->yc[m] = ycv;
+            }
+        }
         __syncthreads();
         if (j >= 0 && w == 0) {
             int2 nn = p.lnodes[j];
@@ -1089,9 +1144,21 @@ __device__ __forceinline__ void outfallPrologue(const Params& p, const double* c
             double prev = p.nNewDepth[o];
             if (kFirst) p.nOldDepth[o] = prev;             // node_setOldHydState before the update
             if (p.nNC) p.nPrevDepth[o] = prev;
-            p.nNewDepth[o] = outfallCombine(p, o, p.nflags[o], j, yn, yc[lane]);
+            p.nNewDepth[o] = outfallCombine(p, o, p.nflags[o], j, yn, sh->yc[lane]);
         }
         __syncthreads();
+    }
+}
+
+// Append i (where `me`) to a list: one atomic per wave
+__device__ __forceinline__ void waveAppend(bool me, int i, int* count, int* list)
+{
+    unsigned long long m = __ballot(me);
+    if (m) {
+        int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1, base = 0;
+        if (lane == leader) base = atomicAdd(count, __popcll(m));
+        base = __shfl(base, leader, 64);
+        if (me) list[base + __popcll(m & ((1ull << lane) - 1ull))] = i;
     }
 }
 
@@ -1246,15 +1313,7 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
         }
         }
         // list this iteration's unconverged nodes for the next k_link
-        if (!kFirst) {
-            unsigned long long m = __ballot(listMe);
-            if (m) {
-                int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1, base = 0;
-                if (lane == leader) base = atomicAdd(&p.ucount[k], __popcll(m));
-                base = __shfl(base, leader, 64);
-                if (listMe) ulist[base + __popcll(m & ((1ull << lane) - 1ull))] = i;
-            }
-        }
+        if (!kFirst) waveAppend(listMe, i, &p.ucount[k], ulist);
     }
     // one flag per iteration; any writer stores 1 (no atomics needed)
     if (__any(anyUnconv) && (threadIdx.x & 63) == 0) p.unconv[k] = 1;   // all-reduced over the ranks
@@ -1287,9 +1346,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
     // depths while wave 1 finds their critical depths, then wave 0 combines.
     if (blockIdx.x * 64 < p.nOutLinks) {
         __shared__ double ct[5 * SWX_CIRC_N];
-        __shared__ double yc[64];
+        __shared__ OutfallLds sh;
         stageTables(ct, p.gTables);
-        outfallPrologue<kFirst, kGeneral>(p, ct, yc);
+        outfallPrologue<kFirst, kGeneral>(p, ct, &sh);
     }
     nodePass<kFirst, kGeneral>(p, k, blockIdx.x * kBlock + threadIdx.x, gridDim.x * kBlock);
 }
@@ -1344,7 +1403,7 @@ template <bool kFast, bool kGeneral>
 __global__ __launch_bounds__(kBlock) void k_tail(Params p)
 {
     __shared__ double ct[kFast ? kCtFast : 5 * SWX_CIRC_N];
-    __shared__ double yc[64];
+    __shared__ OutfallLds sh;
     const int tid = blockIdx.x * kBlock + threadIdx.x, nthr = gridDim.x * kBlock;
     const double dt = p.ctl->dt;
     unsigned arrivals = 0;
@@ -1362,7 +1421,7 @@ __global__ __launch_bounds__(kBlock) void k_tail(Params p)
         if (!tailBarrier(p, arrivals)) return;
         // the every-shape root finders (the cold conduits' callees): calling
         // the lean ones would loosen their register budget, and k_node's
-        if (blockIdx.x * 64 < p.nOutLinks) outfallPrologue<false, true>(p, ct, yc);
+        if (blockIdx.x * 64 < p.nOutLinks) outfallPrologue<false, true>(p, ct, &sh);
         nodePass<false, kGeneral>(p, k, tid, nthr);
         arrivals += gridDim.x;
         if (!tailBarrier(p, arrivals)) return;
@@ -1408,18 +1467,18 @@ __global__ __launch_bounds__(kBlock) void k_xunpack(Params p, int k)
     }
 }
 // once per step, before the node quality: the ghost links' concentrations
-// (the owners' qualLink of the previous step end), P values each
+// (computed by their owners in the previous step), P values each
 __global__ __launch_bounds__(kBlock) void k_xpack_qual(Params p)
 {
     for (int e = blockIdx.x * kBlock + threadIdx.x; e < p.nSend; e += gridDim.x * kBlock)
         for (int q = 0; q < p.P; q++)
-            p.xsend[(size_t)p.P * e + q] = p.lNewQual[(size_t)q * p.nLs + p.sendLink[e]];
+            p.xsend[(size_t)p.P * e + q] = p.lQual[p.ctl->qualPar][(size_t)q * p.nLs + p.sendLink[e]];
 }
 __global__ __launch_bounds__(kBlock) void k_xunpack_qual(Params p)
 {
     for (int g = blockIdx.x * kBlock + threadIdx.x; g < p.nGhost; g += gridDim.x * kBlock)
         for (int q = 0; q < p.P; q++)
-            p.lNewQual[(size_t)q * p.nLs + p.nL + g] = p.xrecv[(size_t)p.P * g + q];
+            p.lQual[p.ctl->qualPar][(size_t)q * p.nLs + p.nL + g] = p.xrecv[(size_t)p.P * g + q];
 }
 
 // ---------------------------------------------------------------------------
@@ -1634,11 +1693,22 @@ __device__ __forceinline__ double reactedQual(double kDecay, double c, double tS
     return gmax(0.0, c2);
 }
 
-// qualrout.c:100-142 -- node part: link mass flows (findLinkMassFlow, link
-// order) + node quality (findNodeQual / findStorageQual); rotates node quality.
+// qualrout.c:100-142 in one pass over the nodes: each node's mass inflow
+// from its downstream-flowing links (findLinkMassFlow, link order), its new
+// quality (findNodeQual / findStorageQual), then the quality of every link
+// the node feeds (findLinkQual: a link's quality needs only its upstream
+// node's new quality and its own state, so the thread that has just computed
+// that node updates it; each link has exactly one upstream end).  Old values
+// are read from buffer [qualPar], new ones written to [qualPar ^ 1], so no
+// thread reads a concentration another one writes.
 __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
 {
     const double dt = p.ctl->dt;
+    const int par = p.ctl->qualPar;
+    const double* nOld = p.nQual[par];
+    double* nNew = p.nQual[par ^ 1];
+    const double* lOld = p.lQual[par];
+    double* lNew = p.lQual[par ^ 1];
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
         const double depth = p.nNewDepth[i];
         double qIn = p.inflow[i];
@@ -1656,7 +1726,7 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
         }
         // mass inflow of every pollutant in one pass over the node's links
         // (each pollutant's sum in link order, as qualrout.c:162-174 adds it)
-        double wq[kQualBatch];
+        double wq[kQualBatch], cn[kQualBatch];
         for (int p0 = 0; p0 < p.P; p0 += kQualBatch) {
         const int np = (p.P - p0 < kQualBatch) ? p.P - p0 : kQualBatch;
         for (int b = 0; b < np; b++) wq[b] = p.qualIn[(size_t)(p0 + b) * p.nN + i];
@@ -1668,14 +1738,13 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
             bool down = isN2 ? !(ql < 0.0) : (ql < 0.0);
             if (down) {
                 const double aq = fabs(ql);
-                for (int b = 0; b < np; b++) wq[b] += aq * p.lNewQual[(size_t)(p0 + b) * p.nLs + l];
+                for (int b = 0; b < np; b++) wq[b] += aq * lOld[(size_t)(p0 + b) * p.nLs + l];
             }
         }
         for (int b = 0; b < np; b++) {
             const int pp = p0 + b;
             size_t ni = (size_t)pp * p.nN + i;
-            double cOld = p.nNewQual[ni];           // node_setOldQualState
-            p.nOldQual[ni] = cOld;
+            double cOld = nOld[ni];                 // node_setOldQualState: old <- new (buffer flip)
             double w = wq[b];
             double c;
             if (isStorage || oldVol > 0.0353147) {
@@ -1687,50 +1756,45 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
             } else {
                 c = (depth > 0.003281) ? cOld : 0.0;
             }
-            p.nNewQual[ni] = c;
+            nNew[ni] = c;
+            cn[b] = c;
         }
-        }
-    }
-}
-
-// qualrout.c:253-353 (DW) -- quality of link j; rotates link quality.  Runs
-// in k_step_end's link pass (after k_qual_node), which reads the same link
-// state.
-__device__ __forceinline__ void qualLink(const Params& p, int j, uint32_t f, double dt)
-{
-    {
-        int2 nn = p.lnodes[j];
-        double nf = p.lNewFlow[j];
-        int up = (nf < 0.0) ? nn.y : nn.x;
-        if (f & LF_NC) {                      // non-conduit: upstream node's quality (qualrout.c:283-291)
-            for (int pp = 0; pp < p.P; pp++) {
-                size_t li = (size_t)pp * p.nLs + j;
-                p.lOldQual[li] = p.lNewQual[li];
-                p.lNewQual[li] = p.nNewQual[(size_t)pp * p.nN + up];
+        // findLinkQual (qualrout.c:253-353, DW) of the links this node feeds
+        for (int e = e0; e < e1; e++) {
+            int ent = p.qcsr[e];
+            int l = ent & 0x7FFFFFFF;
+            if (l >= p.nL) continue;                // a ghost link: its owner updates it
+            bool isN2 = ent < 0;
+            double ql = p.lNewFlow[l];
+            bool up = isN2 ? (ql < 0.0) : !(ql < 0.0);
+            if (!up) continue;
+            uint32_t f = p.lflags[l];
+            if (f & LF_NC) {                        // non-conduit: its upstream node's quality (qualrout.c:283-291)
+                for (int b = 0; b < np; b++) lNew[(size_t)(p0 + b) * p.nLs + l] = cn[b];
+                continue;
             }
-            return;
+            double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
+            double lq = fabs(p.q1[l]) * barrels;
+            double qSeep = p.seepLoss[l] * barrels;
+            double vEvap = p.evapLoss[l] * barrels * dt;
+            double v1 = p.lOldVolume[l], v2 = p.lNewVolume[l];
+            double vLosses = qSeep * dt + vEvap;
+            double fe = 1.0;
+            if (vEvap > 0.0 && v1 > 0.0353147) fe += vEvap / v1;
+            lq = lq + (v2 + vLosses - v1) / dt;
+            lq = gmax(lq, 0.0);
+            bool dry = (v2 < 0.0353147 || p.lNewDepth[l] <= 0.003281);
+            for (int b = 0; b < np; b++) {
+                const int pp = p0 + b;
+                size_t li = (size_t)pp * p.nLs + l;
+                double c1 = lOld[li] * fe;
+                double c2 = reactedQual(p.kDecay[pp], c1, dt);
+                double wIn = cn[b] * lq;
+                c2 = mixedQual(c2, v1, wIn, lq, dt);
+                if (dry) c2 = 0.0;
+                lNew[li] = c2;
+            }
         }
-        double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
-        double qIn = fabs(p.q1[j]) * barrels;
-        double qSeep = p.seepLoss[j] * barrels;
-        double vEvap = p.evapLoss[j] * barrels * dt;
-        double v1 = p.lOldVolume[j], v2 = p.lNewVolume[j];
-        double vLosses = qSeep * dt + vEvap;
-        double fEvap = 1.0;
-        if (vEvap > 0.0 && v1 > 0.0353147) fEvap += vEvap / v1;
-        qIn = qIn + (v2 + vLosses - v1) / dt;
-        qIn = gmax(qIn, 0.0);
-        bool dry = (v2 < 0.0353147 || p.lNewDepth[j] <= 0.003281);
-        for (int pp = 0; pp < p.P; pp++) {
-            size_t li = (size_t)pp * p.nLs + j;
-            double c1 = p.lNewQual[li];
-            p.lOldQual[li] = c1;
-            c1 *= fEvap;
-            double c2 = reactedQual(p.kDecay[pp], c1, dt);
-            double wIn = p.nNewQual[(size_t)pp * p.nN + up] * qIn;
-            c2 = mixedQual(c2, v1, wIn, qIn, dt);
-            if (dry) c2 = 0.0;
-            p.lNewQual[li] = c2;
         }
     }
 }
@@ -1804,20 +1868,13 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
     const bool stats = !(aDate < c->statsStart);
     // convergence of this step (dynwave.c:242-257): nodes count non-convergence
     bool converged;
-    int steps = p.maxTrials < 1 ? 0 : 1;
-    if (p.maxTrials <= 1) converged = false;
-    else {
-        steps = 2;
-        while (steps < p.maxTrials && p.unconv[steps - 1]) steps++;
-        converged = (p.unconv[steps - 1] == 0);
-    }
+    const int steps = stepIterations(p, &converged);
     const StatsDev& S = p.st;
     int n = gridDim.x * kBlock;
     int tid = blockIdx.x * kBlock + threadIdx.x;
     // links (fixed order within a thread: j = tid, tid + n, ...)
     for (int j = tid; j < p.nL; j += n) {
         uint32_t f = p.lflags[j];
-        if (p.P > 0) qualLink(p, j, f, dt);                // qualrout_execute's link part
         if (f & LF_NC) {                                   // stats_updateLinkStats, non-conduits
             if (!stats) continue;
             double newFlow = p.lNewFlow[j], oldFlow = p.lOldFlow[j];
@@ -1934,7 +1991,7 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
         } else {
             acc[2] += -q;
         }
-        double newDepth = p.nNewDepth[i];
+        const double newDepth = p.nNewDepth[i];
         if (type != OUTFALL)              // setNodeDepth's last dYdT (dynwave.c:750)
             p.dYdT[i] = fabs(newDepth - p.nOldDepth[i]) / dt;
         if (p.varStep && type != OUTFALL) {
@@ -1998,8 +2055,8 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
                 S.oMaxFlow[i] = gmax(S.oMaxFlow[i], inflow);
                 S.oPeriods[i] += 1;
             }
-            for (int pp = 0; pp < p.P; pp++)
-                S.oLoad[(size_t)pp * p.nN + i] += inflow * p.nNewQual[(size_t)pp * p.nN + i] * dt;
+            for (int pp = 0; pp < p.P; pp++)                // this step's concentrations (k_qual_node)
+                S.oLoad[(size_t)pp * p.nN + i] += inflow * p.nQual[c->qualPar ^ 1][(size_t)pp * p.nN + i] * dt;
             acc[7] += inflow;
         }
         double newLat = p.newLat[i];
@@ -2086,6 +2143,7 @@ __global__ void k_finalize(Params p)
     }
     c->lastSteps = steps;
     c->totalSteps += 1;
+    if (p.P > 0) c->qualPar ^= 1;                      // this step's concentrations become the latest
     c->totalIters += steps;
     if (!converged) c->nonConverge += 1;
     // mass balance: massbal_updateRoutingTotals(dt/2) at both ends of the step
@@ -2189,7 +2247,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_results(Params p, double f, dou
         x[5] = (float)z;
         for (int q = 0; q < p.P; q++) {
             size_t k = (size_t)q * p.nN + j;
-            z = f1 * p.nOldQual[k] + f * p.nNewQual[k];
+            z = f1 * p.nQual[p.ctl->qualPar ^ 1][k] + f * p.nQual[p.ctl->qualPar][k];
             x[6 + q] = (float)z;
         }
     }
@@ -2227,7 +2285,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_results(Params p, double f, dou
         x[4] = (float)c;
         for (int qq = 0; qq < p.P; qq++) {
             size_t k = (size_t)qq * p.nLs + j;
-            c = f1 * p.lOldQual[k] + f * p.lNewQual[k];
+            c = f1 * p.lQual[p.ctl->qualPar ^ 1][k] + f * p.lQual[p.ctl->qualPar][k];
             x[5 + qq] = (float)c;
         }
     }
@@ -2260,6 +2318,7 @@ struct Router::Impl {
     bool useGraph = true;
     bool timing = false;
     int gridL = 1, gridN = 1, gridEnd = 1, gridC = 1;
+    int gridLinkSparse = 1;          // k_link grid of iterations k >= 2 (unconverged-list walk)
     int linkWaves = kLinkWavesDefault;
     bool fastLinks = false;          // all streaming conduits circular, no SLOT
     bool general = false;            // storage units or non-basic shapes (k_node/k_step_end<.., true>)
@@ -2525,7 +2584,8 @@ static int launchIteration(Router::Impl* d, int k)
         (void)hipEventRecord(d->joinEv[k], d->side);
     }
     hipEvent_t e0 = d->timing ? d->curEv[4 * k] : nullptr, e1 = d->timing ? d->curHot[k] : nullptr;
-    launchTimed(d, linkKernel(k == 0, d->linkWaves, d->fastLinks), dim3(d->gridL), e0, e1, p, k);
+    launchTimed(d, linkKernel(k == 0, d->linkWaves, d->fastLinks), dim3(k >= 2 ? d->gridLinkSparse : d->gridL), e0,
+                e1, p, k);
     if (p.nCold) (void)hipStreamWaitEvent(d->stream, d->joinEv[k], 0);
     if (multi) {                                   // ghost links' values from their owners
         if (p.nSend) hipLaunchKernelGGL(k_xpack, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
@@ -2909,6 +2969,15 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         int* rp;
         UPI(rp, rowptr, nN + 1); p.rowptr = rp;
         UPI(rp, csr, csr.size()); p.csr = rp;
+        {
+            std::vector<int> other(csr.size(), -1);
+            for (int i = 0; i < nN; i++)
+                for (int e = rowptr[i]; e < rowptr[i + 1]; e++) {
+                    const int l = csr[e] & 0x7FFFFFFF;
+                    other[e] = (csr[e] < 0) ? nodes2[2 * l] : nodes2[2 * l + 1];
+                }
+            UPI(rp, other, other.size()); p.csrOther = rp;
+        }
         if (net.nNC > 0) {
             UPI(rp, qrowptr, nN + 1); p.qrowptr = rp;
             UPI(rp, qcsr, qcsr.size()); p.qcsr = rp;
@@ -3075,10 +3144,11 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         for (int q = 0; q < P; q++) kd[q] = net.pollut[q].kDecay;
         UPD(tmp, kd, kd.size()); p.kDecay = tmp;
         size_t nq = (size_t)std::max(P, 0);
-        UPD(p.nOldQual, gq(st.nOldQual, gN, LN), nq * nN);
-        UPD(p.nNewQual, gq(st.nNewQual, gN, LN), nq * nN);
-        UPD(p.lOldQual, gq(st.lOldQual, gL, LL), nq * nL);
-        UPD(p.lNewQual, gq(st.lNewQual, gL, LL), nq * nL);
+        // qualPar starts at 0: [0] holds the latest concentrations
+        UPD(p.nQual[0], gq(st.nNewQual, gN, LN), nq * nN);
+        UPD(p.nQual[1], gq(st.nOldQual, gN, LN), nq * nN);
+        UPD(p.lQual[0], gq(st.lNewQual, gL, LL), nq * nL);
+        UPD(p.lQual[1], gq(st.lOldQual, gL, LL), nq * nL);
     }
     // ---- tables, partials, control ---------------------------------------
     {
@@ -3122,6 +3192,13 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     double nodeFactor = 2.0;
     if (const char* g = getenv("SWMM5_NODE_GRID_FACTOR")) nodeFactor = atof(g);
     d->gridN = resident((const void*)nodeKernel(false, d->general), nN, nodeFactor);
+    // iterations k >= 2 walk short lists of unconverged nodes (a few thousand
+    // on the surcharged 1M grid): one workgroup per CU, measured faster than
+    // the streaming grid of three per CU (0.4658 vs 0.4686 ms/step); the
+    // grid-stride walk covers a long list too
+    d->gridLinkSparse = std::max(1, std::min(d->gridL, std::max(prop.multiProcessorCount, 1)));
+    if (const char* g = getenv("SWMM5_LINK_SPARSE_GRID_FACTOR"))
+        d->gridLinkSparse = std::max(1, std::min(d->gridL, (int)(atof(g) * std::max(prop.multiProcessorCount, 1))));
     d->gridC = std::max(1, std::min((p.nCold + kBlock - 1) / kBlock, maxBlocks));
     d->gridEnd = resident((const void*)stepEndKernel(d->fastLinks, d->allShapes),
                           std::max(nN, nL));
@@ -3324,10 +3401,14 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         //   dYdT (84), the volume totals and pending rates (r+w, 80), the node
         //   statistics avgDepth (r+w), maxDepth, newLat, oldLat, totLat (r+w),
         //   maxLat, maxInflow, maxOverflow, conv (96): 260 (conditional
-        //   updates of maxima and times not counted); with pollutants the
-        //   links' quality update (qualLink) runs here too: 72 + 24 P
-        d->kbytes[2] = L * (148.0 + (P ? 72 + 24.0 * P : 0.0)) + N * 260.0;
-        d->kbytes[3] = P ? (N * (24 + 16.0 * P) + E * (4 + 8 + 8.0 * P)) : 0.0;
+        //   updates of maxima and times not counted)
+        d->kbytes[2] = L * 148.0 + N * 260.0;
+        // quality (k_qual_node): per node depth inflow oldVolume newVolume
+        //   flags qrowptr 40 + loads, old and new concentration 24 P; per CSR
+        //   entry index 4 + newFlow 8 + a downstream link's concentration 8 P
+        //   (half the entries); per link its update: flags q1 seep evap
+        //   volumes depth 52, old and new concentration 16 P
+        d->kbytes[3] = P ? (N * (40 + 24.0 * P) + E * (12 + 4.0 * P) + L * (52 + 16.0 * P)) : 0.0;
     }
 
     // ---- capture the step graph ----------------------------------------------
@@ -3360,6 +3441,10 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         const char* tw = getenv("SWMM5_TAIL_PER_CU");
         int perCU = std::max(1, std::min(tw ? atoi(tw) : 1, occ - 1 > 0 ? occ - 1 : 1));
         d->tailGrid = (ok && occ >= 1 && cus > 0) ? perCU * cus : 0;
+        // a smaller resident grid (SWMM5_TAIL_GRID workgroups): fewer barrier
+        // arrivals when the iterations' lists are short
+        if (const char* tg = getenv("SWMM5_TAIL_GRID"))
+            if (d->tailGrid > 0 && atoi(tg) > 0) d->tailGrid = std::min(d->tailGrid, atoi(tg));
     }
     if (d->tailGrid > 0) {
         HIPCHECK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
@@ -3650,15 +3735,22 @@ int Router::download(Project& prj)
     HIPCHECK(dnL(st.seepLossRate, p.seepLoss));
     HIPCHECK(dnL(st.setting, p.setting));
     size_t P = p.P;
+    int qp = 0;                                     // the buffer holding the latest concentrations
+    if (P) {
+        HIPCHECK(hipMemcpyAsync(&d->hostCtl->qualPar, &d->ctl->qualPar, sizeof(int), hipMemcpyDeviceToHost,
+                                d->stream));
+        HIPCHECK(hipStreamSynchronize(d->stream));
+        qp = d->hostCtl->qualPar;
+    }
     if (P && !multi) {
         auto dn = [&](std::vector<double>& v, const double* src, size_t n) {
             v.resize(n);
             return hipMemcpyAsync(v.data(), src, n * sizeof(double), hipMemcpyDeviceToHost, d->stream);
         };
-        HIPCHECK(dn(st.nOldQual, p.nOldQual, P * nN));
-        HIPCHECK(dn(st.nNewQual, p.nNewQual, P * nN));
-        HIPCHECK(dn(st.lOldQual, p.lOldQual, P * nL));
-        HIPCHECK(dn(st.lNewQual, p.lNewQual, P * nL));
+        HIPCHECK(dn(st.nOldQual, p.nQual[qp ^ 1], P * nN));
+        HIPCHECK(dn(st.nNewQual, p.nQual[qp], P * nN));
+        HIPCHECK(dn(st.lOldQual, p.lQual[qp ^ 1], P * nL));
+        HIPCHECK(dn(st.lNewQual, p.lQual[qp], P * nL));
     } else if (P) {                                 // owned nodes / links to their global slots
         const size_t gN = prj.net.nNodes(), gL = prj.net.nLinks(), nLs = p.nLs;
         auto qn = [&](std::vector<double>& v, const double* src) -> hipError_t {
@@ -3678,10 +3770,10 @@ int Router::download(Project& prj)
                 for (size_t j = 0; j < nL; j++) v[q * gL + part.llink[j]] = tmp[q * nLs + j];
             return r;
         };
-        HIPCHECK(qn(st.nOldQual, p.nOldQual));
-        HIPCHECK(qn(st.nNewQual, p.nNewQual));
-        HIPCHECK(ql(st.lOldQual, p.lOldQual));
-        HIPCHECK(ql(st.lNewQual, p.lNewQual));
+        HIPCHECK(qn(st.nOldQual, p.nQual[qp ^ 1]));
+        HIPCHECK(qn(st.nNewQual, p.nQual[qp]));
+        HIPCHECK(ql(st.lOldQual, p.lQual[qp ^ 1]));
+        HIPCHECK(ql(st.lNewQual, p.lQual[qp]));
     }
     std::vector<int> ls(nL), cv(nN);
     HIPCHECK(hipMemcpyAsync(ls.data(), p.lstate, nL * sizeof(int), hipMemcpyDeviceToHost, d->stream));

@@ -954,6 +954,56 @@ SWX_HD_COLD double yCritEnum(const Geom& x, double q, double y0, const double* c
     return yc;
 }
 
+// yCritEnum's search (xsect.c:1634-1696) over the critical flows qcs[i] =
+// qCritical(i * yFull / 25) of all 26 depth increments, evaluated beforehand
+// (in parallel, one lane per increment): the same operations on the same
+// values, so the same critical depth
+SWX_HD double yCritEnumScan(const Geom& x, double q, double y0, const double* qcs)
+{
+    double dy = x.yFull / 25., yc, qc;
+    int i1 = (int)(y0 / dy);
+    double q0 = qcs[i1];
+    if (q0 < q) {
+        yc = x.yFull;
+        for (int i = i1 + 1; i <= 25; i++) {
+            qc = qcs[i];
+            if (qc >= q) {
+                yc = ((q - q0) / (qc - q0) + ((double)i - 1)) * dy;
+                break;
+            }
+            q0 = qc;
+        }
+    } else {
+        yc = 0.0;
+        for (int i = i1 - 1; i >= 0; i--) {
+            qc = qcs[i];
+            if (qc < q) {
+                yc = ((q - qc) / (q0 - qc) + (double)i) * dy;
+                break;
+            }
+            q0 = qc;
+        }
+    }
+    return yc;
+}
+// getYcrit takes the enumeration branch (xsect.c:1297-1312): its starting
+// estimate y0 is returned in *y0
+SWX_HD bool yCritByEnum(const Geom& x, double q, double* y0)
+{
+    double q2g = (q * q) / 32.2;
+    if (q2g == 0.0) return false;
+    switch (x.type) {
+    case G_DUMMY: case G_RECT_OPEN: case G_RECT_CLOSED: case G_TRIANGULAR: case G_PARABOLIC: case G_POWERFUNC:
+        return false;
+    default: break;
+    }
+    double y = 1.01 * pow(q2g / x.yFull, 1. / 4.);
+    if (y >= x.yFull) y = 0.97 * x.yFull;
+    double r = x.aFull / (3.141592654 / 4.0 * (x.yFull * x.yFull));
+    *y0 = y;
+    return r >= 0.5 && r <= 2.0;
+}
+
 // xsect.c:1700-1748 with findroot_Ridder (findroot.c:90-138)
 template <bool kAll = true>
 SWX_HD_COLD double yCritRidder(const Geom& x, double q, double y0, const double* ct)

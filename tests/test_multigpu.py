@@ -328,7 +328,7 @@ def _assert_bitwise(parts, one):
     # between ranks 1 and 2 must still keep rank 0 iterating
     (dict(route_step=5.0, variable_step=0.75, diameter=1.0, q=0.5), 250, True, 3),
     # water quality (qualrout): ghost links' concentrations move once per step
-    (dict(route_step=5.0, variable_step=0.75, diameter=1.0, q=0.3, pollutants=3), 200, True, 2)])
+    (dict(route_step=5.0, variable_step=0.75, diameter=1.0, q=0.5, pollutants=3), 250, True, 2)])
 def test_ranks_match_one_gpu_bitwise(kw, steps, surcharged, world, tmp_path):
     """Every held node is summed over all its links in the reference's order
     on every rank (ghost links exchanged between neighbours), so the
