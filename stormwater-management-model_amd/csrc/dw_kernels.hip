@@ -56,6 +56,12 @@ namespace swx {
     } while (0)
 
 constexpr int kBlock = 256;
+// phase probe slots per Picard iteration (Params::probe): link entry (min),
+// link exit, link exit of workgroups with list work, node entry (min), last
+// node workgroup's entry, block 0's outfall prologue end, node exit, node
+// exit of block 0
+enum { PR_L_IN = 0, PR_L_OUT, PR_L_WORK, PR_N_IN, PR_N_LAST_IN, PR_N_PRO, PR_N_OUT, PR_N_B0,
+       PR_P_STAGED, PR_P_YN, PR_P_YC, PR_L_SCAN, PR_L_STAGED, kProbeSlots };
 // per-block partials written by k_step_end: [0] outflow [1] flooding [2] extra
 // external inflow [3] evap [4] seep (sums), [5] link Courant step [6] node
 // Courant step (min, with their first-occurrence indices in [8] [9]),
@@ -271,12 +277,20 @@ struct Params {
     // (not frozen), relaxation-only node updates
     int* unconv;
     int* ucount;
+    int2* ulistRow;               // [2][nN] each listed node's CSR row bounds (rowptr[u], rowptr[u + 1])
     unsigned long long* work;
+    // phase probe (SWMM5_PROBE=1, timing mode only; null otherwise): per
+    // iteration k, kProbeSlots wall-clock stamps (probeMark)
+    unsigned long long* probe;    // [k][slot][probeBlocks]
+    int probeBlocks;
     double* hostDt;               // host-mapped rings: per-step dt (Router::launchedDt), then
                                   // the Picard iterations each step ran (auto k_tail choice)
     int nCold, nOutLinks;
     const int* coldLinks;         // LF_COLD conduits, ascending
     const int* outLinks;          // conduits with an outfall end, ascending
+    int outInl0, outInl1, outInl2, outInl3;   // outLinks[0..3] (-1: none), read without a load
+    const double* ofQcs;          // [nOutLinks][26] their critical flows at the enumeration's
+                                  // depths i yFull / 25 (static geometry: k_outfall_qcs at init)
     StepCtl* ctl;
 };
 
@@ -397,14 +411,15 @@ __device__ double conduitLossRate(const Params& p, int j, const Geom& x, double 
 // advances by the relaxation of setNodeDepth's plain branch (dynwave.c:
 // 700-715, omega = 0.5, yNew = yOld + dV / surfArea = yRaw unchanged), the
 // same operations the live update would have made
+__device__ __forceinline__ double frozenDepthV(double y, double yr, int fz, int m)
+{
+    if (fz)
+        for (int j = fz - 1; j < m; j++) y = (1.0 - 0.5) * y + 0.5 * yr;
+    return y;
+}
 __device__ __forceinline__ double frozenDepth(const Params& p, int i, int fz, int m)
 {
-    double y = p.nNewDepth[i];
-    if (fz) {
-        const double yr = p.yRaw[i];
-        for (int j = fz - 1; j < m; j++) y = (1.0 - 0.5) * y + 0.5 * yr;
-    }
-    return y;
+    return frozenDepthV(p.nNewDepth[i], fz ? p.yRaw[i] : 0.0, fz, m);
 }
 
 // dwflow.c:297-413.  kCold = false is the specialisation for links with both
@@ -771,36 +786,51 @@ __device__ __forceinline__ int stepIterations(const Params& p, bool* converged)
 }
 
 
+// measurement only: thread 0 stamps the wall clock into probe slot `slot` of
+// iteration k
+// (per workgroup: no atomics, whose serialisation would be what is measured;
+// the host takes the minimum or maximum over the workgroups)
+__device__ __forceinline__ void probeMark(const Params& p, int k, int slot, unsigned who = 0)
+{
+    if (p.probe && threadIdx.x == who && blockIdx.x < (unsigned)p.probeBlocks)
+        p.probe[((size_t)kProbeSlots * k + slot) * p.probeBlocks + blockIdx.x] = (unsigned long long)wall_clock64();
+}
+
 // Iterations k >= 2: a conduit is updated unless both end nodes have
 // converged (findBypassedLinks dynwave.c:335-345), i.e. exactly the conduits
 // incident to the nodes the node update listed as unconverged in the previous
 // iteration (outfalls are always listed).  Four threads per listed node walk
-// its CSR row; a conduit whose ends are both listed is taken by the
-// lower-numbered end.  cnt = the number of listed nodes; ct = staged tables.
+// its CSR row, whose bounds came with the list entry; a conduit whose ends
+// are both listed is taken by the lower-numbered end.  cnt = the number of
+// listed nodes; ct = staged tables.
 template <bool kFast>
 __device__ __forceinline__ int linkListWalk(const Params& p, int k, int cnt, double dt, const double* ct,
                                             int tid, int nthr)
 {
     const int* list = p.ulist + (size_t)((k - 1) & 1) * p.nN;
+    const int2* rows = p.ulistRow + (size_t)((k - 1) & 1) * p.nN;
     const int slots = 4 * cnt;
     int work = 0;
     for (int t = tid; t < slots; t += nthr) {
-        int u = list[t >> 2];
-        int e1 = p.rowptr[u + 1];
-        for (int e = p.rowptr[u] + (t & 3); e < e1; e += 4) {
+        const int u = list[t >> 2];
+        const int2 rb = rows[t >> 2];
+        for (int e = rb.x + (t & 3); e < rb.y; e += 4) {
             // the entry names the link and (csrOther) its other end, so the
-            // end nodes' state loads in parallel with the link's own
-            const int ent = p.csr[e], v = p.csrOther[e];
+            // end nodes' state loads in parallel with the link's own; the
+            // filters' operands and both end depths load together
+            const int ent = p.csr[e], o = p.csrOther[e];
             const int l = ent & 0x7FFFFFFF;
-            if (v < 0) continue;                      // a ghost link (multi-GPU): its owner updates it
-            uint32_t f = p.lflags[l];
-            const int2 nn = (ent < 0) ? make_int2(v, u) : make_int2(u, v);
+            if (o < 0) continue;                      // a ghost link (multi-GPU): its owner updates it
+            const int2 nn = (ent < 0) ? make_int2(o, u) : make_int2(u, o);
+            const uint32_t f = p.lflags[l];
             const int f1 = p.frz[nn.x], f2 = p.frz[nn.y];
-            const int cv = p.conv[v];
+            const int cv = p.conv[o];
+            const double d1 = p.nNewDepth[nn.x], d2 = p.nNewDepth[nn.y];
+            const double r1 = p.yRaw[nn.x], r2 = p.yRaw[nn.y];
             if (f & LF_COLD) continue;                // the cold conduits' loop
-            if (!cv && v < u) continue;               // listed too: v takes it
-            double y1 = frozenDepth(p, nn.x, f1, k - 1);
-            double y2 = frozenDepth(p, nn.y, f2, k - 1);
+            if (!cv && o < u) continue;               // listed too: o takes it
+            double y1 = frozenDepthV(d1, r1, f1, k - 1);
+            double y2 = frozenDepthV(d2, r2, f2, k - 1);
             conduitFlow<false, false, kFast>(p, l, f, nn, k, dt, ct, y1, y2);
             p.dirty[nn.x] = 1;                        // their sums are stale
             p.dirty[nn.y] = 1;
@@ -823,6 +853,7 @@ void k_link(Params p, int k)
         return;
     }
     __shared__ double ct[kFast ? kCtFast : 5 * SWX_CIRC_N];
+    probeMark(p, k, PR_L_IN);
     double dt = p.ctl->dt;
     int work = 0;
     if (kFirst && blockIdx.x == 0)
@@ -840,9 +871,12 @@ void k_link(Params p, int k)
         const int cnt = p.ucount[k - 1];
         if (blockIdx.x * kBlock < 4 * cnt) {                // uniform per block
             stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
+            probeMark(p, k, PR_L_STAGED);
             work = linkListWalk<kFast>(p, k, cnt, dt, ct, tid, nthr);
+            probeMark(p, k, PR_L_WORK);
         }
     }
+    probeMark(p, k, PR_L_OUT);
     // measurement only (eager timing launches, iterations >= 2 where links can
     // be bypassed): one atomic per workgroup after an LDS reduction
     if (k >= 2 && p.countWork) {
@@ -858,19 +892,6 @@ void k_link(Params p, int k)
     }
 }
 
-// link_setOutfallDepth + outfall_setOutletDepth (link.c:728-766, node.c:1413-1492),
-// in two halves that can run on different waves: the normal depth (kPart 0)
-// and the critical depth (kPart 1) of the outfall conduit's flow, then the
-// outlet depth from both (outfallCombine)
-template <int kPart, bool kAll>
-__device__ __forceinline__ double outfallPart(const Params& p, int j, uint32_t f, const double* ct)
-{
-    Geom x = loadGeom(p, j, f);
-    double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
-    double q = fabs(p.lNewFlow[j] / barrels);
-    if (kPart == 0) return linkYnorm<kAll>(x, q, p.qMax[j], p.beta[j], ct);
-    return getYcrit<kAll>(x, q, ct);
-}
 // table_lookup (table.c:395-426) and table_tseriesLookup with extend = TRUE
 // (table.c:745-804) on (x, y) pairs: first / last value outside the range,
 // linear interpolation (tableInterp, storage.h) inside
@@ -1092,8 +1113,9 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
 // round.  Wave 0 finds their normal depths (one lane per conduit; the
 // small-flow circular case is an inherently serial Newton solve).  Waves 1-3
 // find their critical depths in groups of 32 lanes, one conduit per group:
-// the 26 critical flows of getYcritEnum's depth increments are evaluated one
-// per lane and the group's first lane runs the enumeration's search on them
+// the 26 critical flows at getYcritEnum's depth increments (geometry only,
+// tabulated at init by k_outfall_qcs) are loaded one per lane and the group's
+// first lane runs the enumeration's search on them
 // (yCritEnumScan: the same values and operations as the serial search, which
 // evaluates up to 25 of them one after another).  Wave 0 then combines.
 // ct = staged circular tables; sh = OutfallLds scratch.
@@ -1101,84 +1123,151 @@ struct OutfallLds {
     double yc[64];
     double qcs[6][32];
 };
+__device__ __forceinline__ int outLinkAt(const Params& p, int c)
+{
+    // the first four from the kernel arguments: no load before the conduit's own
+    if (c < 4) return c == 0 ? p.outInl0 : c == 1 ? p.outInl1 : c == 2 ? p.outInl2 : p.outInl3;
+    return p.outLinks[c];
+}
+// link_setOutfallDepth + outfall_setOutletDepth (link.c:728-766,
+// node.c:1413-1492): the normal and the critical depth of each outfall
+// conduit's flow on different waves, then the outlet depth from both
+// (outfallCombine).  stage: the tables are staged into ct here, after the
+// first round's operand loads are issued (they then travel together)
 template <bool kFirst, bool kGeneral>
-__device__ __forceinline__ void outfallPrologue(const Params& p, const double* ct, OutfallLds* sh)
+__device__ __forceinline__ void outfallPrologue(const Params& p, double* ct, OutfallLds* sh, bool stage,
+                                                int kProbeK = 0)
 {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = (threadIdx.x - 64) >> 5, gl = threadIdx.x & 31;    // waves 1-3: 6 groups of 32 lanes
     for (int base = blockIdx.x * 64; base < p.nOutLinks; base += gridDim.x * 64) {
         const int nHere = (p.nOutLinks - base < 64) ? p.nOutLinks - base : 64;
-        int c = base + lane;
-        int j = (c < p.nOutLinks) ? p.outLinks[c] : -1;
-        uint32_t f = (j >= 0) ? p.lflags[j] : 0u;
+        // wave 0: lane's outfall conduit (normal depth, then the outlet
+        // depth); waves 1-3: their group's first conduit (critical depth)
+        const int c = (w == 0) ? lane : g;
+        const int j = (c < nHere) ? outLinkAt(p, base + c) : -1;
+        const uint32_t f = (j >= 0) ? p.lflags[j] : 0u;
+        const bool cond = (j >= 0) && !(f & LF_NC);
+        Geom x = {};
+        double q = 0.0, qMax = 0.0, beta = 0.0;
+        int o = -1;
+        double prev = 0.0;
+        uint32_t nfo = 0;
+        if (cond) {
+            x = loadGeom(p, j, f);
+            q = fabs(p.lNewFlow[j] / (double)((f >> LF_BARREL_SHIFT) & 0xFF));
+            if (w == 0) { qMax = p.qMax[j]; beta = p.beta[j]; }
+        }
+        if (j >= 0 && w == 0) {                        // the outlet node's operands
+            const int2 nn = p.lnodes[j];
+            o = (f & LF_N2_OUTFALL) ? nn.y : nn.x;     // link.c:743-753 (node2 first)
+            prev = p.nNewDepth[o];
+            nfo = p.nflags[o];
+        }
+        if (stage) { stageTables(ct, p.gTables); stage = false; }
+        if (base == 0) probeMark(p, kProbeK, PR_P_STAGED);
         double yn = 0.0;                               // non-conduits: yNorm = yCrit = 0
-        if (j >= 0 && w == 0 && !(f & LF_NC)) yn = outfallPart<0, kGeneral>(p, j, f, ct);
+        if (w == 0 && cond) yn = linkYnorm<kGeneral>(x, q, qMax, beta, ct);
+        if (base == 0) probeMark(p, kProbeK, PR_P_YN);
         if (w >= 1) {
-            const int g = (threadIdx.x - 64) >> 5, gl = threadIdx.x & 31;    // 6 groups of 32 lanes
             for (int m = g; m < nHere; m += 6) {
-                const int jj = p.outLinks[base + m];
-                const uint32_t ff = p.lflags[jj];
+                uint32_t ff = f;
+                double qq = q;
+                Geom xx = x;
+                bool cc = cond;
+                if (m != g) {                          // later conduits of the group
+                    const int jj = outLinkAt(p, base + m);
+                    ff = p.lflags[jj];
+                    cc = !(ff & LF_NC);
+                    if (cc) {
+                        xx = loadGeom(p, jj, ff);
+                        qq = fabs(p.lNewFlow[jj] / (double)((ff >> LF_BARREL_SHIFT) & 0xFF));
+                    }
+                }
                 double ycv = 0.0;
-                if (!(ff & LF_NC)) {
-                    Geom x = loadGeom(p, jj, ff);
-                    double barrels = (double)((ff >> LF_BARREL_SHIFT) & 0xFF);
-                    double q = fabs(p.lNewFlow[jj] / barrels);
+                if (cc) {
                     double y0 = 0.0;
-                    if (yCritByEnum(x, q, &y0)) {
-                        if (gl <= 25) sh->qcs[g][gl] = qCritical<kGeneral>(x, gl * (x.yFull / 25.), 0.0, ct);
+                    if (yCritByEnum(xx, qq, &y0)) {
+                        if (gl <= 25) sh->qcs[g][gl] = p.ofQcs[26 * (base + m) + gl];
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                         __builtin_amdgcn_wave_barrier();
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                        if (gl == 0) ycv = gmin(yCritEnumScan(x, q, y0, sh->qcs[g]), x.yFull);
+                        if (gl == 0) ycv = gmin(yCritEnumScan(xx, qq, y0, sh->qcs[g]), xx.yFull);
                         __builtin_amdgcn_wave_barrier();
                     } else if (gl == 0) {
-                        ycv = getYcrit<kGeneral>(x, q, ct);
+                        ycv = getYcrit<kGeneral>(xx, qq, ct);
                     }
                 }
                 if (gl == 0) sh->yc[m] = ycv;
             }
+            if (base == 0) probeMark(p, kProbeK, PR_P_YC, 64);
         }
         __syncthreads();
         if (j >= 0 && w == 0) {
-            int2 nn = p.lnodes[j];
-            int o = (f & LF_N2_OUTFALL) ? nn.y : nn.x;    // link.c:743-753 (node2 first)
-            double prev = p.nNewDepth[o];
             if (kFirst) p.nOldDepth[o] = prev;             // node_setOldHydState before the update
             if (p.nNC) p.nPrevDepth[o] = prev;
-            p.nNewDepth[o] = outfallCombine(p, o, p.nflags[o], j, yn, sh->yc[lane]);
+            p.nNewDepth[o] = outfallCombine(p, o, nfo, j, yn, sh->yc[lane]);
         }
         __syncthreads();
     }
 }
 
-// Append i (where `me`) to a list: one atomic per wave
-__device__ __forceinline__ void waveAppend(bool me, int i, int* count, int* list)
+// Append i (where `me`) with its CSR row bounds to a list: one atomic per
+// wave.  (Per-chunk segments without atomics were measured slower on the
+// surcharged 1M grid: its unconverged nodes are clustered, so the adds are
+// few, and the walk over segments could not pack them as tightly.)
+__device__ __forceinline__ void waveAppend(bool me, int i, int2 row, int* count, int* list, int2* rows)
 {
     unsigned long long m = __ballot(me);
     if (m) {
         int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1, base = 0;
         if (lane == leader) base = atomicAdd(count, __popcll(m));
         base = __shfl(base, leader, 64);
-        if (me) list[base + __popcll(m & ((1ull << lane) - 1ull))] = i;
+        if (me) {
+            const int e = base + __popcll(m & ((1ull << lane) - 1ull));
+            list[e] = i;
+            rows[e] = row;
+        }
     }
 }
 
-// findNodeDepths (dynwave.c:593-626) over the node index space (tid, nthr),
-// plus the unconverged-node list of iteration k and its convergence flag
+// end of a node pass: the iteration's convergence flag (one per iteration;
+// any writer stores 1, no atomics needed; all-reduced over the ranks) and the
+// measurement counters
+__device__ __forceinline__ void nodePassEnd(const Params& p, int k, bool anyUnconv, int gathered, int live, int fast,
+                                            bool counted)
+{
+    if (__any(anyUnconv) && (threadIdx.x & 63) == 0) p.unconv[k] = 1;
+    if (counted && p.countWork) {                          // measurement only
+        for (int off = 32; off > 0; off >>= 1) {
+            gathered += __shfl_down(gathered, off, 64);
+            live += __shfl_down(live, off, 64);
+            fast += __shfl_down(fast, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            if (gathered) atomicAdd(&p.work[p.maxTrials + k], (unsigned long long)gathered);
+            if (live) atomicAdd(&p.work[2 * p.maxTrials + k], (unsigned long long)live);
+            if (fast) atomicAdd(&p.work[3 * p.maxTrials + k], (unsigned long long)fast);
+        }
+    }
+}
+
+// One node of findNodeDepths (dynwave.c:593-626) at iteration k: the
+// frozen-junction and relaxation shortcuts (k >= 2), the CSR gather and
+// setNodeDepth.  listMe: unconverged after this iteration (outfalls always);
+// row: its CSR row bounds for the next link walk.  gathered / live / fast:
+// measurement counters (countWork).
 template <bool kFirst, bool kGeneral>
-__device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nthr)
+__device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double dt, bool& listMe, int2& row,
+                                         bool& anyUnconv, int& gathered, int& live, int& fast)
 {
     constexpr bool kStorage = kGeneral;
-    const double dt = p.ctl->dt;
-    bool anyUnconv = false;
-    int gathered = 0, live = 0, fast = 0;          // measurement only (countWork)
-    int* ulist = p.ulist + (size_t)(k & 1) * p.nN;
-    for (int i = tid; i < p.nN; i += nthr) {
         uint32_t nf = p.nflags[i];
         int type = (int)(nf & NF_TYPE);
         // an outfall's depth is written by the prologue above: not read here
         double yLast = 0.0;
         bool haveYLast = false;
-        bool listMe = (type == OUTFALL);       // unconverged after this iteration
+        listMe = (type == OUTFALL);
         bool done = false, isFast = false;
         if (!kFirst && k >= 2) {
             unsigned char cache = p.dirty[i];
@@ -1203,6 +1292,7 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
                 // plain clean junction: the relaxation step of setNodeDepth
                 // (dynwave.c:700-715) on the cached unrelaxed depth
                 double yLast2 = p.nNewDepth[i], yCrown = p.yCrown[i], yRaw = p.yRaw[i], yMax = p.yMaxNP[i];
+                row = make_int2(p.rowptr[i], p.rowptr[i + 1]);
                 bool sur = p.surchargeMethod == SUR_EXTRAN && yCrown > 0.0 && yLast2 > yCrown;
                 if (!sur) {
                     const double omega = 0.5;
@@ -1224,6 +1314,10 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
         if (!done || isFast) live++;
         if (isFast) fast++;
         if (!done) {
+        // the CSR row bounds load with the node's own state (not after the
+        // reuse test): one dependent round trip fewer before the gather
+        const int e0 = p.rowptr[i], e1 = p.rowptr[i + 1];
+        row = make_int2(e0, e1);
         if (!haveYLast) yLast = (type == OUTFALL) ? 0.0 : p.nNewDepth[i];
         double yOld, lat;
         if (kFirst) {
@@ -1269,31 +1363,52 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
             if (lat >= 0.0) inflow += lat;
             else outflow -= lat;
             sumdqdh = 0.0;
-            // CSR gather in link-index order == updateNodeFlows serial order
-            int e0 = p.rowptr[i], e1 = p.rowptr[i + 1];
-            for (int e = e0; e < e1; e++) {
-                int ent = p.csr[e];
-                int l = ent & 0x7FFFFFFF;
-                bool isN2 = ent < 0;
-                double q = p.lNewFlow[l];
-                uint32_t lf = p.lflags[l];
-                double barrels = (double)((lf >> LF_BARREL_SHIFT) & 0xFF);
-                if (!isN2) {
-                    if (q >= 0.0) outflow += q; else inflow -= q;
-                } else {
-                    if (q >= 0.0) inflow += q; else outflow -= q;
-                }
-                if (lf & LF_SEEP) {
-                    double lossRate = (p.evapLoss[l] + p.seepLoss[l]) * barrels;
-                    if (lossRate > 0.0) {
-                        bool o1 = (lf & LF_N1_OUTFALL) != 0, o2 = (lf & LF_N2_OUTFALL) != 0;
-                        if (!o1 && !o2) lossRate /= 2.0;
-                        if (!isN2 && !o1) outflow += lossRate;
-                        if (isN2 && !o2) outflow += lossRate;
+            // CSR gather in link-index order == updateNodeFlows serial order,
+            // kGather entries at a time: their CSR words, then all their link
+            // values, are loaded together before the in-order sums (a row
+            // walked one entry at a time is two dependent loads per entry)
+            constexpr int kGather = 4;
+            for (int eb = e0; eb < e1; eb += kGather) {
+                int ent[kGather];
+                double qv[kGather], sav[kGather], dqv[kGather];
+                uint32_t lfv[kGather];
+#pragma unroll
+                for (int t = 0; t < kGather; t++) ent[t] = (eb + t < e1) ? p.csr[eb + t] : 0;
+#pragma unroll
+                for (int t = 0; t < kGather; t++) {
+                    if (eb + t < e1) {
+                        const int l = ent[t] & 0x7FFFFFFF;
+                        qv[t] = p.lNewFlow[l];
+                        lfv[t] = p.lflags[l];
+                        sav[t] = (ent[t] < 0) ? p.sa2[l] : p.sa1[l];
+                        dqv[t] = p.dqdh[l];
                     }
                 }
-                surf += (isN2 ? p.sa2[l] : p.sa1[l]) * barrels;
-                sumdqdh += p.dqdh[l];
+#pragma unroll
+                for (int t = 0; t < kGather; t++) {
+                    if (eb + t >= e1) break;
+                    const bool isN2 = ent[t] < 0;
+                    const double q = qv[t];
+                    const uint32_t lf = lfv[t];
+                    double barrels = (double)((lf >> LF_BARREL_SHIFT) & 0xFF);
+                    if (!isN2) {
+                        if (q >= 0.0) outflow += q; else inflow -= q;
+                    } else {
+                        if (q >= 0.0) inflow += q; else outflow -= q;
+                    }
+                    if (lf & LF_SEEP) {
+                        const int l = ent[t] & 0x7FFFFFFF;
+                        double lossRate = (p.evapLoss[l] + p.seepLoss[l]) * barrels;
+                        if (lossRate > 0.0) {
+                            bool o1 = (lf & LF_N1_OUTFALL) != 0, o2 = (lf & LF_N2_OUTFALL) != 0;
+                            if (!o1 && !o2) lossRate /= 2.0;
+                            if (!isN2 && !o1) outflow += lossRate;
+                            if (isN2 && !o2) outflow += lossRate;
+                        }
+                    }
+                    surf += sav[t] * barrels;
+                    sumdqdh += dqv[t];
+                }
             }
             p.inflow[i] = inflow;
             p.outflow[i] = outflow;
@@ -1312,29 +1427,32 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
             listMe = true;
         }
         }
+}
+
+template <bool kFirst, bool kGeneral>
+__device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nthr)
+{
+    const double dt = p.ctl->dt;
+    bool anyUnconv = false;
+    int gathered = 0, live = 0, fast = 0;          // measurement only (countWork)
+    int* ulist = p.ulist + (size_t)(k & 1) * p.nN;
+    int2* urow = p.ulistRow + (size_t)(k & 1) * p.nN;
+    for (int i = tid; i < p.nN; i += nthr) {
+        bool listMe = false;                   // unconverged after this iteration
+        int2 row = make_int2(0, 0);            // its CSR row, for the next walk
+        nodeItem<kFirst, kGeneral>(p, k, i, dt, listMe, row, anyUnconv, gathered, live, fast);
         // list this iteration's unconverged nodes for the next k_link
-        if (!kFirst) waveAppend(listMe, i, &p.ucount[k], ulist);
+        if (!kFirst) waveAppend(listMe, i, row, &p.ucount[k], ulist, urow);
     }
-    // one flag per iteration; any writer stores 1 (no atomics needed)
-    if (__any(anyUnconv) && (threadIdx.x & 63) == 0) p.unconv[k] = 1;   // all-reduced over the ranks
-    if (!kFirst && k >= 2 && p.countWork) {                // measurement only
-        for (int off = 32; off > 0; off >>= 1) {
-            gathered += __shfl_down(gathered, off, 64);
-            live += __shfl_down(live, off, 64);
-            fast += __shfl_down(fast, off, 64);
-        }
-        if ((threadIdx.x & 63) == 0) {
-            if (gathered) atomicAdd(&p.work[p.maxTrials + k], (unsigned long long)gathered);
-            if (live) atomicAdd(&p.work[2 * p.maxTrials + k], (unsigned long long)live);
-            if (fast) atomicAdd(&p.work[3 * p.maxTrials + k], (unsigned long long)fast);
-        }
-    }
+    nodePassEnd(p, k, anyUnconv, gathered, live, fast, !kFirst && k >= 2);
 }
 
 template <bool kFirst, bool kGeneral, bool kProbe = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral ? 3 : 4))) void k_node(Params p, int k)
 {
     if (k >= 2 && p.unconv[k - 1] == 0) return;
+    probeMark(p, k, PR_N_IN);
+    probeMark(p, k, PR_N_LAST_IN);
     // prologue: outfall depths (link_setOutfallDepth, findNodeDepths
     // dynwave.c:605) from this iteration's link flows.  Only the outfall's
     // single link reads that depth (next iteration), and this kernel never
@@ -1347,10 +1465,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
     if (blockIdx.x * 64 < p.nOutLinks) {
         __shared__ double ct[5 * SWX_CIRC_N];
         __shared__ OutfallLds sh;
-        stageTables(ct, p.gTables);
-        outfallPrologue<kFirst, kGeneral>(p, ct, &sh);
+        outfallPrologue<kFirst, kGeneral>(p, ct, &sh, true, k);
+        if (blockIdx.x == 0) probeMark(p, k, PR_N_PRO);
     }
     nodePass<kFirst, kGeneral>(p, k, blockIdx.x * kBlock + threadIdx.x, gridDim.x * kBlock);
+    probeMark(p, k, PR_N_OUT);
+    if (blockIdx.x == 0) probeMark(p, k, PR_N_B0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1421,10 +1541,30 @@ __global__ __launch_bounds__(kBlock) void k_tail(Params p)
         if (!tailBarrier(p, arrivals)) return;
         // the every-shape root finders (the cold conduits' callees): calling
         // the lean ones would loosen their register budget, and k_node's
-        if (blockIdx.x * 64 < p.nOutLinks) outfallPrologue<false, true>(p, ct, &sh);
+        if (blockIdx.x * 64 < p.nOutLinks) outfallPrologue<false, true>(p, ct, &sh, false, k);
         nodePass<false, kGeneral>(p, k, tid, nthr);
         arrivals += gridDim.x;
         if (!tailBarrier(p, arrivals)) return;
+    }
+}
+
+// Init: the critical flows qCritical(i yFull / 25) (xsect.c:1612-1630) of the
+// outfall conduits' enumeration depths (getYcritEnum xsect.c:1634-1696), i =
+// 0..25: they depend on the section only, so the outfall prologue reads them
+// instead of evaluating 26 section relations per iteration
+__global__ __launch_bounds__(kBlock) void k_outfall_qcs(Params p, double* out)
+{
+    __shared__ double ct[5 * SWX_CIRC_N];
+    stageTables(ct, p.gTables);
+    for (int t = blockIdx.x * kBlock + threadIdx.x; t < 26 * p.nOutLinks; t += gridDim.x * kBlock) {
+        const int j = p.outLinks[t / 26], i = t % 26;
+        const uint32_t f = p.lflags[j];
+        double v = 0.0;
+        if (!(f & LF_NC)) {
+            Geom x = loadGeom(p, j, f);
+            v = qCritical<true>(x, i * (x.yFull / 25.), 0.0, ct);
+        }
+        out[t] = v;
     }
 }
 
@@ -1644,11 +1784,14 @@ __global__ __launch_bounds__(kBlock) void k_nc(Params p, int k)
     // ---- phase C: setNodeDepth for the deferred nodes
     bool anyUnconv = false;
     int* ulist = p.ulist + (size_t)(k & 1) * p.nN;
+    int2* urow = p.ulistRow + (size_t)(k & 1) * p.nN;
     for (int base = 0; base < p.nDef; base += kBlock) {
         int d = base + threadIdx.x;
         bool listMe = false;
+        int2 row = make_int2(0, 0);
         if (d < p.nDef) {
             int i = p.defNodes[d];
+            row = make_int2(p.rowptr[i], p.rowptr[i + 1]);
             uint32_t nf = p.nflags[i];
             if ((int)(nf & NF_TYPE) != OUTFALL) {
                 double yLast = p.nNewDepth[i], yOld = p.nOldDepth[i];
@@ -1659,15 +1802,7 @@ __global__ __launch_bounds__(kBlock) void k_nc(Params p, int k)
                 }
             }
         }
-        if (!kFirst) {
-            unsigned long long m = __ballot(listMe);
-            if (m) {
-                int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1, b = 0;
-                if (lane == leader) b = atomicAdd(&p.ucount[k], __popcll(m));
-                b = __shfl(b, leader, 64);
-                if (listMe) ulist[b + __popcll(m & ((1ull << lane) - 1ull))] = p.defNodes[d];
-            }
-        }
+        if (!kFirst) waveAppend(listMe, d < p.nDef ? p.defNodes[d] : -1, row, &p.ucount[k], ulist, urow);
     }
     if (anyUnconv) anyU = 1;
     __syncthreads();
@@ -2336,6 +2471,8 @@ struct Router::Impl {
         unsigned long long* pinned = nullptr;   // [0] iterations run, [1..] conduits updated, nodes gathered
     };
     std::vector<TimingSlot> tslots;
+    std::vector<double> probeSum;     // SWMM5_PROBE: [k][kProbeSlots + 1] phase microseconds, count
+    double wallKHz = 100000.0;
     int tUsed = 0;
     hipEvent_t* curEv = nullptr;     // event set of the step being launched
     hipEvent_t* curHot = nullptr;
@@ -2699,6 +2836,11 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     HIPCHECK(hipSetDevice(device));
     hipDeviceProp_t prop;
     HIPCHECK(hipGetDeviceProperties(&prop, device));
+    {
+        int wr = 0;                                // wall_clock64 rate (kHz), for the phase probe
+        if (hipDeviceGetAttribute(&wr, hipDeviceAttributeWallClockRate, device) == hipSuccess && wr > 0)
+            d->wallKHz = wr;
+    }
     devName_ = std::string("hip:") + prop.gcnArchName + ":" + prop.name;
     HIPCHECK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     HIPCHECK(hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking));
@@ -2950,6 +3092,8 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         int* cl;
         UPI(cl, outLinks, outLinks.size());
         p.outLinks = cl;
+        int* inl[4] = {&p.outInl0, &p.outInl1, &p.outInl2, &p.outInl3};
+        for (int c = 0; c < 4; c++) *inl[c] = (c < (int)outLinks.size()) ? outLinks[c] : -1;
         p.nOutLinks = getenv("SWMM5_TIMING_NO_OUTFALL") ? 0 : (int)outLinks.size();   // timing experiment only
     }
     // end nodes of pumps / regulators: depth updated by k_nc
@@ -3101,6 +3245,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         for (size_t i = 0; i < nN; i++) ym[i] = net.fullDepth[LN[i]] + net.surDepth[LN[i]];
         UPD(p.yMaxNP, ym, nN);
         p.ulist = devAlloc<int>(d, 2 * (size_t)nN, &e);
+        if (e == hipSuccess) p.ulistRow = devAlloc<int2>(d, 2 * (size_t)nN, &e);
         if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
         p.dirty = devAlloc<unsigned char>(d, nN, &e);
         if (e == hipSuccess) e = hipMemset(p.dirty, 0, std::max<size_t>(nN, 1));
@@ -3286,6 +3431,8 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         UPI(p.ucount, zi, M);
         p.work = devAlloc<unsigned long long>(d, 4 * M, &e);
         if (e == hipSuccess) e = hipMemset(p.work, 0, 4 * M * sizeof(unsigned long long));
+        p.probe = nullptr;                         // set in timing mode under SWMM5_PROBE
+        p.probeBlocks = 0;
         if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
     }
     d->ctl = p.ctl;
@@ -3411,6 +3558,18 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         d->kbytes[3] = P ? (N * (40 + 24.0 * P) + E * (12 + 4.0 * P) + L * (52 + 16.0 * P)) : 0.0;
     }
 
+    {   // the outfall conduits' enumeration critical flows (static)
+        double* q = devAlloc<double>(d, 26 * (size_t)std::max(p.nOutLinks, 1), &e);
+        if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+        if (p.nOutLinks > 0) {
+            hipLaunchKernelGGL(k_outfall_qcs, dim3((26 * p.nOutLinks + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                               d->stream, p, q);
+            HIPCHECK(hipGetLastError());
+            HIPCHECK(hipStreamSynchronize(d->stream));
+        }
+        p.ofQcs = q;
+    }
+
     // ---- capture the step graph ----------------------------------------------
     // (the host-callback test transport synchronises inside the step: eager)
     d->useGraph = !(part.active() && part.transport == XCHG_HOST);
@@ -3465,6 +3624,78 @@ int Router::init(Project& prj, int device, const Partition* partIn)
 }
 
 // Accumulate the per-kernel-class times of all pending timed steps.
+// SWMM5_PROBE (timing mode): read the step's per-workgroup phase stamps back
+// (synchronously: a measurement run), fold them into per-iteration phase
+// times relative to the link kernel's first workgroup start, and clear them
+static void probeCollect(Router::Impl* d)
+{
+    const Params& p = d->p;
+    const int M = std::max(p.maxTrials, 1), B = p.probeBlocks;
+    std::vector<unsigned long long> h((size_t)M * kProbeSlots * B);
+    if (hipMemcpyAsync(h.data(), p.probe, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost, d->stream) != hipSuccess ||
+        hipStreamSynchronize(d->stream) != hipSuccess)
+        return;
+    (void)hipMemsetAsync(p.probe, 0, h.size() * sizeof(h[0]), d->stream);
+    const int C = kProbeSlots + 7;
+    if (d->probeSum.size() < (size_t)C * M) d->probeSum.assign((size_t)C * M, 0.0);
+    const double us = 1000.0 / d->wallKHz;
+    for (int k = 0; k < M; k++) {
+        auto slot = [&](int sl, bool mx, bool b0) {
+            const unsigned long long* q = h.data() + ((size_t)kProbeSlots * k + sl) * B;
+            if (b0) return (double)q[0];
+            unsigned long long v = mx ? 0ull : ~0ull;
+            for (int b = 0; b < B; b++)
+                if (q[b]) v = mx ? std::max(v, q[b]) : std::min(v, q[b]);
+            return (v == 0ull || v == ~0ull) ? 0.0 : (double)v;
+        };
+        const double l0 = slot(PR_L_IN, false, false), n0 = slot(PR_N_IN, false, false);
+        if (l0 == 0.0 || n0 == 0.0) continue;          // iteration k did not run
+        double* o = d->probeSum.data() + (size_t)C * k;
+        o[PR_L_IN] += (slot(PR_L_IN, true, false) - l0) * us;         // last link workgroup's start
+        o[PR_L_OUT] += (slot(PR_L_OUT, true, false) - l0) * us;
+        const double w = slot(PR_L_WORK, true, false);
+        if (w > 0.0) o[PR_L_WORK] += (w - l0) * us;
+        o[PR_N_IN] += (n0 - l0) * us;
+        o[PR_N_LAST_IN] += (slot(PR_N_LAST_IN, true, false) - l0) * us;
+        const double pr = slot(PR_N_PRO, true, true);
+        if (pr > 0.0) o[PR_N_PRO] += (pr - l0) * us;
+        o[PR_N_OUT] += (slot(PR_N_OUT, true, false) - l0) * us;
+        o[PR_N_B0] += (slot(PR_N_B0, true, true) - l0) * us;
+        for (int sl : {PR_P_STAGED, PR_P_YN, PR_P_YC}) {
+            const double v = slot(sl, true, true);
+            if (v > 0.0) o[sl] += (v - l0) * us;
+        }
+        {   // link workgroups with list work: median phase times after their own start
+            const unsigned long long* a = h.data() + ((size_t)kProbeSlots * k + PR_L_IN) * B;
+            std::vector<double> ph[3];
+            const int sl[3] = {PR_L_SCAN, PR_L_STAGED, PR_L_WORK};
+            for (int x = 0; x < 3; x++) {
+                const unsigned long long* z = h.data() + ((size_t)kProbeSlots * k + sl[x]) * B;
+                for (int b = 0; b < B; b++)
+                    if (a[b] && z[b]) ph[x].push_back((double)(z[b] - a[b]) * us);
+                if (!ph[x].empty()) {
+                    std::sort(ph[x].begin(), ph[x].end());
+                    o[kProbeSlots + 4 + x] += ph[x][ph[x].size() / 2];
+                }
+            }
+        }
+        {   // per-workgroup node kernel durations: median, maximum, slowest workgroup
+            const unsigned long long* a = h.data() + ((size_t)kProbeSlots * k + PR_N_IN) * B;
+            const unsigned long long* z = h.data() + ((size_t)kProbeSlots * k + PR_N_OUT) * B;
+            std::vector<std::pair<double, int>> dur;
+            for (int b = 0; b < B; b++)
+                if (a[b] && z[b]) dur.push_back({(double)(z[b] - a[b]) * us, b});
+            if (!dur.empty()) {
+                std::sort(dur.begin(), dur.end());
+                o[kProbeSlots + 1] += dur[dur.size() / 2].first;
+                o[kProbeSlots + 2] += dur.back().first;
+                o[kProbeSlots + 3] = dur.back().second;
+            }
+        }
+        o[kProbeSlots] += 1;
+    }
+}
+
 static void flushTiming(Router::Impl* d)
 {
     if (!d->tUsed) return;
@@ -3623,6 +3854,7 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
         const size_t wb = 4 * (size_t)std::max(p.maxTrials, 1) * sizeof(unsigned long long);
         HIPCHECK(hipMemcpyAsync(t.pinned + 1, p.work, wb, hipMemcpyDeviceToHost, d->stream));
         HIPCHECK(hipMemsetAsync(p.work, 0, wb, d->stream));
+        if (p.probe) probeCollect(d);
     } else if (d->useGraph) {
         HIPCHECK(hipGraphLaunch(useTail(d) ? d->graphTail : d->graph, d->stream));
     } else if (launchStep(d)) {                   // eager (host-transport exchange)
@@ -4009,6 +4241,35 @@ void Router::stepTotals(double out[6])
 void Router::setTiming(bool on)
 {
     flushTiming(d_);
+    if (!d_->probeSum.empty()) {                   // SWMM5_PROBE report (stderr)
+        const int C = kProbeSlots + 7;
+        fprintf(stderr, "probe (us after the first link workgroup start): k n  link_last_start  link_end  link_work_end  node_start  node_last_start  prologue_end  node_end  node_block0_end | node workgroup duration median max (slowest workgroup) | outfall tables_staged ynorm_done ycrit_done | link workgroup median scan staged walked\n");
+        for (int k = 0; k * C < (int)d_->probeSum.size(); k++) {
+            const double* o = d_->probeSum.data() + (size_t)C * k;
+            if (o[kProbeSlots] <= 0) continue;
+            const double n = o[kProbeSlots];
+            fprintf(stderr, "probe k=%d n=%.0f  %.2f  %.2f  %.2f  %.2f  %.2f  %.2f  %.2f  %.2f | %.2f %.2f (%.0f) | %.2f %.2f %.2f | %.2f %.2f %.2f\n",
+                    k, n, o[PR_L_IN] / n, o[PR_L_OUT] / n, o[PR_L_WORK] / n, o[PR_N_IN] / n, o[PR_N_LAST_IN] / n,
+                    o[PR_N_PRO] / n, o[PR_N_OUT] / n, o[PR_N_B0] / n, o[kProbeSlots + 1] / n, o[kProbeSlots + 2] / n,
+                    o[kProbeSlots + 3], o[PR_P_STAGED] / n, o[PR_P_YN] / n, o[PR_P_YC] / n, o[kProbeSlots + 4] / n,
+                    o[kProbeSlots + 5] / n, o[kProbeSlots + 6] / n);
+        }
+        d_->probeSum.clear();
+    }
+    if (on && getenv("SWMM5_PROBE") && !d_->p.probe) {
+        const int B = std::max(std::max(d_->gridL, d_->gridN), d_->gridLinkSparse);
+        const size_t n = (size_t)std::max(d_->p.maxTrials, 1) * kProbeSlots * B;
+        if (hipMalloc((void**)&d_->p.probe, n * sizeof(unsigned long long)) == hipSuccess &&
+            hipMemset(d_->p.probe, 0, n * sizeof(unsigned long long)) == hipSuccess)
+            d_->p.probeBlocks = B;
+        else
+            d_->p.probe = nullptr;
+    } else if (!on && d_->p.probe) {
+        (void)hipStreamSynchronize(d_->stream);
+        (void)hipFree(d_->p.probe);
+        d_->p.probe = nullptr;
+        d_->p.probeBlocks = 0;
+    }
     d_->timing = on;
     d_->p.countWork = on ? 1 : 0;                  // eager launches only; the graph keeps 0
     for (int k = 0; k < Impl::kClasses; k++) { d_->kms[k] = 0; d_->kcnt[k] = 0; d_->kbytesSum[k] = 0; }

@@ -17,7 +17,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libswmm5_mi355x.so")
+LIB_PATH = os.environ.get("SWMM5_LIB") or os.path.join(PKG_DIR, "libswmm5_mi355x.so")   # SWMM5_LIB: A/B builds
 
 # swmm5.h enums (values are the reference's)
 GAGE, SUBCATCH, NODE, LINK, SYSTEM = 0, 1, 2, 3, 100
