@@ -90,6 +90,7 @@ enum : uint32_t {
     LF_COLD = 1u << 22,           // an invert offset: may need normal/critical depth
     LF_NC = 1u << 23,             // pump / orifice / weir / outlet (k_nc; also LF_COLD)
     LF_PUMP = 1u << 24,
+    LF_DUMMY = 1u << 31,          // a DUMMY conduit (with LF_NC only: bit 31 is a geometry-id bit of streaming conduits)
     LF_CULVERT_SHIFT = 25,        // bits 25-30 culvert code (cold conduits only)
     LF_GEOM_SHIFT = 25,           // bits 25-31 geometry id (streaming conduits, kFast only)
 };
@@ -1727,6 +1728,9 @@ __global__ __launch_bounds__(kBlock) void k_nc(Params p, int k)
         p.lstate[j] = (p.lstate[j] & ~0xF) | (o.flowClass & 0xF);
         if (L.type == LK_PUMP) {
             p.ncQ[c] = q;
+        } else if (L.type == LK_CONDUIT) {
+            // DUMMY conduit: its flow is its upstream node's outflow at its
+            // turn in link order (phase B)
         } else {
             if (k > 0) {                                    // under-relaxation (dynwave.c:455-461)
                 q = (1.0 - 0.5) * qLast + 0.5 * q;
@@ -1765,6 +1769,23 @@ __global__ __launch_bounds__(kBlock) void k_nc(Params p, int k)
                         double y = p.nOldDepth[n1] + vol / p.nSurf[n1];
                         if (y <= 0.0) q = p.inflow[n1];
                     }
+                }
+                p.lNewFlow[j] = q;
+            } else if (L.type == LK_CONDUIT && !p.ncBypass[c]) {
+                // DUMMY conduit (findNonConduitFlow dynwave.c:423-461):
+                // link_getInflow -> conduit_getInflow (link.c:543-560,
+                // 1320-1330) = node_getOutflow of its upstream node (a junction:
+                // inflow + overflow so far, node.c:400-414), capped by its flow
+                // limit, then under-relaxed (not a pump)
+                const double qLast = p.lNewFlow[j];
+                double q = 0.0;
+                if (p.setting[j] != 0.0) {
+                    q = p.inflow[n1] + p.overflow[n1];
+                    if (L.qLimit > 0.0) q = gmin(q, L.qLimit);
+                }
+                if (k > 0) {
+                    q = (1.0 - 0.5) * qLast + 0.5 * q;
+                    if (q * qLast < 0.0) q = 0.001 * ((q < 0.0) ? -1.0 : 1.0);
                 }
                 p.lNewFlow[j] = q;
             }
@@ -2037,6 +2058,25 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
                     p.pPeriods[j] += 1;
                     S.lTimeSurch[j] += dt;
                     S.lTimeFullUp[j] += dt;
+                    S.lTimeFullDn[j] += dt;
+                }
+            }
+            if (f & LF_DUMMY) {                            // still a CONDUIT (stats.c:707-745)
+                const int s = p.lstate[j];
+                if (s & (1 << 8)) S.lTimeNormal[j] += dt;
+                if (s & (1 << 10)) S.lTimeInlet[j] += dt;
+                const int fc = s & 0xF;
+                if (fc < 7) S.lTimeClass[(size_t)fc * p.nL + j] += dt;
+                if (q >= S.qFull[j] * (double)((f >> LF_BARREL_SHIFT) & 0xFF)) S.lTimeFullFlow[j] += dt;
+                if (s & (1 << 9)) S.lTimeCapLim[j] += dt;
+                const int fs = (s >> 4) & 0xF;
+                if (fs == FS_ALL_FULL) {
+                    S.lTimeSurch[j] += dt;
+                    S.lTimeFullUp[j] += dt;
+                    S.lTimeFullDn[j] += dt;
+                } else if (fs == FS_UP_FULL) {
+                    S.lTimeFullUp[j] += dt;
+                } else if (fs == FS_DN_FULL) {
                     S.lTimeFullDn[j] += dt;
                 }
             }
@@ -2395,7 +2435,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_results(Params p, double f, dou
         double v = f1 * p.lOldVolume[j] + f * p.lNewVolume[j];
         double u = 0.0;
         double c = 0.0;
-        if (fl & LF_NC) {
+        if ((fl & LF_NC) && !(fl & LF_DUMMY)) {         // DUMMY conduits: u = c = 0 below
             c = p.setting[j];                            // link.c:699-707
             double qo = p.lOldFlow[j], qn = p.lNewFlow[j];
             if ((fl & LF_PUMP) && qo * qn == 0.0) q = (f >= f1) ? qn : qo;
@@ -2890,11 +2930,6 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     std::vector<int> lflags(nL), coldLinks, outLinks;
     std::vector<double> inv1(nL), inv2(nL), xd[11];
     for (auto& v : xd) v.resize(nL);
-    for (int jj = 0; jj < gL; jj++)
-        if (net.linkType[jj] == CONDUIT && net.xsect[jj].type == X_DUMMY) {
-            fail("dummy conduits are not supported yet");
-            return err_;
-        }
     for (int j = 0; j < nL; j++) {
         const int g = LL[j];                        // global link index
         int n1 = net.node1[g], n2 = net.node2[g];   // global node indices
@@ -2914,9 +2949,10 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (net.direction[g] < 0) f |= LF_DIRNEG;
         if (j >= nOwn) {
             f |= LF_COLD;                           // ghost: computed by its owner, never here
-        } else if (net.linkType[g] != CONDUIT) {
+        } else if (!net.isTrueConduit(g)) {
             f |= LF_NC | LF_COLD;                   // k_nc, not the conduit kernels
             if (net.linkType[g] == PUMP) f |= LF_PUMP;
+            if (net.linkType[g] == CONDUIT) f |= LF_DUMMY;
         } else if (net.offset1[g] > 0.0 || net.offset2[g] > 0.0 || !isBasicShape(x.type) ||
                    x.culvertCode > 0) {
             if (x.culvertCode > 0) f |= ((uint32_t)std::min(x.culvertCode, 63) & 0x3Fu) << LF_CULVERT_SHIFT;
@@ -3077,7 +3113,9 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     // link in link order (findLinkMassFlow, qualrout.c:111).
     std::vector<int> rowptr, csr, qrowptr, qcsr;
     buildLocalCsr(net, part, true, rowptr, csr);
-    if (net.nNC > 0) buildLocalCsr(net, part, false, qrowptr, qcsr);
+    bool anyNC = false;                             // pumps, regulators or DUMMY conduits
+    for (int g = 0; g < gL && !anyNC; g++) anyNC = !net.isTrueConduit(g);
+    if (anyNC) buildLocalCsr(net, part, false, qrowptr, qcsr);
     // the reference's link_setOutfallDepth loop (findNodeDepths): the last
     // link touching an outfall sets its depth
     for (int j = 0; j < nOwn; j++) {
@@ -3122,7 +3160,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
                 }
             UPI(rp, other, other.size()); p.csrOther = rp;
         }
-        if (net.nNC > 0) {
+        if (anyNC) {
             UPI(rp, qrowptr, nN + 1); p.qrowptr = rp;
             UPI(rp, qcsr, qcsr.size()); p.qcsr = rp;
         } else {
@@ -3181,9 +3219,9 @@ int Router::init(Project& prj, int device, const Partition* partIn)
             std::vector<double> coef, target, zero;
             for (int j = 0; j < nOwn; j++) {
                 const int g = LL[j];
-                if (net.linkType[g] == CONDUIT) continue;
+                if (net.isTrueConduit(g)) continue;
                 ncl.push_back(j);
-                NcLink L = prj.ncLink(g);
+                NcLink L = prj.ncLink(g);          // DUMMY conduits: type LK_CONDUIT
                 int c = net.ncCurve[g];
                 L.cOff = c >= 0 ? curveOff[c] : 0;
                 ncs.push_back(L);

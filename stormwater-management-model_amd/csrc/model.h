@@ -197,6 +197,9 @@ struct Network {
     std::vector<double> ncRoadWidth;    // roadway weirs (link.c:381-382)
     std::vector<int> ncRoadSurf;
     int nNC = 0, nPumps = 0;
+    // dynwave.c:416-419 isTrueConduit: a conduit that is not a DUMMY link
+    // (DUMMY conduits are routed with the non-conduit links)
+    bool isTrueConduit(int j) const { return linkType[j] == CONDUIT && xsect[j].type != X_DUMMY; }
     // inflows / quality inputs
     std::vector<ExtInflow> extInflows;
     std::vector<DwfInflow> dwfInflows;

@@ -39,7 +39,7 @@ int buildPartition(const Network& net, Partition& part, std::string* msg)
     // the owner of the group's smallest node
     std::vector<char> deferred(nN, 0);
     for (int j = 0; j < nL; j++)
-        if (net.linkType[j] != CONDUIT) deferred[net.node1[j]] = deferred[net.node2[j]] = 1;
+        if (!net.isTrueConduit(j)) deferred[net.node1[j]] = deferred[net.node2[j]] = 1;
     {
         std::vector<int> up(nN);
         std::iota(up.begin(), up.end(), 0);
@@ -193,7 +193,7 @@ void buildLocalCsr(const Network& net, const Partition& part, bool conduitsOnly,
     rowptr.assign(n + 1, 0);
     for (int l = 0; l < nLoc; l++) {
         const int g = global(l);
-        if (conduitsOnly && net.linkType[g] != CONDUIT) continue;
+        if (conduitsOnly && !net.isTrueConduit(g)) continue;
         for (int e : {net.node1[g], net.node2[g]})
             if (part.gnode[e] >= 0) rowptr[part.gnode[e] + 1]++;
     }
@@ -202,7 +202,7 @@ void buildLocalCsr(const Network& net, const Partition& part, bool conduitsOnly,
     std::vector<int> fill(rowptr.begin(), rowptr.end() - 1);
     for (int l = 0; l < nLoc; l++) {
         const int g = global(l);
-        if (conduitsOnly && net.linkType[g] != CONDUIT) continue;
+        if (conduitsOnly && !net.isTrueConduit(g)) continue;
         const int a = part.gnode[net.node1[g]], b = part.gnode[net.node2[g]];
         if (a >= 0) csr[fill[a]++] = l;
         if (b >= 0) csr[fill[b]++] = (int)((unsigned)l | 0x80000000u);

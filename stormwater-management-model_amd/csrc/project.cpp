@@ -2230,6 +2230,10 @@ void Project::validateConduit(int j)  // link.c:992-1154 (supported shapes)
 {
     Xsect& xs = net.xsect[j];
     if (xs.type < 0) { setError(117, "ERROR 117: no cross section defined for link " + net.linkId[j]); return; }
+    if (xs.type == X_DUMMY && net.nodeType[net.node1[j]] == STORAGE) {   // link.c:1003-1011 (DW)
+        setError(134, "ERROR 134: Node " + net.nodeId[net.node1[j]] + " has illegal DUMMY link connections.");
+        return;
+    }
     const XTable* tt = nullptr;
     if (xs.type == X_CUSTOM) {                         // xsect_setCustomXsectParams xsect.c:664-696
         int sh = (xs.transect >= 0 && xs.transect < (int)net.curveShape.size()) ? net.curveShape[xs.transect] : -1;
@@ -2556,6 +2560,24 @@ void Project::validate()  // project.c:186-270
         int i = net.node1[j];
         if (net.nodeType[i] != OUTFALL) i = net.node2[j];
         inCount[i] += 1.0;
+        // a DUMMY conduit or an ideal pump must be the only link leaving its
+        // upstream node (flowrout.c:295-307)
+        const bool dummy = net.linkType[j] == CONDUIT && net.xsect[j].type == X_DUMMY;
+        const bool ideal = net.linkType[j] == PUMP && net.ncSub[j] == PT_IDEAL;
+        if (dummy || ideal) {
+            const int u = (net.direction[j] < 0) ? net.node2[j] : net.node1[j];
+            if (net.degree[u] > 1) {
+                setError(134, "ERROR 134: Node " + net.nodeId[u] + " has illegal DUMMY link connections.");
+                return;
+            }
+            // its flow is node_getOutflow of that node (node.c:400-414): a
+            // divider's share (divider_getOutflow) is not modelled
+            if (net.nodeType[u] == DIVIDER) {
+                setError(200, "ERROR 200: a DUMMY conduit or ideal pump leaving Divider " + net.nodeId[u] +
+                                  " is not supported by the MI355X engine");
+                return;
+            }
+        }
     }
     int outletCount = 0;
     for (int i = 0; i < nn; i++)
@@ -2838,6 +2860,7 @@ NcLink Project::ncLink(int j) const
     L.si = opt.unitSystem;
     L.roadWidth = net.ncRoadWidth[j];
     L.roadSurf = net.ncRoadSurf[j];
+    L.qLimit = net.qLimit[j];
     return L;
 }
 

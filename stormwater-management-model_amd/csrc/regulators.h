@@ -33,6 +33,7 @@ struct NcLink {
     int si;                     // UnitSystem == SI
     double roadWidth;           // roadway weirs: road width (ft), surface 1 paved / 2 gravel
     int roadSurf;
+    double qLimit;              // DUMMY conduits: Link.qLimit (0: none)
 };
 
 // setting-dependent coefficients (orifice_setSetting, weir_setSetting)

@@ -417,7 +417,7 @@ def write_example(path: str, *, route_step: float = 5.0,
                   culverts: bool = False, tidal: bool = False, roadway: bool = False,
                   dividers: bool = False, streets: bool = False, extfile: bool = False,
                   options: dict | None = None, ponding: bool = False,
-                  branches: bool = False) -> None:
+                  branches: bool = False, dummy: bool = False) -> None:
     """Write the authored Example network (see module docstring).  `files`
     is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf");
     `storage` turns six junctions into storage units (_STORAGE); `options`
@@ -426,7 +426,11 @@ def write_example(path: str, *, route_step: float = 5.0,
     areas (flooding and ponding, dynwave.c:661-795, node.c:562-585);
     `branches` adds the backwater branch _BRANCHES (reverse flow over an
     invert offset and a weir crest: UP_CRITICAL, dwflow.c:347, 391,
-    link.c:2274; a depth-curve pump below its curve: DN_DRY, link.c:1624)."""
+    link.c:2274; a depth-curve pump below its curve: DN_DRY, link.c:1624);
+    `dummy` makes C4 and C9 DUMMY conduits (the only outflow links of N5 and
+    N10; C9 with a 1.5 cfs flow limit): routed as non-conduit links that pass
+    their upstream node's inflow (dynwave.c:416-419, link.c:543-560,
+    1320-1330)."""
     if pollutants:
         pollut = ("TSS MG/L 0 0 0 0.5 NO * 0 20 0\n"
                   "BOD MG/L 0 0 0 0 NO * 0 10 0\n")
@@ -549,6 +553,10 @@ def write_example(path: str, *, route_step: float = 5.0,
                 txt = txt.replace(sect + "\n", sect + "\n" + body, 1)
             else:
                 txt += "\n" + sect + "\n" + body
+    if dummy:
+        txt = txt.replace("C4  RECT_OPEN    2.0  3.0  0    0  1", "C4  DUMMY        0    0    0    0  1", 1)
+        txt = txt.replace("C9  TRAPEZOIDAL  2.0  2.0  1.5  1.5 1", "C9  DUMMY        0    0    0    0  1", 1)
+        txt = txt.replace("C9  N10 N8  300  0.014  0.5  0    0  0", "C9  N10 N8  300  0.014  0.5  0    0  1.5", 1)
     if options:
         lines = txt.split("\n")
         for key, val in options.items():

@@ -17,7 +17,7 @@ CASES = ["grid12", "grid12_var_qual", "grid10_surcharge", "example", "example_va
          "example_tidal", "example_tidal_var", "example_roadway", "example_dividers",
          "example_streets", "example_extfile", "example_branches", "example_branches_var",
          "example_slot_pond", "example_options", "grid10_slot", "example_stride",
-         "example_stride_fixed"]
+         "example_stride_fixed", "example_dummy", "example_dummy_var"]
 # cases using objects outside the C restatement's scope (oracle/dw_oracle.c
 # covers junctions, outfalls and conduits): pinned by the GPU tests against the
 # reference's own fixtures only
@@ -26,7 +26,7 @@ BEYOND_ORACLE = {"example_storage", "example_storage_var", "example_storage_qual
                  "example_shapes_var", "example_irregular", "example_irregular_var",
                  "example_culverts", "example_culverts_var", "example_tidal", "example_tidal_var",
                  "example_roadway", "example_dividers", "example_streets", "example_branches",
-                 "example_branches_var",
+                 "example_branches_var", "example_dummy", "example_dummy_var",
                  # swmm_stride calls: an API driver the C restatement does not model
                  "example_stride", "example_stride_fixed"}
 # cases whose input writes a file next to itself ([FILES] SAVE ...): they run
@@ -42,7 +42,7 @@ GRID_CONC = [5.0, 10.0, 15.0, 20.0, 25.0, 30.0]
 # spread ("env.*", tests/golden/make_golden.py ENVELOPE)
 ENVELOPE = {"example_shapes", "example_shapes_var", "example_irregular", "example_irregular_var",
             "example_culverts", "example_culverts_var", "example_streets", "example_branches",
-            "example_branches_var"}
+            "example_branches_var", "example_dummy", "example_dummy_var"}
 
 
 def first_divergence(d, node_f, link_f, rtol, atol):

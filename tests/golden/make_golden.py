@@ -38,7 +38,7 @@ REFDUMP_X87 = os.path.join(ROOT, "oracle", "_ref", "x87", "refdump")
 # `make -C oracle ref-fma`
 ENVELOPE = {"example_shapes", "example_shapes_var", "example_irregular", "example_irregular_var",
             "example_culverts", "example_culverts_var", "example_streets", "example_branches",
-            "example_branches_var"}
+            "example_branches_var", "example_dummy", "example_dummy_var"}
 
 # envelope cases whose report tables also carry the x87 build's report (the
 # report test then accepts twice the larger of the two builds' differences)
@@ -114,6 +114,10 @@ CASES = {
     # every flow class (dwflow.c:297-413): backwater over an invert offset and
     # a weir crest (UP_CRITICAL), a depth-curve pump below its curve (DN_DRY)
     "example_branches": (netgen.write_example, dict(end_time="01:40:00", route_step=5.0, branches=True), 1),
+    "example_dummy": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, dummy=True,
+                                                 pollutants=True), 1),
+    "example_dummy_var": (netgen.write_example, dict(end_time="02:00:00", route_step=10.0, variable_step=0.75,
+                                                     dummy=True), 1),
     "example_branches_var": (netgen.write_example, dict(end_time="01:40:00", route_step=10.0,
                                                         variable_step=0.75, branches=True,
                                                         options={"INERTIAL_DAMPING": "NONE"}), 1),

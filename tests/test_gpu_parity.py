@@ -69,7 +69,10 @@ def _run(name, tmp_path):
             n_out, n_all = dev.get(key, (0, 0))
             dev[key] = (n_out + int((np.abs(a - b) > bound).sum()), n_all + a.size)
             return
-        np.testing.assert_allclose(a, b, rtol=RTOL, atol=ATOL, err_msg=msg)
+        # before the builds diverge: the tolerance plus twice the reference's
+        # own build-to-build spread at this step (0 while they agree bitwise)
+        spread = 2.0 * float(d["env." + key][rec]) if env and "env." + key in d else 0.0
+        np.testing.assert_allclose(a, b, rtol=RTOL, atol=ATOL + spread, err_msg=msg)
     for step in range(1, total + 1):
         err, t = _golden.advance(s, acts, step - 1)
         assert err == 0, s.getError()

@@ -116,6 +116,26 @@ def test_divider_with_unattached_link_is_rejected(tmp_path):
     s.close()
 
 
+@pytest.mark.parametrize("layout", ["second_outflow", "storage_upstream"])
+def test_illegal_dummy_links_rejected(layout, tmp_path):
+    """A DUMMY conduit must be the only link leaving a non-storage node
+    (flowrout.c:295-307, link.c:1003-1011): ERROR 134, as the compiled
+    reference reports for these two inputs."""
+    src = open(_golden.inp("example_dummy")).read()
+    if layout == "second_outflow":
+        src = src.replace("C5  N6  N4", "CX  N5  N6  100  0.013  0  0  0  0\nC5  N6  N4", 1)
+        src = src.replace("C5  RECT_OPEN", "CX  CIRCULAR 1.0 0 0 0 1\nC5  RECT_OPEN", 1)
+    else:
+        src = src.replace("N5  119.0  7  0    0  0\n", "", 1)
+        src = src.replace("[OUTFALLS]", "[STORAGE]\nN5  119.0  7  0  FUNCTIONAL 1000 0 0 0 0\n\n[OUTFALLS]", 1)
+    p = tmp_path / "d.inp"
+    p.write_text(src)
+    s = swmm5.SWMM()
+    assert s.open(str(p), str(tmp_path / "d.rpt"), str(tmp_path / "d.out")) == 134
+    assert "Node N5 has illegal DUMMY link connections" in s.getError()[1]
+    s.close()
+
+
 def test_step_without_gpu_start_is_an_error(tmp_path):
     s = swmm5.SWMM()
     assert s.open(_golden.inp("grid12"), str(tmp_path / "a.rpt"), str(tmp_path / "a.out")) == 0

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""In-graph kernel durations of bench.py's timed window from a rocprofv3
+--kernel-trace run (tools/gpu_round.sh prof), for the bench line's roofline.
+
+usage: rocprof_summary.py <prof_dir> <bench_log> [tag]
+
+<prof_dir>/run_kernel_trace.csv is the trace of `python3 bench.py ...`;
+<bench_log> holds that run's JSON line (workload, spin-up, warm-up, steps).
+Dispatches are ordered by start time and a routing step ends at its
+k_finalize, so the timed window is the dispatches after the (spinup +
+warmup)-th k_finalize through the (spinup + warmup + steps)-th -- graph
+launches only, none of the timing-mode or measurement launches after it.
+
+Prints a markdown table (average duration per kernel and per launch
+position) and records the window's k_link<first> average in
+profiles/kernel_timing.json, keyed by workload and stamped with the sha256 of
+dw_kernels.hip (bench.py uses it only for that kernel source and window)."""
+import collections
+import csv
+import hashlib
+import json
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "stormwater-management-model_amd", "csrc", "dw_kernels.hip")
+
+
+def short(n):
+    n = re.sub(r"\(swx::Params.*", "", n).replace("void swx::", "")
+    return re.sub(r"\(.*", "", n)
+
+
+def main():
+    d, blog = sys.argv[1], sys.argv[2]
+    tag = sys.argv[3] if len(sys.argv) > 3 else ""
+    line = [l for l in open(blog) if l.startswith('{"metric"')][-1]
+    b = json.loads(line)
+    workload = b["config"]["workload"]
+    spinup, warmup, steps = b["config"]["spinup_steps"], b["warmup"], b["steps"]
+    rows = list(csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv"))))
+    ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])) for r in rows)
+    fin = [i for i, e in enumerate(ev) if e[2].startswith("k_finalize")]
+    s0, s1 = spinup + warmup, spinup + warmup + steps
+    win = ev[fin[s0 - 1] + 1: fin[s1 - 1] + 1]
+    per = collections.defaultdict(list)
+    for t0, t1, n in win:
+        per[n].append((t1 - t0) / 1000.0)
+    first = [k for k in per if k.startswith("k_link<true")]
+    if len(first) != 1:
+        sys.exit("expected one k_link<first> instantiation in the window, found %s" % first)
+    fus = sum(per[first[0]]) / len(per[first[0]])
+    step_us = (win[-1][1] - win[0][0]) / 1000.0 / steps
+    print("# rocprofv3 kernel trace %s\n" % tag)
+    print("Workload `%s`; the timed window's %d graph-launched steps after %d spin-up + %d warm-up "
+          "steps; %.1f us per step first start to last end.\n" % (workload, steps, spinup, warmup, step_us))
+    print("| kernel | launches/step | average us | total us/step |")
+    print("|---|---|---|---|")
+    for n, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
+        print("| `%s` | %.2f | %.2f | %.2f |" % (n, len(v) / steps, sum(v) / len(v), sum(v) / steps))
+    tp = os.path.join(ROOT, "profiles", "kernel_timing.json")
+    rec = json.load(open(tp)) if os.path.exists(tp) else {}
+    rec[workload] = {
+        "kernel": first[0],
+        "avg_launch_us": round(fus, 3),
+        "launches": len(per[first[0]]),
+        "step_us": round(step_us, 2),
+        "window": [spinup, warmup, steps],
+        "src_sha": hashlib.sha256(open(SRC, "rb").read()).hexdigest()[:16],
+        "source": "profiles/%s_rocprof_window.md (rocprofv3 --kernel-trace of bench.py, timed window)"
+                  % (tag or "prof"),
+    }
+    with open(tp, "w") as f:
+        json.dump(rec, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
