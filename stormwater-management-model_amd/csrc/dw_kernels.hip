@@ -804,17 +804,18 @@ __device__ __forceinline__ void probeMark(const Params& p, int k, int slot, unsi
 // its CSR row, whose bounds came with the list entry; a conduit whose ends
 // are both listed is taken by the lower-numbered end.  cnt = the number of
 // listed nodes; ct = staged tables.
+// (u0, rb0): thread tid's first entry, loaded by the caller ahead of staging
 template <bool kFast>
 __device__ __forceinline__ int linkListWalk(const Params& p, int k, int cnt, double dt, const double* ct,
-                                            int tid, int nthr)
+                                            int tid, int nthr, int u0, int2 rb0)
 {
     const int* list = p.ulist + (size_t)((k - 1) & 1) * p.nN;
     const int2* rows = p.ulistRow + (size_t)((k - 1) & 1) * p.nN;
     const int slots = 4 * cnt;
     int work = 0;
     for (int t = tid; t < slots; t += nthr) {
-        const int u = list[t >> 2];
-        const int2 rb = rows[t >> 2];
+        const int u = (t == tid) ? u0 : list[t >> 2];
+        const int2 rb = (t == tid) ? rb0 : rows[t >> 2];
         for (int e = rb.x + (t & 3); e < rb.y; e += 4) {
             // the entry names the link and (csrOther) its other end, so the
             // end nodes' state loads in parallel with the link's own; the
@@ -848,6 +849,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
 void k_link(Params p, int k)
 {
     const int tid = blockIdx.x * kBlock + threadIdx.x, nthr = gridDim.x * kBlock;
+    const int cnt = (!kFirst && k >= 2) ? p.ucount[k - 1] : 0;   // loads with the flag below
     if (k >= 2 && p.unconv[k - 1] == 0) {            // converged: dynwave.c:249-251
         // the first launch after the step converged (iteration k-1 ran)
         if (p.freeze && (k == 2 || p.unconv[k - 2] != 0)) finalizeFrozen(p, k - 1, tid, nthr);
@@ -869,11 +871,16 @@ void k_link(Params p, int k)
             conduitFlow<kFirst, false, kFast>(p, j, f, nn, k, dt, ct, p.nNewDepth[nn.x], p.nNewDepth[nn.y]);
         }
     } else {
-        const int cnt = p.ucount[k - 1];
         if (blockIdx.x * kBlock < 4 * cnt) {                // uniform per block
+            int u0 = 0;
+            int2 rb0 = make_int2(0, 0);
+            if (tid < 4 * cnt) {                             // first entry: loads with the staging
+                u0 = p.ulist[(size_t)((k - 1) & 1) * p.nN + (tid >> 2)];
+                rb0 = p.ulistRow[(size_t)((k - 1) & 1) * p.nN + (tid >> 2)];
+            }
             stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
             probeMark(p, k, PR_L_STAGED);
-            work = linkListWalk<kFast>(p, k, cnt, dt, ct, tid, nthr);
+            work = linkListWalk<kFast>(p, k, cnt, dt, ct, tid, nthr, u0, rb0);
             probeMark(p, k, PR_L_WORK);
         }
     }
@@ -1165,6 +1172,8 @@ __device__ __forceinline__ void outfallPrologue(const Params& p, double* ct, Out
             prev = p.nNewDepth[o];
             nfo = p.nflags[o];
         }
+        // the group's first conduit's tabulated critical flows (static)
+        const double qcs0 = (w >= 1 && g < nHere && gl <= 25) ? p.ofQcs[26 * (base + g) + gl] : 0.0;
         if (stage) { stageTables(ct, p.gTables); stage = false; }
         if (base == 0) probeMark(p, kProbeK, PR_P_STAGED);
         double yn = 0.0;                               // non-conduits: yNorm = yCrit = 0
@@ -1189,7 +1198,7 @@ __device__ __forceinline__ void outfallPrologue(const Params& p, double* ct, Out
                 if (cc) {
                     double y0 = 0.0;
                     if (yCritByEnum(xx, qq, &y0)) {
-                        if (gl <= 25) sh->qcs[g][gl] = p.ofQcs[26 * (base + m) + gl];
+                        if (gl <= 25) sh->qcs[g][gl] = (m == g) ? qcs0 : p.ofQcs[26 * (base + m) + gl];
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                         __builtin_amdgcn_wave_barrier();
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1258,12 +1267,31 @@ __device__ __forceinline__ void nodePassEnd(const Params& p, int k, bool anyUnco
 // setNodeDepth.  listMe: unconverged after this iteration (outfalls always);
 // row: its CSR row bounds for the next link walk.  gathered / live / fast:
 // measurement counters (countWork).
+// a node's flag words, loaded ahead of its update (NodePre)
+struct NodePre {
+    uint32_t nf;
+    unsigned char cache;      // dirty[i] (iterations k >= 2)
+    unsigned char fz;         // frz[i] (iterations k >= 2)
+};
+__device__ __forceinline__ NodePre loadNodePre(const Params& p, int i, int k)
+{
+    NodePre q{0u, 0, 0};
+    if (i < p.nN) {
+        q.nf = p.nflags[i];
+        if (k >= 2) {
+            q.cache = p.dirty[i];
+            q.fz = p.frz[i];
+        }
+    }
+    return q;
+}
+
 template <bool kFirst, bool kGeneral>
-__device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double dt, bool& listMe, int2& row,
-                                         bool& anyUnconv, int& gathered, int& live, int& fast)
+__device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double dt, NodePre pre, bool& listMe,
+                                         int2& row, bool& anyUnconv, int& gathered, int& live, int& fast)
 {
     constexpr bool kStorage = kGeneral;
-        uint32_t nf = p.nflags[i];
+        const uint32_t nf = pre.nf;
         int type = (int)(nf & NF_TYPE);
         // an outfall's depth is written by the prologue above: not read here
         double yLast = 0.0;
@@ -1271,8 +1299,8 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
         listMe = (type == OUTFALL);
         bool done = false, isFast = false;
         if (!kFirst && k >= 2) {
-            unsigned char cache = p.dirty[i];
-            const int fz = p.frz[i];
+            const unsigned char cache = pre.cache;
+            const int fz = pre.fz;
             if (fz) {
                 // frozen junction: nothing to do while its conduits are
                 // bypassed (it stays converged; none of its operands is
@@ -1431,7 +1459,7 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
 }
 
 template <bool kFirst, bool kGeneral>
-__device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nthr)
+__device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nthr, NodePre pre0)
 {
     const double dt = p.ctl->dt;
     bool anyUnconv = false;
@@ -1441,7 +1469,8 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
     for (int i = tid; i < p.nN; i += nthr) {
         bool listMe = false;                   // unconverged after this iteration
         int2 row = make_int2(0, 0);            // its CSR row, for the next walk
-        nodeItem<kFirst, kGeneral>(p, k, i, dt, listMe, row, anyUnconv, gathered, live, fast);
+        const NodePre pre = (i == tid) ? pre0 : loadNodePre(p, i, k);
+        nodeItem<kFirst, kGeneral>(p, k, i, dt, pre, listMe, row, anyUnconv, gathered, live, fast);
         // list this iteration's unconverged nodes for the next k_link
         if (!kFirst) waveAppend(listMe, i, row, &p.ucount[k], ulist, urow);
     }
@@ -1451,6 +1480,8 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
 template <bool kFirst, bool kGeneral, bool kProbe = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral ? 3 : 4))) void k_node(Params p, int k)
 {
+    // the first node's flag words load alongside the convergence flag
+    const NodePre pre0 = loadNodePre(p, blockIdx.x * kBlock + threadIdx.x, kFirst ? 0 : k);
     if (k >= 2 && p.unconv[k - 1] == 0) return;
     probeMark(p, k, PR_N_IN);
     probeMark(p, k, PR_N_LAST_IN);
@@ -1469,7 +1500,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
         outfallPrologue<kFirst, kGeneral>(p, ct, &sh, true, k);
         if (blockIdx.x == 0) probeMark(p, k, PR_N_PRO);
     }
-    nodePass<kFirst, kGeneral>(p, k, blockIdx.x * kBlock + threadIdx.x, gridDim.x * kBlock);
+    nodePass<kFirst, kGeneral>(p, k, blockIdx.x * kBlock + threadIdx.x, gridDim.x * kBlock, pre0);
     probeMark(p, k, PR_N_OUT);
     if (blockIdx.x == 0) probeMark(p, k, PR_N_B0);
 }
@@ -1537,13 +1568,19 @@ __global__ __launch_bounds__(kBlock) void k_tail(Params p)
         if (k == 2) stageTables(ct, p.gTables, kFast ? p.nGeom : 0);   // only when an iteration runs
         coldConduits<false>(p, k, dt, ct, tid, nthr);
         const int cnt = __hip_atomic_load(&p.ucount[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        (void)linkListWalk<kFast>(p, k, cnt, dt, ct, tid, nthr);
+        int u0 = 0;
+        int2 rb0 = make_int2(0, 0);
+        if (tid < 4 * cnt) {
+            u0 = p.ulist[(size_t)((k - 1) & 1) * p.nN + (tid >> 2)];
+            rb0 = p.ulistRow[(size_t)((k - 1) & 1) * p.nN + (tid >> 2)];
+        }
+        (void)linkListWalk<kFast>(p, k, cnt, dt, ct, tid, nthr, u0, rb0);
         arrivals += gridDim.x;
         if (!tailBarrier(p, arrivals)) return;
         // the every-shape root finders (the cold conduits' callees): calling
         // the lean ones would loosen their register budget, and k_node's
         if (blockIdx.x * 64 < p.nOutLinks) outfallPrologue<false, true>(p, ct, &sh, false, k);
-        nodePass<false, kGeneral>(p, k, tid, nthr);
+        nodePass<false, kGeneral>(p, k, tid, nthr, loadNodePre(p, tid, k));
         arrivals += gridDim.x;
         if (!tailBarrier(p, arrivals)) return;
     }
