@@ -787,6 +787,22 @@ __device__ __forceinline__ int stepIterations(const Params& p, bool* converged)
 }
 
 
+// XCD-aware block order for the node passes (cdna_hip_programming.md §5.5
+// T1): workgroups are dealt round-robin over the 8 XCDs, so block b runs the
+// (b % 8)-th eighth of the logical blocks and each XCD sweeps one contiguous
+// node range per grid-stride round (a node's links, gathered by both end
+// nodes, then mostly meet in one L2).  Speed only: any placement gives the
+// same results (each index is still taken by exactly one thread).  Measured
+// on the surcharged 1M grid: k_node(0) 40.2 -> 38.5 us, k_node(1) 34.9 ->
+// 32.3 us; the streaming k_link got 1.7 us slower with it, so it keeps the
+// plain order.
+__device__ __forceinline__ int xcdBlock()
+{
+    const int g = (int)gridDim.x, b = (int)blockIdx.x;
+    if (g & 7) return b;
+    return (b & 7) * (g >> 3) + (b >> 3);
+}
+
 // measurement only: thread 0 stamps the wall clock into probe slot `slot` of
 // iteration k
 // (per workgroup: no atomics, whose serialisation would be what is measured;
@@ -1481,7 +1497,8 @@ template <bool kFirst, bool kGeneral, bool kProbe = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral ? 3 : 4))) void k_node(Params p, int k)
 {
     // the first node's flag words load alongside the convergence flag
-    const NodePre pre0 = loadNodePre(p, blockIdx.x * kBlock + threadIdx.x, kFirst ? 0 : k);
+    const int tidX = xcdBlock() * kBlock + threadIdx.x;
+    const NodePre pre0 = loadNodePre(p, tidX, kFirst ? 0 : k);
     if (k >= 2 && p.unconv[k - 1] == 0) return;
     probeMark(p, k, PR_N_IN);
     probeMark(p, k, PR_N_LAST_IN);
@@ -1500,7 +1517,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
         outfallPrologue<kFirst, kGeneral>(p, ct, &sh, true, k);
         if (blockIdx.x == 0) probeMark(p, k, PR_N_PRO);
     }
-    nodePass<kFirst, kGeneral>(p, k, blockIdx.x * kBlock + threadIdx.x, gridDim.x * kBlock, pre0);
+    nodePass<kFirst, kGeneral>(p, k, tidX, gridDim.x * kBlock, pre0);
     probeMark(p, k, PR_N_OUT);
     if (blockIdx.x == 0) probeMark(p, k, PR_N_B0);
 }
