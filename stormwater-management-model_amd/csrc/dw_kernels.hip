@@ -794,8 +794,8 @@ __device__ __forceinline__ int stepIterations(const Params& p, bool* converged)
 // nodes, then mostly meet in one L2).  Speed only: any placement gives the
 // same results (each index is still taken by exactly one thread).  Measured
 // on the surcharged 1M grid: k_node(0) 40.2 -> 38.5 us, k_node(1) 34.9 ->
-// 32.3 us; the streaming k_link got 1.7 us slower with it, so it keeps the
-// plain order.
+// 32.3 us; the streaming k_link (+1.7 us), k_step_end (+6 us) and
+// k_qual_node (+0.7 us) were slower with it and keep the plain order.
 __device__ __forceinline__ int xcdBlock()
 {
     const int g = (int)gridDim.x, b = (int)blockIdx.x;
