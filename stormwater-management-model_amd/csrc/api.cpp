@@ -172,6 +172,8 @@ static int execRouting()   // swmm5.c:514-575 + routing.c:203-265 on the device
     Router& r = *G->router;
     G->totalStepCount++;
     double currentDate = prj.getDateTime(G->newRoutingTime);
+    // no runoff: climate_setState for evaporation (swmm5.c:555-556)
+    if (r.setEvapRate(prj.climateSetState(currentDate))) return setErr(r.lastError(), r.lastErrorMsg());
     int rc;
     if (G->constantInflow) {
         rc = r.step(nullptr, nullptr, nullptr);

@@ -131,6 +131,7 @@ struct StepCtl {
     double newRoutingTime;            // msec (swmm5.c / routing.c clock mirror)
     double routingDuration;           // msec
     double routeStep;                 // fixed step (sec)
+    double evapRate;                  // Evap.rate (ft/s) of this step (host: climate_setState)
     unsigned tailBar;             // k_tail's grid-barrier arrivals (zeroed by k_link<first>)
     int tailErr;                  // k_tail gave up waiting at a barrier (never expected)
     int qualPar;                  // quality buffer holding the latest concentrations (Params::nQual)
@@ -170,7 +171,7 @@ struct Params {
     // options
     int surchargeMethod, inertDamping, normalFlowLtd, allowPonding, varStep;
     int forceMainEqn;             // FM_H_W or FM_D_W (FORCE_MAIN_EQUATION)
-    double crownCutoff, minSurfArea, headTol, evapRate, courantFactor, minRouteStep, routeStep;
+    double crownCutoff, minSurfArea, headTol, courantFactor, minRouteStep, routeStep;
     // link static
     const int2* lnodes;
     const uint32_t* lflags;
@@ -380,9 +381,10 @@ __device__ double conduitLossRate(const Params& p, int j, const Geom& x, double 
     double evapLossRate = 0.0, seepLossRate = 0.0, totalLossRate = 0.0;
     if (depth > 0.0001) {
         double len = p.length[j];
-        if (isOpen(x.type) && p.evapRate > 0.0) {
+        const double evapRate = p.ctl->evapRate;
+        if (isOpen(x.type) && evapRate > 0.0) {
             double topWidth = getWofY<kAll>(x, depth, ct);
-            evapLossRate = topWidth * len * p.evapRate;
+            evapLossRate = topWidth * len * evapRate;
         }
         double sr = p.seepRate[j];
         if (sr > 0.0) {
@@ -1029,7 +1031,7 @@ __device__ __attribute__((noinline)) double devStorageArea(const Params& p, int 
 __device__ __attribute__((noinline)) double devStorageLosses(const Params& p, int i, double depth,
                                                             double volume, double dt, double* evapVol)
 {
-    return storageLosses(devStorageGeom(p, i), p.stFEvap[i], p.evapRate, depth, volume, dt, evapVol);
+    return storageLosses(devStorageGeom(p, i), p.stFEvap[i], p.ctl->evapRate, depth, volume, dt, evapVol);
 }
 
 // A converged plain junction (not surcharged, ponded or flooded, no storage
@@ -2565,6 +2567,7 @@ struct Router::Impl {
         unsigned long long* pinned = nullptr;   // [0] iterations run, [1..] conduits updated, nodes gathered
     };
     std::vector<TimingSlot> tslots;
+    double evapRateDev = 0.0;         // the evaporation rate the device holds (StepCtl::evapRate)
     std::vector<double> probeSum;     // SWMM5_PROBE: [k][kProbeSlots + 1] phase microseconds, count
     double wallKHz = 100000.0;
     int tUsed = 0;
@@ -2959,7 +2962,6 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     p.crownCutoff = prj.opt.crownCutoff;
     p.minSurfArea = prj.opt.minSurfArea;
     p.headTol = prj.opt.headTol;
-    p.evapRate = prj.opt.evapRate;
     p.courantFactor = prj.opt.courantFactor;
     p.minRouteStep = prj.opt.minRouteStep;
     p.routeStep = prj.opt.routeStep;
@@ -2998,7 +3000,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (net.hasFlapGate[g]) f |= LF_FLAP;
         if (net.nodeType[n1] == OUTFALL) { f |= LF_N1_OUTFALL; if (net.outfallFlap[n1]) f |= LF_N1_OFLAP; }
         if (net.nodeType[n2] == OUTFALL) { f |= LF_N2_OUTFALL; if (net.outfallFlap[n2]) f |= LF_N2_OFLAP; }
-        if (net.seepRate[g] > 0.0 || (prj.opt.evapRate > 0.0 && isOpen(x.type))) f |= LF_SEEP;
+        if (net.seepRate[g] > 0.0 || (prj.evapCanBePositive() && isOpen(x.type))) f |= LF_SEEP;
         if (net.qLimit[g] > 0.0) f |= LF_QLIMIT;
         if (net.direction[g] < 0) f |= LF_DIRNEG;
         if (j >= nOwn) {
@@ -3546,6 +3548,8 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     hc->latTot[1] = d->latTot0[1];
     hc->latTot[2] = d->latTot0[2];
     hc->statsStart = prj.opt.reportStart;
+    hc->evapRate = prj.opt.evapRate;
+    d->evapRateDev = prj.opt.evapRate;
     {
         int h, m, sec;
         decodeTime(prj.opt.startDateTime, &h, &m, &sec);
@@ -4518,6 +4522,19 @@ int Router::repickStep(double cap, double durBefore, double durAfter)
     h->dt = dtn;
     HIPCHECK(hipMemcpy(d->ctl, d->hostCtl, sizeof(StepCtl), hipMemcpyHostToDevice));
     d->hostDt[d->launched % Impl::kRing] = dtn;            // the next step's slot
+    return 0;
+}
+
+// climate_setState's evaporation rate for the next step; uploaded only when it
+// changes (a month boundary or a time-series entry), behind the queued steps
+int Router::setEvapRate(double rate)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    if (rate == d->evapRateDev) return 0;
+    HIPCHECK(hipStreamSynchronize(d->stream));
+    HIPCHECK(hipMemcpy(&d->p.ctl->evapRate, &rate, sizeof(double), hipMemcpyHostToDevice));
+    d->evapRateDev = rate;
     return 0;
 }
 

@@ -78,7 +78,15 @@ struct Options {
     double startDate = 0, startTime = 0, endDate = 0, endTime = 0;
     double reportStartDate = -693594, reportStartTime = -693594;
     bool haveReportStartDate = false, haveReportStartTime = false;
-    double evapRate = 0.0;           // constant evaporation (ft/s)
+    double evapRate = 0.0;           // evaporation rate in force (ft/s): the CONSTANT value until
+                                     // the first routing step's climate_setState
+    // [EVAPORATION] (climate.c:285-365): 0 CONSTANT, 1 MONTHLY, 2 TIMESERIES;
+    // monthly values as input (user units); [ADJUSTMENTS] EVAPORATION (ft/s
+    // after validation, climate.c:525)
+    int evapType = 0;
+    double monthlyEvap[12] = {};
+    int evapSeries = -1;
+    double adjustEvap[12] = {};
     // derived
     double startDateTime = 0, endDateTime = 0, reportStart = 0, totalDuration = 0; // msec
 };

@@ -210,12 +210,12 @@ static bool getDouble(const char* s, double* y)
 enum Sect {
     S_NONE = -1, S_TITLE, S_OPTION, S_EVAP, S_JUNC, S_OUTFALL, S_CONDUIT, S_XSECT, S_LOSS,
     S_POLLUT, S_INFLOW, S_DWF, S_PATTERN, S_TSERIES, S_REPORT, S_FILES, S_STORAGE, S_CURVES,
-    S_PUMP, S_ORIFICE, S_WEIR, S_OUTLET, S_TRANSECT, S_DIVIDER, S_STREET, S_SKIP, S_UNSUPPORTED
+    S_PUMP, S_ORIFICE, S_WEIR, S_OUTLET, S_TRANSECT, S_DIVIDER, S_STREET, S_ADJUST, S_SKIP, S_UNSUPPORTED
 };
 static const char* const kSectWords[] = {
     "[TITLE", "[OPTION", "[EVAP", "[JUNC", "[OUTFALL", "[CONDUIT", "[XSECT", "[LOSS",
     "[POLLUT", "[INFLOW", "[DWF", "[PATTERN", "[TIMESERIES", "[REPORT", "[FILES", "[STORAGE",
-    "[CURVE", "[PUMP", "[ORIFICE", "[WEIR", "[OUTLET", "[TRANSECT", "[DIVIDER", "[STREET", nullptr};
+    "[CURVE", "[PUMP", "[ORIFICE", "[WEIR", "[OUTLET", "[TRANSECT", "[DIVIDER", "[STREET", "[ADJUST", nullptr};
 static const char* const kOffOnWords[] = {"OFF", "ON", nullptr};
 static const char* const kOrificeTypeWords[] = {"SIDE", "BOTTOM", nullptr};
 static const char* const kWeirTypeWords[] = {"TRANSVERSE", "SIDEFLOW", "V-NOTCH", "TRAPEZOIDAL",
@@ -505,6 +505,7 @@ int Project::parseLine(int sect, std::vector<char*>& tok, int pass)
     switch (sect) {
     case S_OPTION: return 0;
     case S_EVAP: return readEvap(tok);
+    case S_ADJUST: return readAdjust(tok);
     case S_JUNC: return readJunction(tok);
     case S_DIVIDER: return readDivider(tok);
     case S_OUTFALL: return readOutfall(tok);
@@ -674,18 +675,71 @@ int Project::readOption(const char* s1, const char* s2)  // project.c:445-769
     return 0;
 }
 
-int Project::readEvap(std::vector<char*>& tok)  // climate.c:285 (CONSTANT only)
+// climate_readEvapParams (climate.c:285-365): CONSTANT, MONTHLY and
+// TIMESERIES evaporation.  TEMPERATURE and FILE need a climate file (not on
+// the routing path); RECOVERY (infiltration) and DRY_ONLY (runoff) have no
+// routing effect and are read and checked only.
+int Project::readEvap(std::vector<char*>& tok)
 {
-    if (tok.size() < 2) return 203;
-    if (kmatch(tok[0], "CONSTANT")) {
+    static const char* const kEvapWords[] = {"CONSTANT", "MONTHLY", "TIMESERIES", "TEMPERATURE", "FILE",
+                                             "RECOVERY", "DRY_ONLY", nullptr};
+    const int nt = (int)tok.size();
+    const int k = kfind(tok[0], kEvapWords);
+    if (k < 0) return 205;
+    if (k == 5) {                                  // RECOVERY pattern
+        if (nt < 2) return 203;
+        return net.patternIndex.count(tok[1]) ? 0 : 209;
+    }
+    if (k == 6) {                                  // DRY_ONLY YES / NO
+        if (nt < 2) return 203;
+        return kfind(tok[1], kNoYes) >= 0 ? 0 : 205;
+    }
+    if (k == 3 || k == 4)
+        return setError(200, std::string("ERROR 200: EVAPORATION option ") + tok[0] +
+                                 " (climate file) is not supported by the MI355X engine");
+    if (nt < 2) return 203;
+    opt.evapType = k;
+    switch (k) {
+    case 0: {                                      // CONSTANT
         double x;
         if (!getDouble(tok[1], &x) || x < 0.0) return 211;
+        for (double& m : opt.monthlyEvap) m = x;
         opt.evapRate = x / ucfEvapRate();
         return 0;
     }
-    if (kmatch(tok[0], "DRY_ONLY")) return 0;
-    return setError(200, std::string("ERROR 200: EVAPORATION option ") + tok[0] +
-                             " is not supported by the MI355X engine (CONSTANT only)");
+    case 1:                                        // MONTHLY v1 ... v12
+        if (nt < 13) return 203;
+        for (int i = 0; i < 12; i++)
+            if (!getDouble(tok[i + 1], &opt.monthlyEvap[i]) || opt.monthlyEvap[i] < 0.0) return 211;
+        return 0;
+    default: {                                     // TIMESERIES name
+        auto it = net.tseriesIndex.find(tok[1]);
+        if (it == net.tseriesIndex.end()) return 209;
+        opt.evapSeries = it->second;
+        return 0;
+    }
+    }
+}
+
+// climate_readAdjustments (climate.c:377-452): the monthly evaporation
+// adjustments; TEMPERATURE / RAINFALL / CONDUCTIVITY act on runoff only and
+// are checked and ignored; the subcatchment patterns need subcatchments
+int Project::readAdjust(std::vector<char*>& tok)
+{
+    const int nt = (int)tok.size();
+    if (nt == 1) return 0;
+    static const char* const kAdjWords[] = {"TEMP", "EVAP", "RAIN", "CONDUCT", nullptr};
+    const int k = kfind(tok[0], kAdjWords);
+    if (k < 0)
+        return setError(200, std::string("ERROR 200: ADJUSTMENTS ") + tok[0] +
+                                 " (subcatchment patterns) is not supported by the MI355X engine");
+    if (nt < 13) return 203;
+    for (int i = 0; i < 12; i++) {
+        double x;
+        if (!getDouble(tok[i + 1], &x)) return 211;
+        if (k == 1) opt.adjustEvap[i] = x;
+    }
+    return 0;
 }
 
 // divider_readParams (node.c:1124-1212).  Under dynamic wave a flow divider
@@ -2454,6 +2508,21 @@ void Project::validate()  // project.c:186-270
     for (auto& ts : net.tseries)
         for (size_t i = 1; i < ts.x.size(); i++)
             if (ts.x[i] <= ts.x[i - 1]) { setError(173, "ERROR 173: time series " + ts.id + " has its data out of sequence."); return; }
+    // climate_validate (climate.c:521-528): monthly evaporation adjustments in ft/s
+    for (double& a : opt.adjustEvap) a /= ucfEvapRate();
+    if (opt.evapType == 2) {
+        // the reference walks the series' shared entry cursor for evaporation
+        // (table_getNextEntry); a series another object also reads would
+        // interleave two walks of that cursor, which is not modelled
+        bool shared = false;
+        for (const auto& in : net.extInflows) shared = shared || in.tseries == opt.evapSeries;
+        for (int s : net.outfallSeries) shared = shared || s == opt.evapSeries;
+        if (shared) {
+            setError(200, "ERROR 200: an evaporation time series that also feeds an inflow or an outfall "
+                          "is not supported by the MI355X engine");
+            return;
+        }
+    }
     for (const Divider& dv : net.dividers) {              // divider_validate (node.c:1216-1247)
         int i = dv.link;
         if (i < 0 || (net.node1[i] != dv.node && net.node2[i] != dv.node)) {
@@ -2667,6 +2736,7 @@ void Project::initDepths()
 
 int Project::initState()
 {
+    climateInit();                                  // project_init (project.c:295)
     int nn = net.nNodes(), nl = net.nLinks(), P = net.nPollut();
     const double* ct = &SWX_CIRC_TABLES[0][0];
     auto geom = [&](int j) {
@@ -2886,6 +2956,97 @@ StorageGeom Project::storageGeom(int j) const
 double Project::getDateTime(double elapsedMsec) const
 {
     return addSeconds(opt.startDateTime, (elapsedMsec + 1) / 1000.0);
+}
+
+// climate_initState (climate.c:598-626), the evaporation part.  StartDate
+// is the start's date without its time of day, as in the reference.
+void Project::climateInit()
+{
+    nextEvapDate_ = opt.startDate;
+    nextEvapRate_ = 0.0;
+    evapCursor_ = 0;
+    if (opt.evapType == 2 && opt.evapSeries >= 0) {
+        const Tseries& t = net.tseries[opt.evapSeries];
+        if (!t.x.empty()) {                        // table_getFirstEntry
+            nextEvapDate_ = t.x[0];
+            nextEvapRate_ = t.y[0];
+            evapCursor_ = 0;
+        }
+        if (nextEvapDate_ < opt.startDate) setNextEvapDate(opt.startDate);
+        opt.evapRate = nextEvapRate_ / ucfEvapRate();
+        setNextEvapDate(nextEvapDate_);
+        // project_init then runs table_tseriesInit on every series
+        // (project.c:297): the cursor goes to the series' second entry
+        evapCursor_ = (t.x.size() > 1) ? 1 : 0;
+    }
+}
+
+// setNextEvapDate (climate.c:671-725): CONSTANT, MONTHLY, TIMESERIES
+void Project::setNextEvapDate(double theDate)
+{
+    if (nextEvapDate_ > theDate) return;
+    switch (opt.evapType) {
+    case 0:
+        nextEvapDate_ = theDate + 365.;
+        break;
+    case 1: {
+        int yr, mon, day;
+        decodeDate(theDate, &yr, &mon, &day);
+        if (mon == 12) { mon = 1; yr++; }
+        else mon++;
+        nextEvapDate_ = encodeDate(yr, mon, 1);
+        break;
+    }
+    default:
+        if (opt.evapSeries >= 0) {
+            const Tseries& t = net.tseries[opt.evapSeries];
+            nextEvapDate_ = theDate + 365.;
+            // table_getNextEntry from the cursor, entries up to EndDateTime
+            while (evapCursor_ + 1 < t.x.size() && t.x[evapCursor_ + 1] <= opt.endDateTime) {
+                evapCursor_++;
+                const double d = t.x[evapCursor_], e = t.y[evapCursor_];
+                if (d >= theDate) {
+                    nextEvapDate_ = d;
+                    nextEvapRate_ = e;
+                    break;
+                }
+            }
+        }
+        break;
+    }
+}
+
+// climate_setState (climate.c:641-655) -> setEvap (876-911): the rate for the
+// routing step starting at theDate (swmm5.c:556 without runoff)
+double Project::climateSetState(double theDate)
+{
+    const int mon = monthOfYear(theDate);
+    switch (opt.evapType) {
+    case 0: opt.evapRate = opt.monthlyEvap[0] / ucfEvapRate(); break;
+    case 1: opt.evapRate = opt.monthlyEvap[mon - 1] / ucfEvapRate(); break;
+    default:
+        if (theDate >= nextEvapDate_) opt.evapRate = nextEvapRate_ / ucfEvapRate();
+        break;
+    }
+    // the climate change adjustment is added at every call (for a time series
+    // the unrefreshed rate keeps the earlier additions, as in the reference)
+    opt.evapRate += opt.adjustEvap[mon - 1];
+    setNextEvapDate(theDate);
+    return opt.evapRate;
+}
+
+bool Project::evapCanBePositive() const
+{
+    bool adj = false;
+    for (double a : opt.adjustEvap) adj = adj || a != 0.0;
+    if (opt.evapType == 0) return opt.evapRate > 0.0 || adj;
+    if (opt.evapType == 1) {
+        for (double m : opt.monthlyEvap) adj = adj || m > 0.0;
+        return adj;
+    }
+    if (opt.evapSeries >= 0)
+        for (double y : net.tseries[opt.evapSeries].y) adj = adj || y > 0.0;
+    return adj;
 }
 
 double Project::patternFactor(int p, int month, int day, int hour) const  // inflow.c:456-484

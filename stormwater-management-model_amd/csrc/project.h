@@ -62,6 +62,12 @@ public:
     void evalInflows(double currentDate, std::vector<double>& lat, std::vector<double>* qualLoad,
                      double* dwfTotal, double* extTotal, double* extOutTotal);
     bool inflowsAreConstant() const;        // no time series / patterns
+    // climate_initState / climate_setState for evaporation (climate.c:598-637,
+    // 641-655, 671-725, 876-911): the rate (ft/s) in force for the routing
+    // step that starts at theDate
+    void climateInit();
+    double climateSetState(double theDate);
+    bool evapCanBePositive() const;         // some step may evaporate (open conduits then carry LF_SEEP)
     double getDateTime(double elapsedMsec) const;  // swmm5.c:1543
     StorageGeom storageGeom(int node) const;        // storage unit j's area relation
     NcLink ncLink(int link) const;                  // pump / orifice / weir / outlet j
@@ -109,6 +115,13 @@ private:
     int readTimeseries(std::vector<char*>& tok);
     int readReport(std::vector<char*>& tok);
     int readEvap(std::vector<char*>& tok);
+    int readAdjust(std::vector<char*>& tok);
+    // evaporation state (climate.c NextEvapDate / NextEvapRate, and the time
+    // series' entry cursor, private to evaporation: a series evaporation
+    // reads is used by nothing else)
+    double nextEvapDate_ = 0.0, nextEvapRate_ = 0.0;
+    size_t evapCursor_ = 0;
+    void setNextEvapDate(double theDate);
     void validate();
     void validateConduit(int j);
     double patternFactor(int p, int month, int day, int hour) const;

@@ -63,6 +63,8 @@ public:
     // swmm_setValue(NODE_HEAD) on an outfall: FIXED type with this stage (ft)
     // (setOutfallStage, swmm5.c:1173-1188)
     int setOutfallStage(int g, double stage);
+    // Evap.rate (ft/s) for the steps launched from now on (climate_setState)
+    int setEvapRate(double rate);
     // swmm_setValue(ROUTESTEP) between steps (setRoutingStep, swmm5.c:1360-
     // 1370): fixed steps of `step` sec from now on, next step dtNext sec
     int setRouteStep(double step, double dtNext);

@@ -417,7 +417,7 @@ def write_example(path: str, *, route_step: float = 5.0,
                   culverts: bool = False, tidal: bool = False, roadway: bool = False,
                   dividers: bool = False, streets: bool = False, extfile: bool = False,
                   options: dict | None = None, ponding: bool = False,
-                  branches: bool = False, dummy: bool = False) -> None:
+                  branches: bool = False, dummy: bool = False, evap: str = "") -> None:
     """Write the authored Example network (see module docstring).  `files`
     is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf");
     `storage` turns six junctions into storage units (_STORAGE); `options`
@@ -430,7 +430,10 @@ def write_example(path: str, *, route_step: float = 5.0,
     `dummy` makes C4 and C9 DUMMY conduits (the only outflow links of N5 and
     N10; C9 with a 1.5 cfs flow limit): routed as non-conduit links that pass
     their upstream node's inflow (dynwave.c:416-419, link.c:543-560,
-    1320-1330)."""
+    1320-1330);
+    `evap` ("MONTHLY" or "TIMESERIES") replaces the evaporation data with
+    monthly or time-series rates plus monthly [ADJUSTMENTS], on a run that
+    crosses from January into February (climate.c:598-725, 876-911)."""
     if pollutants:
         pollut = ("TSS MG/L 0 0 0 0.5 NO * 0 20 0\n"
                   "BOD MG/L 0 0 0 0 NO * 0 10 0\n")
@@ -557,6 +560,22 @@ def write_example(path: str, *, route_step: float = 5.0,
         txt = txt.replace("C4  RECT_OPEN    2.0  3.0  0    0  1", "C4  DUMMY        0    0    0    0  1", 1)
         txt = txt.replace("C9  TRAPEZOIDAL  2.0  2.0  1.5  1.5 1", "C9  DUMMY        0    0    0    0  1", 1)
         txt = txt.replace("C9  N10 N8  300  0.014  0.5  0    0  0", "C9  N10 N8  300  0.014  0.5  0    0  1.5", 1)
+    if evap:
+        txt = "\n".join(ln for ln in txt.split("\n")
+                        if ln.split()[:1] not in (["CONSTANT"], ["DRY_ONLY"], ["[EVAPORATION]"]))
+        if evap == "MONTHLY":
+            txt += "\n[EVAPORATION]\nMONTHLY  3.0 8.0 1 1 1 1 1 1 1 1 1 1\nDRY_ONLY NO\n"
+        else:
+            txt += "\n[EVAPORATION]\nTIMESERIES EV1\n"
+            txt = txt.replace("[TIMESERIES]\n;;Name Date Time Value\n",
+                              "[TIMESERIES]\n;;Name Date Time Value\n"
+                              "EV1 01/31/2020 22:00 2.0\nEV1 01/31/2020 23:20 6.0\nEV1 01/31/2020 23:50 1.5\n"
+                              "EV1 02/01/2020 00:15 9.0\nEV1 02/01/2020 00:40 4.0\n", 1)
+        txt += "\n[ADJUSTMENTS]\nEVAPORATION 0.5 -0.2 0 0 0 0 0 0 0 0 0 0\n"
+        options = dict(options or {})
+        options.update({"START_DATE": "01/31/2020", "START_TIME": "23:00:00",
+                        "REPORT_START_DATE": "01/31/2020", "REPORT_START_TIME": "23:00:00",
+                        "END_DATE": "02/01/2020", "END_TIME": end_time})
     if options:
         lines = txt.split("\n")
         for key, val in options.items():

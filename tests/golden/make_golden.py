@@ -114,6 +114,10 @@ CASES = {
     # every flow class (dwflow.c:297-413): backwater over an invert offset and
     # a weir crest (UP_CRITICAL), a depth-curve pump below its curve (DN_DRY)
     "example_branches": (netgen.write_example, dict(end_time="01:40:00", route_step=5.0, branches=True), 1),
+    "example_evap_monthly": (netgen.write_example, dict(end_time="01:00:00", route_step=5.0, storage=True,
+                                                        evap="MONTHLY"), 1),
+    "example_evap_series": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
+                                                       variable_step=0.75, storage=True, evap="TIMESERIES"), 1),
     "example_dummy": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, dummy=True,
                                                  pollutants=True), 1),
     "example_dummy_var": (netgen.write_example, dict(end_time="02:00:00", route_step=10.0, variable_step=0.75,
