@@ -1294,7 +1294,7 @@ struct NodePre {
 __device__ __forceinline__ NodePre loadNodePre(const Params& p, int i, int k)
 {
     NodePre q{0u, 0, 0};
-    if (i < p.nN) {
+    if ((unsigned)i < (unsigned)p.nN) {
         q.nf = p.nflags[i];
         if (k >= 2) {
             q.cache = p.dirty[i];
@@ -1498,8 +1498,13 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
 template <bool kFirst, bool kGeneral, bool kProbe = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral ? 3 : 4))) void k_node(Params p, int k)
 {
-    // the first node's flag words load alongside the convergence flag
-    const int tidX = xcdBlock() * kBlock + threadIdx.x;
+    // the first node's flag words load alongside the convergence flag.  With
+    // at most 64 outfall links, block 0 runs the outfall prologue only (it is
+    // the launch's long pole: serial root finding) and the other blocks take
+    // the nodes; xcdBlock() maps block 0 to 0 either way
+    const bool proOnly = p.nOutLinks > 0 && p.nOutLinks <= 64 && gridDim.x > 1;
+    const int nodeBlocks = (int)gridDim.x - (proOnly ? 1 : 0);
+    const int tidX = (xcdBlock() - (proOnly ? 1 : 0)) * kBlock + (int)threadIdx.x;
     const NodePre pre0 = loadNodePre(p, tidX, kFirst ? 0 : k);
     if (k >= 2 && p.unconv[k - 1] == 0) return;
     probeMark(p, k, PR_N_IN);
@@ -1518,8 +1523,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
         __shared__ OutfallLds sh;
         outfallPrologue<kFirst, kGeneral>(p, ct, &sh, true, k);
         if (blockIdx.x == 0) probeMark(p, k, PR_N_PRO);
+        if (proOnly) {
+            probeMark(p, k, PR_N_OUT);
+            probeMark(p, k, PR_N_B0);
+            return;
+        }
     }
-    nodePass<kFirst, kGeneral>(p, k, tidX, gridDim.x * kBlock, pre0);
+    nodePass<kFirst, kGeneral>(p, k, tidX, nodeBlocks * kBlock, pre0);
     probeMark(p, k, PR_N_OUT);
     if (blockIdx.x == 0) probeMark(p, k, PR_N_B0);
 }
