@@ -2090,7 +2090,7 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
     const bool stats = !(aDate < c->statsStart);
     // convergence of this step (dynwave.c:242-257): nodes count non-convergence
     bool converged;
-    const int steps = stepIterations(p, &converged);
+    [[maybe_unused]] const int steps = stepIterations(p, &converged);
     const StatsDev& S = p.st;
     int n = gridDim.x * kBlock;
     int tid = blockIdx.x * kBlock + threadIdx.x;

@@ -156,6 +156,40 @@ SWX_HD double invLookup(double y, const double* t, int nItems)
     return x;
 }
 
+// Device forms of the Newton solves' transcendentals.  A single lane runs
+// these solves (the outfall prologue's normal depth), so their instruction
+// count is their latency: on the device sin and cos share one argument
+// reduction (sincos) and x^(1/3), x^(2/3) are taken from cbrt rather than
+// the general pow (a log and an exp in extended precision).  The results
+// differ from glibc's by a few ulp, as OCML's sin, cos and pow already do;
+// the host keeps the reference's calls, bit-identical.
+SWX_HD void swxSinCos(double t, double* s, double* c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    sincos(t, s, c);
+#else
+    *s = sin(t);
+    *c = cos(t);
+#endif
+}
+SWX_HD double swxPowThird(double x)           // pow(x, 1/3) (NaN below 0, as pow)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return x < 0.0 ? __builtin_nan("") : cbrt(x);
+#else
+    return pow(x, 1. / 3.);
+#endif
+}
+SWX_HD double swxPowTwoThirds(double x)       // pow(x, 2/3) (NaN below 0, as pow)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double c = cbrt(x);
+    return x < 0.0 ? __builtin_nan("") : c * c;
+#else
+    return pow(x, 2. / 3.);
+#endif
+}
+
 // xsect.c:2573-2591 -- Newton solve of theta - sin(theta) = 2 pi alpha
 SWX_HD_COLD double thetaOfAlpha(double alpha)
 {
@@ -166,7 +200,9 @@ SWX_HD_COLD double thetaOfAlpha(double alpha)
     double ap = (2.0 * 3.141592654) * alpha;
     #pragma unroll 1
     for (int k = 1; k <= 40; k++) {
-        double d = -(ap - theta + sin(theta)) / (1.0 - cos(theta));
+        double st, cth;
+        swxSinCos(theta, &st, &cth);
+        double d = -(ap - theta + st) / (1.0 - cth);
         if (d > 1.0) d = (d >= 0.0 ? fabs(1.0) : -fabs(1.0));
         theta = theta - d;
         if (fabs(d) <= 0.0001) return theta;
@@ -187,11 +223,13 @@ SWX_HD_COLD double thetaOfPsi(double psi)
     #pragma unroll 1
     for (int k = 1; k <= 40; k++) {
         theta = fabs(theta);
-        double tt = theta - sin(theta);
-        double tt23 = pow(tt, 2. / 3.);
-        double t3 = pow(theta, 1. / 3.);
+        double st, cth;
+        swxSinCos(theta, &st, &cth);
+        double tt = theta - st;
+        double tt23 = swxPowTwoThirds(tt);
+        double t3 = swxPowThird(theta);
         double d = ap * theta / t3 - tt * tt23;
-        d = d / (ap * (2. / 3.) / t3 - (5. / 3.) * tt23 * (1.0 - cos(theta)));
+        d = d / (ap * (2. / 3.) / t3 - (5. / 3.) * tt23 * (1.0 - cth));
         theta = theta - d;
         if (fabs(d) <= 0.0001) return theta;
     }
