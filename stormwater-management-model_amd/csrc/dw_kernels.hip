@@ -1161,7 +1161,7 @@ __device__ __forceinline__ int outLinkAt(const Params& p, int c)
 // (outfallCombine).  stage: the tables are staged into ct here, after the
 // first round's operand loads are issued (they then travel together)
 template <bool kFirst, bool kGeneral>
-__device__ __forceinline__ void outfallPrologue(const Params& p, double* ct, OutfallLds* sh, bool stage,
+__device__ __forceinline__ void outfallPrologue(const Params& p, const double* ct, OutfallLds* sh, bool stage,
                                                 int kProbeK = 0)
 {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1192,7 +1192,7 @@ __device__ __forceinline__ void outfallPrologue(const Params& p, double* ct, Out
         }
         // the group's first conduit's tabulated critical flows (static)
         const double qcs0 = (w >= 1 && g < nHere && gl <= 25) ? p.ofQcs[26 * (base + g) + gl] : 0.0;
-        if (stage) { stageTables(ct, p.gTables); stage = false; }
+        if (stage) { stageTables(const_cast<double*>(ct), p.gTables); stage = false; }
         if (base == 0) probeMark(p, kProbeK, PR_P_STAGED);
         double yn = 0.0;                               // non-conduits: yNorm = yCrit = 0
         if (w == 0 && cond) yn = linkYnorm<kGeneral>(x, q, qMax, beta, ct);
@@ -1518,10 +1518,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
     // bypassed and the depth is refreshed every iteration, as in the reference.
     // 64 outfall conduits per block and round: wave 0 finds their normal
     // depths while wave 1 finds their critical depths, then wave 0 combines.
+    // The prologue reads the circular tables from global memory: the small
+    // flows an outfall usually carries take the closed-form Newton solves and
+    // never touch them, and staging them into LDS (a load round and a
+    // barrier) sat in front of the solves
     if (blockIdx.x * 64 < p.nOutLinks) {
-        __shared__ double ct[5 * SWX_CIRC_N];
         __shared__ OutfallLds sh;
-        outfallPrologue<kFirst, kGeneral>(p, ct, &sh, true, k);
+        outfallPrologue<kFirst, kGeneral>(p, p.gTables, &sh, false, k);
         if (blockIdx.x == 0) probeMark(p, k, PR_N_PRO);
         if (proOnly) {
             probeMark(p, k, PR_N_OUT);
