@@ -1484,13 +1484,18 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
     int gathered = 0, live = 0, fast = 0;          // measurement only (countWork)
     int* ulist = p.ulist + (size_t)(k & 1) * p.nN;
     int2* urow = p.ulistRow + (size_t)(k & 1) * p.nN;
+    NodePre pre = pre0;
     for (int i = tid; i < p.nN; i += nthr) {
         bool listMe = false;                   // unconverged after this iteration
         int2 row = make_int2(0, 0);            // its CSR row, for the next walk
-        const NodePre pre = (i == tid) ? pre0 : loadNodePre(p, i, k);
+        // the thread's next node's flag words load ahead of this node's
+        // update: a sparse iteration skips most nodes on their flags alone,
+        // so a thread's nodes cost one load latency, not one each
+        const NodePre preNext = loadNodePre(p, i + nthr, k);
         nodeItem<kFirst, kGeneral>(p, k, i, dt, pre, listMe, row, anyUnconv, gathered, live, fast);
         // list this iteration's unconverged nodes for the next k_link
         if (!kFirst) waveAppend(listMe, i, row, &p.ucount[k], ulist, urow);
+        pre = preNext;
     }
     nodePassEnd(p, k, anyUnconv, gathered, live, fast, !kFirst && k >= 2);
 }

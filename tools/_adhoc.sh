@@ -6,4 +6,4 @@ b() { # tag env...
   tail -1 gpurun_out/b_$tag.log | python -c "import json,sys; b=json.loads(sys.stdin.read()); o=b['roofline']['other_kernels']; print('$tag', b['value'], b['ms_per_step'], o['k_node<first>']['avg_launch_us'], o['k_node iteration 1']['avg_launch_us'], o['k_node iterations>=2']['avg_launch_us'])"
 }
 H=stormwater-management-model_amd/libswmm5_head.so
-for r in 1 2 3 4; do b head$r SWMM5_LIB=$H; b new$r X=1; done
+for r in 1 2; do b head$r SWMM5_LIB=$H; b new8_$r X=1; b new4_$r SWMM5_NODE_SPARSE_GRID_FACTOR=4; b new2_$r SWMM5_NODE_SPARSE_GRID_FACTOR=2; done
