@@ -213,31 +213,64 @@ static int execRouting()   // swmm5.c:514-575 + routing.c:203-265 on the device
     return 0;
 }
 
+// output_saveResults (output.c:457-505) for the period ending at reportTime:
+// interpolated point results, or with REPORT AVERAGES the period's averages
+static void saveOutput(bool averages)
+{
+    double sys[6];
+    G->router->stepTotals(G->sysStep);
+    // StepFlowTotals of this step: {flooding, outflow, dw, gw, ii, ex}
+    sys[0] = G->sysStep[2];
+    sys[1] = G->sysStep[3];
+    sys[2] = G->sysStep[0];
+    sys[3] = 0.0;
+    sys[4] = 0.0;
+    sys[5] = G->sysStep[1];
+    Project& prj = *G->prj;
+    double reportDate = prj.getDateTime(G->reportTime);
+    if (reportDate < prj.opt.reportStart) return;     // (the averages keep accumulating)
+    const float *nv = nullptr, *lv = nullptr, *an = nullptr, *al = nullptr;
+    const double* depth = nullptr;
+    if (averages) {
+        if (G->router->avgTake(prj.ucfLength(), prj.ucfVolume(), prj.ucfFlow(), &an, &al, &nv, &lv, &depth)) {
+            setErr(G->router->lastError(), G->router->lastErrorMsg());
+            return;
+        }
+    } else {
+        // interpolation weight between the bracketing steps (output.c:645)
+        double f = (G->reportTime - G->oldRoutingTime) / (G->newRoutingTime - G->oldRoutingTime);
+        if (G->router->packResults(f, prj.ucfLength(), prj.ucfVolume(), prj.ucfFlow(), &nv, &lv)) {
+            setErr(G->router->lastError(), G->router->lastErrorMsg());
+            return;
+        }
+    }
+    int e = G->out.saveResults(prj, reportDate, nv, lv, sys, an, al, depth, prj.ucfLength());
+    if (e) setErr(e, "ERROR 309: cannot write to binary results file.");
+}
+
+static void updateAvg()      // output_updateAvgResults (output.c:857-907)
+{
+    Project& prj = *G->prj;
+    if (G->router->avgUpdate(prj.ucfLength(), prj.ucfVolume(), prj.ucfFlow()))
+        setErr(G->router->lastError(), G->router->lastErrorMsg());
+}
+
 static void saveResults()   // swmm5.c:579-613
 {
+    const bool averages = G->prj->rpt.averages != 0;
     if (G->newRoutingTime >= G->reportTime) {
-        double sys[6];
-        // StepFlowTotals of this step: {flooding, outflow, dw, gw, ii, ex}
-        sys[0] = G->sysStep[2];
-        sys[1] = G->sysStep[3];
-        sys[2] = G->sysStep[0];
-        sys[3] = 0.0;
-        sys[4] = 0.0;
-        sys[5] = G->sysStep[1];
-        Project& prj = *G->prj;
-        double reportDate = prj.getDateTime(G->reportTime);
-        if (reportDate >= prj.opt.reportStart) {
-            // interpolation weight between the bracketing steps (output.c:645)
-            double f = (G->reportTime - G->oldRoutingTime) / (G->newRoutingTime - G->oldRoutingTime);
-            const float *nv = nullptr, *lv = nullptr;
-            if (G->router->packResults(f, prj.ucfLength(), prj.ucfVolume(), prj.ucfFlow(), &nv, &lv)) {
-                setErr(G->router->lastError(), G->router->lastErrorMsg());
-                return;
-            }
-            int e = G->out.saveResults(prj, reportDate, nv, lv, sys);
-            if (e) setErr(e, "ERROR 309: cannot write to binary results file.");
+        if (averages) {
+            // the latest results join the period's averages when it ends
+            // exactly now; past its end they open the next period's
+            if (G->newRoutingTime == G->reportTime) updateAvg();
+            if (!G->errorCode) saveOutput(true);
+            if (!G->errorCode && G->newRoutingTime > G->reportTime) updateAvg();
+        } else {
+            saveOutput(false);
         }
         G->reportTime = G->reportTime + 1000 * (double)G->prj->opt.reportStep;
+    } else if (averages) {
+        updateAvg();
     }
 }
 
@@ -251,10 +284,7 @@ int DLLEXPORT swmm_step(double* elapsedTime)
     if (G->newRoutingTime < G->routingDuration) {
         if (execRouting()) return G->errorCode;
     }
-    if (G->saveFlag && G->newRoutingTime >= G->reportTime) {
-        G->router->stepTotals(G->sysStep);
-        saveResults();
-    }
+    if (G->saveFlag && (G->newRoutingTime >= G->reportTime || G->prj->rpt.averages)) saveResults();
     if (G->newRoutingTime < G->routingDuration) G->elapsedTime = G->newRoutingTime / kMsecPerDay;
     else G->elapsedTime = 0.0;
     if (elapsedTime) *elapsedTime = G->elapsedTime;

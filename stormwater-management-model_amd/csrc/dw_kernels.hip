@@ -2540,6 +2540,41 @@ __global__ __launch_bounds__(kBlock) void k_pack_results(Params p, double f, dou
     }
 }
 
+// REPORT AVERAGES: output_updateAvgResults (output.c:857-907) on the current
+// results packed by k_pack_results with f = 1 (node_getResults(i, 1.0),
+// link_getResults(i, 1.0)).  The sums are float32, as the reference's REAL4
+// accumulators; a non-conduit link's capacity entry (pump speed, regulator
+// opening) is not averaged: it holds the current value times the step count
+// plus one, which the average returns.
+__global__ __launch_bounds__(kBlock) void k_avg_accum(Params p, const float* resN, const float* resL,
+                                                      float* avgN, float* avgL, float stepsPlus1)
+{
+    const size_t nv = (size_t)(6 + p.P), lv = (size_t)(5 + p.P);
+    const size_t nN = (size_t)p.nN * nv, nL = (size_t)p.nL * lv, n = (size_t)gridDim.x * kBlock;
+    for (size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x; t < nN; t += n) avgN[t] += resN[t];
+    for (size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x; t < nL; t += n) {
+        const size_t j = t / lv;
+        const uint32_t fl = p.lflags[j];
+        if (t - j * lv == 4 && (fl & LF_NC) && !(fl & LF_DUMMY)) avgL[t] = resL[t] * stepsPlus1;
+        else avgL[t] += resL[t];
+    }
+}
+// output_saveAvgResults (output.c:911-955): sum / Nsteps in float32, then the
+// sums reset (output_initAvgResults, output.c:839-853)
+__global__ __launch_bounds__(kBlock) void k_avg_take(size_t nN, size_t nL, float* avgN, float* avgL, float* outN,
+                                                     float* outL, float steps)
+{
+    const size_t n = (size_t)gridDim.x * kBlock;
+    for (size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x; t < nN; t += n) {
+        outN[t] = avgN[t] / steps;
+        avgN[t] = 0.0f;
+    }
+    for (size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x; t < nL; t += n) {
+        outL[t] = avgL[t] / steps;
+        avgL[t] = 0.0f;
+    }
+}
+
 // ===========================================================================
 //  Router implementation
 // ===========================================================================
@@ -2555,6 +2590,11 @@ struct Router::Impl {
     std::string xerrMsg;             // last failed collective / transfer
     float *resN = nullptr, *resL = nullptr;          // packed period results (device)
     float *resNHost = nullptr, *resLHost = nullptr;  // pinned copies
+    float *avgN = nullptr, *avgL = nullptr;          // REPORT AVERAGES: the period's sums
+    float *avgON = nullptr, *avgOL = nullptr;        // and its averages (device)
+    float *avgONHost = nullptr, *avgOLHost = nullptr;
+    double* depthHost = nullptr;
+    int avgSteps = 0;                                // output.c Nsteps
     std::vector<hipEvent_t> forkEv, joinEv;   // per Picard iteration (cold-conduit fork / join)
     hipGraphExec_t graph = nullptr;
     // step graph whose iterations k >= 2 run in k_tail (Router::step picks
@@ -2641,6 +2681,9 @@ Router::~Router()
         if (d_->hostX) (void)hipHostFree(d_->hostX);
         if (d_->resNHost) (void)hipHostFree(d_->resNHost);
         if (d_->resLHost) (void)hipHostFree(d_->resLHost);
+        if (d_->avgONHost) (void)hipHostFree(d_->avgONHost);
+        if (d_->avgOLHost) (void)hipHostFree(d_->avgOLHost);
+        if (d_->depthHost) (void)hipHostFree(d_->depthHost);
         if (d_->comm) (void)ncclCommDestroy(d_->comm);
         for (auto e : d_->clockEv) if (e) (void)hipEventDestroy(e);
         for (auto e : d_->ringEv) if (e) (void)hipEventDestroy(e);
@@ -4569,21 +4612,18 @@ int Router::setRouteStep(double step, double dtNext)
     return 0;
 }
 
-int Router::packResults(double f, double uL, double uV, double uQ, const float** nodeVals,
-                        const float** linkVals)
+// k_pack_results into d->resN / d->resL (allocated on first use), on the stream
+static int launchPack(Router::Impl* d, double f, double uL, double uV, double uQ, std::string* msg)
 {
-    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
-    Impl* d = d_;
     const Params& p = d->p;
     size_t nb = (size_t)p.nN * (6 + p.P), lb = (size_t)p.nL * (5 + p.P);
+    hipError_t e = hipSuccess;
     if (!d->resN) {
-        hipError_t e;
         d->resN = devAlloc<float>(d, nb, &e);
-        if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
-        d->resL = devAlloc<float>(d, lb, &e);
-        if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
-        HIPCHECK(hipHostMalloc((void**)&d->resNHost, std::max<size_t>(nb, 1) * sizeof(float), hipHostMallocDefault));
-        HIPCHECK(hipHostMalloc((void**)&d->resLHost, std::max<size_t>(lb, 1) * sizeof(float), hipHostMallocDefault));
+        if (e == hipSuccess) d->resL = devAlloc<float>(d, lb, &e);
+        if (e == hipSuccess) e = hipHostMalloc((void**)&d->resNHost, std::max<size_t>(nb, 1) * sizeof(float), hipHostMallocDefault);
+        if (e == hipSuccess) e = hipHostMalloc((void**)&d->resLHost, std::max<size_t>(lb, 1) * sizeof(float), hipHostMallocDefault);
+        if (e != hipSuccess) { *msg = hipGetErrorString(e); return 1; }
     }
     int grid = std::max(d->gridL, d->gridN);
     if (d->fastLinks)
@@ -4592,7 +4632,89 @@ int Router::packResults(double f, double uL, double uV, double uQ, const float**
     else
         hipLaunchKernelGGL(k_pack_results<false>, dim3(grid), dim3(kBlock), 0, d->stream, p, f, uL, uV, uQ,
                            d->resN, d->resL);
+    e = hipGetLastError();
+    if (e != hipSuccess) { *msg = hipGetErrorString(e); return 1; }
+    return 0;
+}
+
+int Router::avgUpdate(double uL, double uV, double uQ)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    const Params& p = d->p;
+    size_t nb = (size_t)p.nN * (6 + p.P), lb = (size_t)p.nL * (5 + p.P);
+    std::string m;
+    if (launchPack(d, 1.0, uL, uV, uQ, &m)) { fail(m); return err_; }
+    if (!d->avgN) {
+        hipError_t e;
+        d->avgN = devAlloc<float>(d, nb, &e);
+        if (e == hipSuccess) d->avgL = devAlloc<float>(d, lb, &e);
+        if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+        HIPCHECK(hipMemsetAsync(d->avgN, 0, std::max<size_t>(nb, 1) * sizeof(float), d->stream));
+        HIPCHECK(hipMemsetAsync(d->avgL, 0, std::max<size_t>(lb, 1) * sizeof(float), d->stream));
+    }
+    int grid = std::max(d->gridL, d->gridN);
+    hipLaunchKernelGGL(k_avg_accum, dim3(grid), dim3(kBlock), 0, d->stream, p, d->resN, d->resL, d->avgN, d->avgL,
+                       (float)(d->avgSteps + 1));
     HIPCHECK(hipGetLastError());
+    d->avgSteps++;
+    return 0;
+}
+
+int Router::avgTake(double uL, double uV, double uQ, const float** avgNode, const float** avgLink,
+                    const float** curNode, const float** curLink, const double** depth)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    const Params& p = d->p;
+    size_t nb = (size_t)p.nN * (6 + p.P), lb = (size_t)p.nL * (5 + p.P);
+    std::string m;
+    if (launchPack(d, 1.0, uL, uV, uQ, &m)) { fail(m); return err_; }
+    if (!d->avgON) {
+        hipError_t e;
+        if (!d->avgN) {
+            d->avgN = devAlloc<float>(d, nb, &e);
+            if (e == hipSuccess) d->avgL = devAlloc<float>(d, lb, &e);
+            if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+            HIPCHECK(hipMemsetAsync(d->avgN, 0, std::max<size_t>(nb, 1) * sizeof(float), d->stream));
+            HIPCHECK(hipMemsetAsync(d->avgL, 0, std::max<size_t>(lb, 1) * sizeof(float), d->stream));
+        }
+        d->avgON = devAlloc<float>(d, nb, &e);
+        if (e == hipSuccess) d->avgOL = devAlloc<float>(d, lb, &e);
+        if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+        HIPCHECK(hipHostMalloc((void**)&d->avgONHost, std::max<size_t>(nb, 1) * sizeof(float), hipHostMallocDefault));
+        HIPCHECK(hipHostMalloc((void**)&d->avgOLHost, std::max<size_t>(lb, 1) * sizeof(float), hipHostMallocDefault));
+        HIPCHECK(hipHostMalloc((void**)&d->depthHost, std::max<int>(p.nN, 1) * sizeof(double), hipHostMallocDefault));
+    }
+    int grid = std::max(d->gridL, d->gridN);
+    hipLaunchKernelGGL(k_avg_take, dim3(grid), dim3(kBlock), 0, d->stream, nb, lb, d->avgN, d->avgL, d->avgON,
+                       d->avgOL, (float)d->avgSteps);
+    HIPCHECK(hipGetLastError());
+    d->avgSteps = 0;
+    HIPCHECK(hipMemcpyAsync(d->avgONHost, d->avgON, nb * sizeof(float), hipMemcpyDeviceToHost, d->stream));
+    HIPCHECK(hipMemcpyAsync(d->avgOLHost, d->avgOL, lb * sizeof(float), hipMemcpyDeviceToHost, d->stream));
+    HIPCHECK(hipMemcpyAsync(d->resNHost, d->resN, nb * sizeof(float), hipMemcpyDeviceToHost, d->stream));
+    HIPCHECK(hipMemcpyAsync(d->resLHost, d->resL, lb * sizeof(float), hipMemcpyDeviceToHost, d->stream));
+    HIPCHECK(hipMemcpyAsync(d->depthHost, p.nNewDepth, (size_t)p.nN * sizeof(double), hipMemcpyDeviceToHost,
+                            d->stream));
+    HIPCHECK(hipStreamSynchronize(d->stream));
+    *avgNode = d->avgONHost;
+    *avgLink = d->avgOLHost;
+    *curNode = d->resNHost;
+    *curLink = d->resLHost;
+    *depth = d->depthHost;
+    return 0;
+}
+
+int Router::packResults(double f, double uL, double uV, double uQ, const float** nodeVals,
+                        const float** linkVals)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    const Params& p = d->p;
+    size_t nb = (size_t)p.nN * (6 + p.P), lb = (size_t)p.nL * (5 + p.P);
+    std::string m;
+    if (launchPack(d, f, uL, uV, uQ, &m)) { fail(m); return err_; }
     HIPCHECK(hipMemcpyAsync(d->resNHost, d->resN, nb * sizeof(float), hipMemcpyDeviceToHost, d->stream));
     HIPCHECK(hipMemcpyAsync(d->resLHost, d->resL, lb * sizeof(float), hipMemcpyDeviceToHost, d->stream));
     HIPCHECK(hipStreamSynchronize(d->stream));

@@ -103,7 +103,8 @@ int OutFile::open(const std::string& path, Project& prj)  // output.c:121-405
 }
 
 int OutFile::saveResults(Project& prj, double reportDate, const float* nodeVals, const float* linkVals,
-                         const double sys[6])   // output.c:457-505, 636-695
+                         const double sys[6], const float* avgNode, const float* avgLink, const double* depth,
+                         double uL)   // output.c:457-505, 636-695 (averages: 911-955)
 {
     if (!f_) return 0;
     Network& net = prj.net;
@@ -116,19 +117,35 @@ int OutFile::saveResults(Project& prj, double reportDate, const float* nodeVals,
     std::vector<double>& rpt = prj.stats.maxRptDepth;
     if ((int)rpt.size() != nn) rpt.assign(nn, 0.0);
     // node rows (node_getResults node.c:497-528, packed on the device)
-    for (int j = 0; j < nn; j++) {
-        const float* x = nodeVals + (size_t)j * nv;
-        if (net.rptFlag[j]) fwrite(x, 4, nNodeVars_, f_);
-        // stats_updateMaxNodeDepth (stats.c:436-445) with the reported value
-        rpt[j] = (rpt[j] >= (double)x[0]) ? rpt[j] : (double)x[0];
-        sysr[12] += x[2];
-    }
-    // link rows (link_getResults link.c:674-724); system storage adds every
-    // link's volume in link order (output.c:668-671)
-    for (int j = 0; j < nl; j++) {
-        const float* x = linkVals + (size_t)j * lv;
-        if (net.linkRpt[j]) fwrite(x, 4, nLinkVars_, f_);
-        sysr[12] += x[3];
+    if (avgNode) {
+        // averaged rows of the reported objects; the maximum reported depth
+        // takes each node's current depth and the system storage its current
+        // volume (output.c:914-950)
+        for (int j = 0; j < nn; j++)
+            if (net.rptFlag[j]) fwrite(avgNode + (size_t)j * nv, 4, nNodeVars_, f_);
+        for (int j = 0; j < nn; j++) {
+            const double y = depth[j] * uL;
+            rpt[j] = (rpt[j] >= y) ? rpt[j] : y;
+            sysr[12] += nodeVals[(size_t)j * nv + 2];
+        }
+        for (int j = 0; j < nl; j++)
+            if (net.linkRpt[j]) fwrite(avgLink + (size_t)j * lv, 4, nLinkVars_, f_);
+        for (int j = 0; j < nl; j++) sysr[12] += linkVals[(size_t)j * lv + 3];
+    } else {
+        for (int j = 0; j < nn; j++) {
+            const float* x = nodeVals + (size_t)j * nv;
+            if (net.rptFlag[j]) fwrite(x, 4, nNodeVars_, f_);
+            // stats_updateMaxNodeDepth (stats.c:436-445) with the reported value
+            rpt[j] = (rpt[j] >= (double)x[0]) ? rpt[j] : (double)x[0];
+            sysr[12] += x[2];
+        }
+        // link rows (link_getResults link.c:674-724); system storage adds every
+        // link's volume in link order (output.c:668-671)
+        for (int j = 0; j < nl; j++) {
+            const float* x = linkVals + (size_t)j * lv;
+            if (net.linkRpt[j]) fwrite(x, 4, nLinkVars_, f_);
+            sysr[12] += x[3];
+        }
     }
     sysr[10] = (float)(sys[0] * uQ);
     sysr[11] = (float)(sys[1] * uQ);

@@ -19,8 +19,13 @@ public:
     // packResults: nodes 6 + P floats, links 5 + P floats, all objects);
     // sysFlows = {flooding, outflow, dwInflow, gwInflow, iiInflow, exInflow}
     // rates of the bracketing step (StepFlowTotals)
+    // REPORT AVERAGES (output_saveAvgResults, output.c:911-955): the rows come
+    // from avgNode / avgLink, while nodeVals / linkVals hold the current state
+    // (f = 1) for the system storage and depth (ft, times uL) the reported
+    // maximum depth
     int saveResults(Project& prj, double reportDate, const float* nodeVals, const float* linkVals,
-                    const double sysFlows[6]);
+                    const double sysFlows[6], const float* avgNode = nullptr, const float* avgLink = nullptr,
+                    const double* depth = nullptr, double uL = 1.0);
     int end(int errorCode);
     void close();
     int periods() const { return nPeriods_; }

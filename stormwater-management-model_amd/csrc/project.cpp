@@ -2237,8 +2237,6 @@ int Project::readReport(std::vector<char*>& tok)  // report.c:report_readOptions
         case 8: rpt.averages = m; break;
         default: break;
         }
-        if (rpt.averages)
-            return setError(200, "ERROR 200: REPORT AVERAGES is not supported by the MI355X engine yet");
         return 0;
     }
     int flag;

@@ -77,6 +77,14 @@ public:
     // host copies valid until the next call.  Synchronises.
     int packResults(double f, double uL, double uV, double uQ, const float** nodeVals,
                     const float** linkVals);
+    // REPORT AVERAGES (output.c:857-955).  avgUpdate: add the current results
+    // (packResults with f = 1) to the reporting period's float32 sums
+    // (output_updateAvgResults).  avgTake: the period's averages, the current
+    // results and the nodes' current depths (ft) on pinned host copies, then
+    // the sums reset (output_saveAvgResults, output_initAvgResults).
+    int avgUpdate(double uL, double uV, double uQ);
+    int avgTake(double uL, double uV, double uQ, const float** avgNode, const float** avgLink,
+                const float** curNode, const float** curLink, const double** depth);
     // Copy the run statistics accumulators into prj.stats; synchronises.
     int downloadStats(Project& prj);
     // Upload the host mirror's dynamic state (after swmm_setValue edits).

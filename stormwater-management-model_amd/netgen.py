@@ -417,7 +417,8 @@ def write_example(path: str, *, route_step: float = 5.0,
                   culverts: bool = False, tidal: bool = False, roadway: bool = False,
                   dividers: bool = False, streets: bool = False, extfile: bool = False,
                   options: dict | None = None, ponding: bool = False,
-                  branches: bool = False, dummy: bool = False, evap: str = "") -> None:
+                  branches: bool = False, dummy: bool = False, evap: str = "",
+                  averages: bool = False) -> None:
     """Write the authored Example network (see module docstring).  `files`
     is the body of an optional [FILES] section (e.g. "SAVE HOTSTART x.hsf");
     `storage` turns six junctions into storage units (_STORAGE); `options`
@@ -433,7 +434,10 @@ def write_example(path: str, *, route_step: float = 5.0,
     1320-1330);
     `evap` ("MONTHLY" or "TIMESERIES") replaces the evaporation data with
     monthly or time-series rates plus monthly [ADJUSTMENTS], on a run that
-    crosses from January into February (climate.c:598-725, 876-911)."""
+    crosses from January into February (climate.c:598-725, 876-911);
+    `averages` sets REPORT AVERAGES YES: the binary results hold each
+    reporting period's average of the routing steps' results
+    (output.c:857-955, swmm5.c:579-613)."""
     if pollutants:
         pollut = ("TSS MG/L 0 0 0 0.5 NO * 0 20 0\n"
                   "BOD MG/L 0 0 0 0 NO * 0 10 0\n")
@@ -587,6 +591,9 @@ def write_example(path: str, *, route_step: float = 5.0,
         txt = "\n".join(lines)
     if files:
         txt += "\n[FILES]\n" + files.rstrip("\n") + "\n"
+    if averages:
+        txt = txt.replace("[REPORT]\nINPUT NO\n", "[REPORT]\nINPUT NO\nAVERAGES YES\n", 1)
+        assert "AVERAGES YES" in txt
     if extfile:
         # HYD1 read from an external time series file (table.c:833-895):
         # undated, dated and commented lines

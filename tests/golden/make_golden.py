@@ -118,6 +118,10 @@ CASES = {
                                                         evap="MONTHLY"), 1),
     "example_evap_series": (netgen.write_example, dict(end_time="01:00:00", route_step=10.0,
                                                        variable_step=0.75, storage=True, evap="TIMESERIES"), 1),
+    # REPORT AVERAGES (output.c:857-955): each period's average of the routing
+    # steps' results, pumps and regulators keeping their current setting
+    "example_avg": (netgen.write_example, dict(end_time="01:30:00", route_step=10.0, variable_step=0.75,
+                                               regulators=True, pollutants=True, averages=True), 1),
     "example_dummy": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, dummy=True,
                                                  pollutants=True), 1),
     "example_dummy_var": (netgen.write_example, dict(end_time="02:00:00", route_step=10.0, variable_step=0.75,
