@@ -70,6 +70,7 @@ constexpr int kNumPartials = 10;
 __host__ __device__ inline bool partialIsMin(int q) { return q == 5 || q == 6; }
 constexpr int kTimeLevels = 6;     // TIMELEVELS (objects.h:941)
 constexpr int kQualBatch = 4;      // pollutants whose node mass inflow k_qual_node sums in one link pass
+constexpr int kQGather = 4;        // CSR entries k_qual_node loads together
 constexpr int kDtRing = 4;          // host-mapped per-step dt ring (k_finalize -> host)
 constexpr int kLinkWavesDefault = 3;   // measured best on MI355X
 constexpr double kTailIters = 2.5;     // auto mode: k_tail while steps average at most this many iterations
@@ -1960,15 +1961,31 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
         for (int p0 = 0; p0 < p.P; p0 += kQualBatch) {
         const int np = (p.P - p0 < kQualBatch) ? p.P - p0 : kQualBatch;
         for (int b = 0; b < np; b++) wq[b] = p.qualIn[(size_t)(p0 + b) * p.nN + i];
-        for (int e = e0; e < e1; e++) {
-            int ent = p.qcsr[e];
-            int l = ent & 0x7FFFFFFF;
-            bool isN2 = ent < 0;
-            double ql = p.lNewFlow[l];
-            bool down = isN2 ? !(ql < 0.0) : (ql < 0.0);
-            if (down) {
-                const double aq = fabs(ql);
-                for (int b = 0; b < np; b++) wq[b] += aq * lOld[(size_t)(p0 + b) * p.nLs + l];
+        // kQGather CSR entries at a time: their words, then their flows, then
+        // the downstream-flowing links' concentrations load together before
+        // the in-order sums (one entry at a time is three dependent loads each)
+        for (int eb = e0; eb < e1; eb += kQGather) {
+            int ent[kQGather];
+            double ql[kQGather], lo[kQGather][kQualBatch];
+            bool down[kQGather];
+#pragma unroll
+            for (int t = 0; t < kQGather; t++) ent[t] = (eb + t < e1) ? p.qcsr[eb + t] : 0;
+#pragma unroll
+            for (int t = 0; t < kQGather; t++) ql[t] = (eb + t < e1) ? p.lNewFlow[ent[t] & 0x7FFFFFFF] : 0.0;
+#pragma unroll
+            for (int t = 0; t < kQGather; t++) {
+                down[t] = (eb + t < e1) && ((ent[t] < 0) ? !(ql[t] < 0.0) : (ql[t] < 0.0));
+#pragma unroll
+                for (int b = 0; b < kQualBatch; b++)
+                    lo[t][b] = (down[t] && b < np) ? lOld[(size_t)(p0 + b) * p.nLs + (ent[t] & 0x7FFFFFFF)] : 0.0;
+            }
+#pragma unroll
+            for (int t = 0; t < kQGather; t++) {
+                if (!down[t]) continue;
+                const double aq = fabs(ql[t]);
+#pragma unroll
+                for (int b = 0; b < kQualBatch; b++)
+                    if (b < np) wq[b] += aq * lo[t][b];
             }
         }
         for (int b = 0; b < np; b++) {
