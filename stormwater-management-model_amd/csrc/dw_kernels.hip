@@ -2006,40 +2006,69 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
             nNew[ni] = c;
             cn[b] = c;
         }
-        // findLinkQual (qualrout.c:253-353, DW) of the links this node feeds
-        for (int e = e0; e < e1; e++) {
-            int ent = p.qcsr[e];
-            int l = ent & 0x7FFFFFFF;
-            if (l >= p.nL) continue;                // a ghost link: its owner updates it
-            bool isN2 = ent < 0;
-            double ql = p.lNewFlow[l];
-            bool up = isN2 ? (ql < 0.0) : !(ql < 0.0);
-            if (!up) continue;
-            uint32_t f = p.lflags[l];
-            if (f & LF_NC) {                        // non-conduit: its upstream node's quality (qualrout.c:283-291)
-                for (int b = 0; b < np; b++) lNew[(size_t)(p0 + b) * p.nLs + l] = cn[b];
-                continue;
+        // findLinkQual (qualrout.c:253-353, DW) of the links this node feeds,
+        // kQGather CSR entries at a time (their state loads together)
+        for (int eb = e0; eb < e1; eb += kQGather) {
+            int ent[kQGather];
+            double ql[kQGather];
+#pragma unroll
+            for (int t = 0; t < kQGather; t++) ent[t] = (eb + t < e1) ? p.qcsr[eb + t] : 0;
+#pragma unroll
+            for (int t = 0; t < kQGather; t++) ql[t] = (eb + t < e1) ? p.lNewFlow[ent[t] & 0x7FFFFFFF] : 0.0;
+            bool up[kQGather];
+            uint32_t fl[kQGather];
+            double q1v[kQGather], sl[kQGather], el[kQGather], v1v[kQGather], v2v[kQGather], dl[kQGather];
+            double lo[kQGather][kQualBatch];
+#pragma unroll
+            for (int t = 0; t < kQGather; t++) {
+                const int l = ent[t] & 0x7FFFFFFF;
+                // a ghost link (l >= nL): its owner updates it
+                up[t] = (eb + t < e1) && l < p.nL && ((ent[t] < 0) ? (ql[t] < 0.0) : !(ql[t] < 0.0));
+                fl[t] = up[t] ? p.lflags[l] : 0u;
+                q1v[t] = up[t] ? p.q1[l] : 0.0;
+                sl[t] = up[t] ? p.seepLoss[l] : 0.0;
+                el[t] = up[t] ? p.evapLoss[l] : 0.0;
+                v1v[t] = up[t] ? p.lOldVolume[l] : 0.0;
+                v2v[t] = up[t] ? p.lNewVolume[l] : 0.0;
+                dl[t] = up[t] ? p.lNewDepth[l] : 0.0;
+#pragma unroll
+                for (int b = 0; b < kQualBatch; b++)
+                    lo[t][b] = (up[t] && b < np) ? lOld[(size_t)(p0 + b) * p.nLs + l] : 0.0;
             }
-            double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
-            double lq = fabs(p.q1[l]) * barrels;
-            double qSeep = p.seepLoss[l] * barrels;
-            double vEvap = p.evapLoss[l] * barrels * dt;
-            double v1 = p.lOldVolume[l], v2 = p.lNewVolume[l];
-            double vLosses = qSeep * dt + vEvap;
-            double fe = 1.0;
-            if (vEvap > 0.0 && v1 > 0.0353147) fe += vEvap / v1;
-            lq = lq + (v2 + vLosses - v1) / dt;
-            lq = gmax(lq, 0.0);
-            bool dry = (v2 < 0.0353147 || p.lNewDepth[l] <= 0.003281);
-            for (int b = 0; b < np; b++) {
-                const int pp = p0 + b;
-                size_t li = (size_t)pp * p.nLs + l;
-                double c1 = lOld[li] * fe;
-                double c2 = reactedQual(p.kDecay[pp], c1, dt);
-                double wIn = cn[b] * lq;
-                c2 = mixedQual(c2, v1, wIn, lq, dt);
-                if (dry) c2 = 0.0;
-                lNew[li] = c2;
+#pragma unroll
+            for (int t = 0; t < kQGather; t++) {
+                if (!up[t]) continue;
+                const int l = ent[t] & 0x7FFFFFFF;
+                const uint32_t f = fl[t];
+                if (f & LF_NC) {                    // non-conduit: its upstream node's quality (qualrout.c:283-291)
+#pragma unroll
+                    for (int b = 0; b < kQualBatch; b++)
+                        if (b < np) lNew[(size_t)(p0 + b) * p.nLs + l] = cn[b];
+                    continue;
+                }
+                double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
+                double lq = fabs(q1v[t]) * barrels;
+                double qSeep = sl[t] * barrels;
+                double vEvap = el[t] * barrels * dt;
+                double v1 = v1v[t], v2 = v2v[t];
+                double vLosses = qSeep * dt + vEvap;
+                double fe = 1.0;
+                if (vEvap > 0.0 && v1 > 0.0353147) fe += vEvap / v1;
+                lq = lq + (v2 + vLosses - v1) / dt;
+                lq = gmax(lq, 0.0);
+                bool dry = (v2 < 0.0353147 || dl[t] <= 0.003281);
+#pragma unroll
+                for (int b = 0; b < kQualBatch; b++) {
+                    if (b >= np) continue;
+                    const int pp = p0 + b;
+                    size_t li = (size_t)pp * p.nLs + l;
+                    double c1 = lo[t][b] * fe;
+                    double c2 = reactedQual(p.kDecay[pp], c1, dt);
+                    double wIn = cn[b] * lq;
+                    c2 = mixedQual(c2, v1, wIn, lq, dt);
+                    if (dry) c2 = 0.0;
+                    lNew[li] = c2;
+                }
             }
         }
         }
