@@ -783,10 +783,20 @@ __device__ __forceinline__ void finalizeFrozen(const Params& p, int m, int tid, 
 __device__ __forceinline__ int stepIterations(const Params& p, bool* converged)
 {
     if (p.maxTrials <= 1) { *converged = false; return p.maxTrials < 1 ? 0 : 1; }
-    int steps = 2;
-    while (steps < p.maxTrials && p.unconv[steps - 1]) steps++;
-    *converged = (p.unconv[steps - 1] == 0);
-    return steps;
+    // the same scan (while (steps < MaxTrials && unconv[steps - 1]) steps++)
+    // over flags loaded eight at a time: the first iteration m >= 1 whose
+    // nodes all converged ends the step after m + 1 iterations.  (One flag
+    // at a time was a chain of dependent loads at the start of the kernels.)
+    for (int base = 1; base < p.maxTrials; base += 8) {
+        int f[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) f[q] = (base + q < p.maxTrials) ? p.unconv[base + q] : 1;
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            if (f[q] == 0) { *converged = true; return base + q + 1; }
+    }
+    *converged = false;
+    return p.maxTrials;
 }
 
 
@@ -2401,6 +2411,10 @@ __global__ void k_finalize(Params p)
         for (int w = t; w < nw; w += kBlock) cw[w] = g[w];
     }
     StepCtl* c = (StepCtl*)cw;
+    // Picard step count / convergence (dynwave.c:242-257): its flags load
+    // alongside the partials
+    bool converged = false;
+    const int steps = (t == 0 && kPhase != 1) ? stepIterations(p, &converged) : 0;
     if (kPhase != 2) {
         double acc[kNumPartials];
         for (int q = 0; q < kNumPartials; q++) acc[q] = partialIsMin(q) || q == 8 || q == 9 ? 1.0e300 : 0.0;
@@ -2427,15 +2441,6 @@ __global__ void k_finalize(Params p)
     if (t == 0 && kPhase != 1) {
     double tot[kNumPartials];
     for (int q = 0; q < kNumPartials; q++) tot[q] = c->stepRed[q];
-    // Picard step count / convergence (dynwave.c:242-257)
-    int steps;
-    bool converged;
-    if (p.maxTrials <= 1) { steps = p.maxTrials < 1 ? 0 : 1; converged = false; }
-    else {
-        steps = 2;
-        while (steps < p.maxTrials && p.unconv[steps - 1]) steps++;
-        converged = (p.unconv[steps - 1] == 0);
-    }
     c->lastSteps = steps;
     c->totalSteps += 1;
     if (p.P > 0) c->qualPar ^= 1;                      // this step's concentrations become the latest
