@@ -2506,7 +2506,9 @@ __global__ void k_finalize(Params p)
     // a k_tail grid barrier that timed out (never expected: its workgroups
     // are co-resident by construction) is reported to the host at once
     p.hostDt[2 * kDtRing] = (double)c->tailErr;
-    __threadfence_system();
+    // (no system-scope fence: the host reads the ring only after
+    // hipEventSynchronize on an event recorded behind this step, whose
+    // completion makes the kernel's host-memory writes visible)
     }
     if (c->tailErr)                                // leave no junction frozen in a failed step
         for (int i = t; i < p.nN; i += kBlock) p.frz[i] = 0;
