@@ -12,7 +12,7 @@ Inputs are resident in HBM before the timed region (swmm_start uploads them).
 Workloads (--config; BASELINE.json configs):
   1m_surcharge (default, configs[2]) 707 x 707 grid = 998,285 conduits /
         499,850 nodes, DYNWAVE, VARIABLE_STEP 0.75, ROUTING_STEP 5 s, 1.0-ft
-        pipes, DWF 0.25 cfs per junction.  The run is first spun up for
+        pipes, DWF 0.12 cfs per junction.  The run is first spun up for
         --spinup steps (untimed, outside warmup) so that 2-20 % of the
         junctions are surcharged in the timed window (fraction
         reported in config.surcharged_pct).
@@ -231,11 +231,13 @@ def main():
         s.set_partition(rank, world, bytes(idt.numpy().tobytes()))
     elif args.rccl_1rank:
         s.set_partition(0, 1, s.nccl_unique_id())
-        if args.exchange == "host":
-            def xchg(arr, op):
-                t = torch.from_numpy(arr)
-                dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MIN)
-            s.set_exchange(xchg)
+    if world > 1 and args.exchange == "host":
+        # host transport (gloo through torch.distributed): the rehearsal of
+        # the multi-rank path with several ranks on one GPU
+        def xchg(arr, op):
+            t = torch.from_numpy(arr)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MIN)
+        s.set_exchange(xchg)
     tmpd = "/tmp/swmm_bench"
     err = s.open(inp, os.path.join(tmpd, "r%d.rpt" % rank), os.path.join(tmpd, "r%d.out" % rank))
     if err:
@@ -457,7 +459,8 @@ def main():
                        "surcharged_pct": round(surcharged, 2),
                        # step graphs the timed steps launched (Router::step's per-step choice)
                        "step_graphs": {g: c1["steps_" + g] - c0["steps_" + g]
-                                       for g in ("unrolled", "tail", "sparse", "list", "fused")},
+                                       for g in ("unrolled", "tail", "sparse", "list", "fused", "compact")},
+                       "compact_grown_nodes": c1["compact_grown"] - c0["compact_grown"],
                        "sim_time_at_end_s": round(t_days * 86400.0, 1),
                        "parallelism": ("link-partitioned x%d (row strips); per Picard iteration "
                                        "%s of the strip neighbours' ghost-link values and an "

@@ -44,7 +44,9 @@ int    DLLEXPORT swmmx_runSteps(int n, double *elapsedTime);
  * launched with the unrolled, k_tail, k_sparse and list step graphs, [15] 1
  * when the outfall depths of iterations >= 2 are found in the next link
  * launch (deferred outfall prologue), [16] steps launched with the fused
- * step graph (one k_fused launch per iteration >= 2).
+ * step graph (one k_fused launch per iteration >= 2), [17] steps launched
+ * with the compact step graph (iterations >= 2 over compact copies of the
+ * live sub-network), [18] nodes its walks added to the compact sets (growth).
  * Synchronises with the device. */
 int    DLLEXPORT swmmx_getCounters(long long *out, int n);
 
@@ -60,15 +62,15 @@ int    DLLEXPORT swmmx_getCounters(long long *out, int n);
  *      conduits skipped), 5 node update of iteration 1, 6 node updates of the
  *      executed iterations >= 2.
  * Returns the number of classes written. */
+int    DLLEXPORT swmmx_setTiming(int mode);
+int    DLLEXPORT swmmx_getKernelTimes(double *out, int n);
+
 /* Host-side evaporation replay (after swmmx_startHost only: the project
  * cannot step afterwards): the evaporation rate (ft/s) climate_setState
  * gives routing steps starting at elapsedMsec[0..n-1] ms after the start, in
  * that order -- constant / monthly / time-series / climate-file / Hargreaves
  * rates with the monthly adjustments.  Returns n, or -(error code). */
 long   DLLEXPORT swmmx_evapReplay(const double *elapsedMsec, long n, double *rates);
-
-int    DLLEXPORT swmmx_setTiming(int mode);
-int    DLLEXPORT swmmx_getKernelTimes(double *out, int n);
 
 /* Algorithmic bytes per launch of each kernel class (the byte model of
  * DESIGN.md), same class order as above: the average over the launches timed
@@ -88,7 +90,8 @@ int    DLLEXPORT swmmx_getIterationStats(double *out, int n);
  * 1 node update of iteration 0.  The launches are of separate instantiations
  * (k_link<..., probe = true>, k_node<..., probe = true>) so that a profiler's
  * per-kernel statistics keep them apart from the routing steps'.  Measurement
- * only: it advances the state, so call it after the run being measured. */
+ * only: it advances the state, so call it after the run being measured
+ * (every later swmm_step / swmm_stride returns error 500). */
 int    DLLEXPORT swmmx_timeKernel(int which, int reps, double *avgUs);
 
 /* Name of the compute backend ("hip:gfx950:<device name>" or "none"). */
@@ -107,7 +110,9 @@ int    DLLEXPORT swmmx_setDevice(int ordinal);
  * the run is bitwise equal to one GPU.  Call before swmm_start, on every rank:
  *   rank 0: swmmx_ncclUniqueId(id, 128) and broadcast the id to the others;
  *   all:    swmmx_setPartition(rank, nranks, id, 128).
- * The binary results file and hot start saving are single-GPU only for now. */
+ * The binary results file and a saved hot start file are gathered from the
+ * owning ranks and written by rank 0 (byte-identical to one GPU's); an error
+ * one rank meets there is returned by every rank from the same call. */
 int    DLLEXPORT swmmx_ncclUniqueId(void *out, int bytes);     /* returns bytes written */
 int    DLLEXPORT swmmx_setPartition(int rank, int nranks, const void *ncclId, int idBytes);
 

@@ -37,6 +37,7 @@ struct Engine {
     bool isOpen = false, isStarted = false, hostOnly = false, saveFlag = true;
     bool mirrorValid = true;         // host mirror equals device state
     int errorCode = 0;
+    bool stateSpent = false;        // swmmx_timeKernel replayed kernels on the live state
     std::string errorMsg;
     double newRoutingTime = 0.0, oldRoutingTime = 0.0, reportTime = 0.0;
     double routingDuration = 0.0, elapsedTime = 0.0;
@@ -71,6 +72,23 @@ int syncMirror()
     if (G->router->download(*G->prj)) return setErr(G->router->lastError(), G->router->lastErrorMsg());
     G->mirrorValid = true;
     return 0;
+}
+
+// Several GPUs: an error one rank alone met (rank 0 writes the results and
+// hot start files) reaches every rank at the same point -- an all-reduce of
+// the error codes (min of their negatives) -- so that no rank goes on into a
+// collective the failed rank never reaches.  Called where such errors arise:
+// the end of swmm_start, around each reporting period's gather, and in
+// swmm_end before and after the hot start gather.  (A device failure inside a
+// step is not covered: that would need an exchange every step.)
+static int syncError()
+{
+    if (!G || !G->router || !G->router->ok() || !G->router->partition().active()) return G ? G->errorCode : 501;
+    double e = -(double)G->errorCode;
+    if (G->router->allreduceHost(&e, 1, 1)) return setErr(G->router->lastError(), G->router->lastErrorMsg());
+    if (e < 0.0 && !G->errorCode)
+        setErr((int)-e, "ERROR " + std::to_string((int)-e) + ": reported by another rank.");
+    return G->errorCode;
 }
 
 int defaultDevice()
@@ -153,7 +171,13 @@ int DLLEXPORT swmm_start(int saveFlag)
     // (several GPUs: the results are gathered from the ranks that own them and
     // written by rank 0 alone, gatherResults; the other ranks write no file)
     const bool writer = !(gPart.active() && gPart.rank != 0);
-    if (writer && G->out.open(G->outPath, prj)) return setErr(307, "ERROR 307: cannot open binary results file.");
+    // (several GPUs: a failure to open the file is kept until every rank has
+    // started its router, whose communicator the error exchange needs)
+    bool openFailed = false;
+    if (writer && G->out.open(G->outPath, prj)) {
+        if (!gPart.active()) return setErr(307, "ERROR 307: cannot open binary results file.");
+        openFailed = true;
+    }
     if (prj.initState()) return setErr(prj.errorCode, prj.errorMsg);
     G->apiExtInflow.assign(prj.net.nNodes(), 0.0);
     G->constantInflow = prj.inflowsAreConstant();
@@ -170,6 +194,8 @@ int DLLEXPORT swmm_start(int saveFlag)
     int dev = (gDevice >= 0) ? gDevice : defaultDevice();
     if (G->router->init(prj, dev, gPart.active() ? &gPart : nullptr))
         return setErr(G->router->lastError(), G->router->lastErrorMsg());
+    if (openFailed) setErr(307, "ERROR 307: cannot open binary results file.");
+    if (gPart.active() && syncError()) return G->errorCode;
     G->isStarted = true;
     G->mirrorValid = true;
     return G->errorCode;
@@ -309,6 +335,7 @@ static void saveOutput(bool averages)
     }
     GatheredResults g;
     if (multi) {
+        if (syncError()) return;                    // every rank gathers, or none
         if (gatherResults(nv, lv, an, al, depth, g)) return;
         nv = g.nv.data();
         lv = g.lv.data();
@@ -320,6 +347,7 @@ static void saveOutput(bool averages)
     }
     int e = G->out.saveResults(prj, reportDate, nv, lv, sys, an, al, depth, prj.ucfLength());
     if (e) setErr(e, "ERROR 309: cannot write to binary results file.");
+    if (multi) syncError();                         // rank 0's write error stops every rank
 }
 
 static void updateAvg()      // output_updateAvgResults (output.c:857-907)
@@ -355,6 +383,9 @@ int DLLEXPORT swmm_step(double* elapsedTime)
     if (G->errorCode) return G->errorCode;
     if (!G->isOpen) return (G->errorCode = 501);
     if (!G->isStarted || G->hostOnly) return (G->errorCode = 502);
+    if (G->stateSpent)
+        return setErr(500, "ERROR 500: the state was advanced by swmmx_timeKernel (measurement only); "
+                           "the run cannot continue.");
     if (G->newRoutingTime < G->routingDuration) {
         if (execRouting()) return G->errorCode;
     }
@@ -517,14 +548,16 @@ int DLLEXPORT swmm_end(void)   // swmm5.c:618-660
             G->router->flowTotals(G->flowTot);
             G->router->allreduceHost(G->flowTot, 6, 0);   // per-rank totals (multi-GPU)
             G->flowError = computeFlowError();
-            G->out.end(G->errorCode);
+            G->out.end(G->errorCode);                   // (output_end: its write errors are not reported)
             if (!G->errorCode) writeReportSummary();
             // hotstart_close (swmm5.c:647): the final state as a hot start
             // file (several GPUs: gathered from the owners, written by rank 0)
             const Partition& part = G->router->partition();
+            if (part.active()) syncError();
             if (!G->errorCode && !G->prj->hotstartSave.empty() && part.active()) gatherMirror();
             if (!G->errorCode && (!part.active() || part.rank == 0) && G->prj->saveHotstart())
                 setErr(G->prj->errorCode, G->prj->errorMsg);
+            if (part.active()) syncError();
         }
         G->isStarted = false;
     }
@@ -1089,8 +1122,8 @@ int DLLEXPORT swmmx_exportState(const char* path)
 int DLLEXPORT swmmx_getCounters(long long* out, int n)
 {
     if (!G || !out) return 0;
-    long long v[17] = {G->totalStepCount, 0, 0, 0, G->prj->net.nLinks(), G->prj->net.nNodes(), 0, 0, 0, 0,
-                       0, 0, 0, 0, 0, 0, 0};
+    long long v[19] = {G->totalStepCount, 0, 0, 0, G->prj->net.nLinks(), G->prj->net.nNodes(), 0, 0, 0, 0,
+                       0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (G->router && G->router->ok()) {
         int last = 0;
         G->router->counters(&v[1], &v[2], &last);
@@ -1103,7 +1136,7 @@ int DLLEXPORT swmmx_getCounters(long long* out, int n)
         v[9] = (long long)git;
         G->router->graphStats(&v[10]);
     }
-    int m = n < 17 ? n : 17;
+    int m = n < 19 ? n : 19;
     for (int i = 0; i < m; i++) out[i] = v[i];
     return m;
 }
@@ -1174,6 +1207,9 @@ int DLLEXPORT swmmx_timeKernel(int which, int reps, double* avgUs)
 {
     if (!G || !G->router || !G->router->ok() || !avgUs) return 502;
     G->mirrorValid = false;
+    // the replays advance the live state (the first passes rotate it; storage
+    // exfiltration moves its Green-Ampt state): no routing step may follow
+    G->stateSpent = true;
     return G->router->timeKernel(which, reps, avgUs);
 }
 

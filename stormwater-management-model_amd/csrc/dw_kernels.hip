@@ -342,6 +342,24 @@ struct Params {
     const double* ofQcs;          // [nOutLinks][26] their critical flows at the enumeration's
                                   // depths i yFull / 25 (static geometry: k_outfall_qcs at init)
     StepCtl* ctl;
+    // ---- the compact graph (GM_COMPACT, k_cgather / k_cwalk / k_cnode) ----
+    // In the Params those kernels hand to conduitFlow / nodeItem (compactView)
+    // the node and link arrays point at the compact copies (CView), and wt at
+    // the global arrays, which every store there updates as well
+    // (write-through: the global arrays stay the canonical state at all times)
+    struct WThrough {
+        double *lNewFlow, *lNewDepth, *lNewVolume, *a1, *q1, *dqdh, *froude, *sa1, *sa2, *evapLoss, *seepLoss;
+        int* lstate;
+        double *nNewDepth, *yRaw, *oldSurfArea, *inflow, *outflow, *nSurf, *nDqdh, *nNewVolume, *overflow;
+        int* conv;
+        unsigned char* frz;
+    } wt;
+    // k_node(1) of a compact step: the live nodes' membership (cmStamp[g] =
+    // iterStamp(1), cmCid[g] = their vlist position = compact id); the outfall
+    // prologue then also writes an outfall's compact depth (cOutDepth[cmCid[o]])
+    unsigned* cmStamp;
+    int* cmCid;
+    double* cOutDepth;
 };
 
 // ===========================================================================
@@ -586,11 +604,28 @@ __device__ __forceinline__ int flowClassOf(const Params& p, int j, const Geom& x
     return fc;
 }
 
+// a store of conduit j's (node i's) state; kWT (the compact graph): p's arrays
+// are the compact copies and the same value also goes to the global array
+// p.wt.<arr> at the global index jg (ig)
+#define SWX_LST(arr, v)                                  \
+    do {                                                 \
+        const auto v_ = (v);                             \
+        p.arr[j] = v_;                                   \
+        if (kWT) p.wt.arr[jg] = v_;                      \
+    } while (0)
+#define SWX_NST(arr, v)                                  \
+    do {                                                 \
+        const auto v_ = (v);                             \
+        p.arr[i] = v_;                                   \
+        if (kWT) p.wt.arr[ig] = v_;                      \
+    } while (0)
+
 // dwflow.c:57-293 -- one conduit, one Picard iteration.
-template <bool kFirst, bool kCold, bool kFast = false>
+template <bool kFirst, bool kCold, bool kFast = false, bool kWT = false>
 __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, int2 nn, int steps,
-                                            double dt, const double* ct, double yn1, double yn2)
+                                            double dt, const double* ct, double yn1, double yn2, int jg = 0)
 {
+    static_assert(!(kWT && kFirst), "write-through only in iterations k >= 2");
     const double omega = 0.5;
     (void)nn;                     // end-node depths arrive as yn1 / yn2
     const double off1 = kCold ? p.off1[j] : 0.0;     // hot links: both offsets are 0
@@ -699,8 +734,8 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         y1 = d1;
         y2 = d2;
     }
-    p.sa1[j] = sa1;
-    p.sa2[j] = sa2;
+    SWX_LST(sa1, sa1);
+    SWX_LST(sa2, sa2);
 
     double wSlot = slotWidth<kFast>(p, x, y1);
     double a1 = areaAt<kCold>(x, y1, wSlot, ct);
@@ -716,26 +751,26 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
 
     if (fc == F_DRY || fc == F_UP_DRY || fc == F_DN_DRY || isClosed || aMid <= 0.0001) {
         double a1n = 0.5 * (a1 + a2);
-        p.a1[j] = a1n;
-        p.q1[j] = 0.0;
-        p.dqdh[j] = 32.2 * dt * aMid / length * barrels;
-        p.froude[j] = 0.0;
-        p.lNewDepth[j] = gmin(yMid, x.yFull);
-        p.lNewVolume[j] = a1n * len0 * barrels;
-        p.lNewFlow[j] = 0.0;
+        SWX_LST(a1, a1n);
+        SWX_LST(q1, 0.0);
+        SWX_LST(dqdh, 32.2 * dt * aMid / length * barrels);
+        SWX_LST(froude, 0.0);
+        SWX_LST(lNewDepth, gmin(yMid, x.yFull));
+        SWX_LST(lNewVolume, a1n * len0 * barrels);
+        SWX_LST(lNewFlow, 0.0);
         if (f & LF_SEEP) {            // always 0 without LF_SEEP: not rewritten
-            p.evapLoss[j] = 0.0;
-            p.seepLoss[j] = 0.0;
+            SWX_LST(evapLoss, 0.0);
+            SWX_LST(seepLoss, 0.0);
         }
         int old = p.lstate[j];
-        p.lstate[j] = (old & ~0xF) | fc;      // fullState / normalFlow / inletControl untouched (dwflow.c:165-180)
+        SWX_LST(lstate, (old & ~0xF) | fc);   // fullState / normalFlow / inletControl untouched (dwflow.c:165-180)
         return;
     }
 
     double v = qLast / aMid;
     if (fabs(v) > 50.) v = 50. * gsgn(qLast);
     double froude = linkFroude<kCold>(x, v, yMid, ct);
-    p.froude[j] = froude;
+    SWX_LST(froude, froude);
     if (fc == F_SUBCRIT && froude > 1.0) fc = F_SUPCRIT;
 
     double sigma;
@@ -790,7 +825,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
 
     double denom = 1.0 + dq1 + dq5;
     double q = (qOld - dq2 + dq3 + dq4 + dq6) / denom;
-    p.dqdh[j] = 1.0 / denom * 32.2 * dt * aWtd / length * barrels;
+    double dqdhV = 1.0 / denom * 32.2 * dt * aWtd / length * barrels;
 
     int normalFlow = 0, inletCtl = 0;
     const int culvert = kCold ? (int)((f >> LF_CULVERT_SHIFT) & 0x3F) : 0;
@@ -798,7 +833,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         if (kCold && culvert > 0 && !isFull) {                  // dwflow.c:250-252
             double dq = 0.0;
             q = culvertInflow(x, culvert, p.slope[j], q, h1 - z1, &dq, &inletCtl, ct);
-            if (inletCtl) p.dqdh[j] = dq;
+            if (inletCtl) dqdhV = dq;
         } else
         if (p.normalFlowLtd != NFL_NEITHER && y1 < x.yFull && (fc == F_SUBCRIT || fc == F_SUPCRIT)) {
             // checkNormalFlow dwflow.c:637-686
@@ -846,21 +881,22 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     if (q > 0.0001 && yn1 <= 0.0001) q = 0.0001;
     if (q < -0.0001 && yn2 <= 0.0001) q = -0.0001;
 
-    p.a1[j] = aMid;
-    p.q1[j] = q;
-    p.lNewDepth[j] = gmin(yMid, x.yFull);
+    SWX_LST(dqdh, dqdhV);
+    SWX_LST(a1, aMid);
+    SWX_LST(q1, q);
+    SWX_LST(lNewDepth, gmin(yMid, x.yFull));
     double aAvg = (a1 + a2) / 2.0;
     int fs = 0;
     if (a1 >= x.aFull) fs = (a2 >= x.aFull) ? FS_ALL_FULL : FS_UP_FULL;
     else if (a2 >= x.aFull) fs = FS_DN_FULL;
-    p.lNewVolume[j] = aAvg * len0 * barrels;
-    p.lNewFlow[j] = q * barrels;
+    SWX_LST(lNewVolume, aAvg * len0 * barrels);
+    SWX_LST(lNewFlow, q * barrels);
     if (f & LF_SEEP) {
-        p.evapLoss[j] = evapRate;
-        p.seepLoss[j] = seepRate;
+        SWX_LST(evapLoss, evapRate);
+        SWX_LST(seepLoss, seepRate);
     }
     int old = p.lstate[j];
-    p.lstate[j] = (old & (1 << 9)) | fc | (fs << 4) | (normalFlow << 8) | (inletCtl << 10);
+    SWX_LST(lstate, (old & (1 << 9)) | fc | (fs << 4) | (normalFlow << 8) | (inletCtl << 10));
 }
 
 // ===========================================================================
@@ -949,7 +985,10 @@ __device__ __forceinline__ void probeMark(const Params& p, int k, int slot, unsi
 // wave.  (Per-chunk segments without atomics were measured slower on the
 // surcharged 1M grid: its unconverged nodes are clustered, so the adds are
 // few, and the walk over segments could not pack them as tightly.)
-__device__ __forceinline__ void waveAppend(bool me, int i, int2 row, int* count, int* list, int2* rows)
+// mStamp / mCid (the compact graph's live list after iteration 1): i's
+// membership stamp and its list position, its compact id
+__device__ __forceinline__ void waveAppend(bool me, int i, int2 row, int* count, int* list, int2* rows,
+                                           unsigned* mStamp = nullptr, int* mCid = nullptr, unsigned mVal = 0)
 {
     unsigned long long m = __ballot(me);
     if (m) {
@@ -960,6 +999,10 @@ __device__ __forceinline__ void waveAppend(bool me, int i, int2 row, int* count,
             const int e = base + __popcll(m & ((1ull << lane) - 1ull));
             list[e] = i;
             if (rows) rows[e] = row;
+            if (mStamp) {
+                mStamp[i] = mVal;
+                mCid[i] = e;
+            }
         }
     }
 }
@@ -987,11 +1030,14 @@ struct ListSink {
     int* list;
     int2* rows;
     LdsList<kRows, kCap>* lds;
+    unsigned* mStamp;             // (waveAppend) null but for the compact graph's live list
+    int* mCid;
+    unsigned mVal;
 };
 template <bool kRows>
 __device__ __forceinline__ ListSink<kRows> directSink(int* count, int* list, int2* rows = nullptr)
 {
-    return ListSink<kRows>{count, list, rows, nullptr};
+    return ListSink<kRows>{count, list, rows, nullptr, nullptr, nullptr, 0u};
 }
 // workgroup-collective: before the first append (a barrier follows before use)
 template <bool kRows, int kCap>
@@ -1003,7 +1049,7 @@ template <bool kRows, int kCap>
 __device__ __forceinline__ void sinkAppend(const ListSink<kRows, kCap>& s, bool me, int i, int2 row)
 {
     if (!s.lds) {
-        waveAppend(me, i, row, s.count, s.list, kRows ? s.rows : (int2*)nullptr);
+        waveAppend(me, i, row, s.count, s.list, kRows ? s.rows : (int2*)nullptr, s.mStamp, s.mCid, s.mVal);
         return;
     }
     const unsigned long long m = __ballot(me);
@@ -1018,7 +1064,7 @@ __device__ __forceinline__ void sinkAppend(const ListSink<kRows, kCap>& s, bool 
         s.lds->idx[e] = i;
         if (kRows) s.lds->row[e] = row;
     }
-    waveAppend(me && !fits, i, row, s.count, s.list, kRows ? s.rows : (int2*)nullptr);
+    waveAppend(me && !fits, i, row, s.count, s.list, kRows ? s.rows : (int2*)nullptr, s.mStamp, s.mCid, s.mVal);
 }
 // workgroup-collective, after the last append; gbase: an LDS int
 template <bool kRows, int kCap>
@@ -1031,8 +1077,13 @@ __device__ __forceinline__ void sinkFlush(const ListSink<kRows, kCap>& s, int* g
     __syncthreads();
     const int b = *gbase;
     for (int e = threadIdx.x; e < n; e += blockDim.x) {
-        s.list[b + e] = s.lds->idx[e];
+        const int i = s.lds->idx[e];
+        s.list[b + e] = i;
         if (kRows) s.rows[b + e] = s.lds->row[e];
+        if (s.mStamp) {
+            s.mStamp[i] = s.mVal;
+            s.mCid[i] = b + e;
+        }
     }
 }
 
@@ -1308,11 +1359,12 @@ __device__ __forceinline__ bool freezable(const Params& p, double yNew, double y
 
 // setNodeDepth (dynwave.c:636-762) for node i given its summed inflow,
 // outflow, surface area and dq/dh; returns 1 when converged (dynwave.c:615-621)
-template <bool kStorage = true>
+template <bool kStorage = true, bool kWT = false>
 __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_t nf, double dt,
                                           double yLast, double yOld, double inflow, double outflow,
-                                          double surf, double sumdqdh)
+                                          double surf, double sumdqdh, int ig = 0)
 {
+    static_assert(!(kWT && kStorage), "the compact graph has no storage units");
     const double omega = 0.5;
     bool canPond = (nf & NF_CANPOND) != 0;
     double fullDepth = p.fullDepth[i];
@@ -1335,7 +1387,7 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
         dy = dV / surfArea;
         yNew = yOld + dy;
         yRaw = yNew;
-        if (!isPonded) p.oldSurfArea[i] = surfArea;
+        if (!isPonded) SWX_NST(oldSurfArea, surfArea);
         if (k > 0) yNew = (1.0 - omega) * yLast + omega * yNew;
         if (isPonded && yNew < fullDepth) yNew = fullDepth - 0.0001;
     } else {
@@ -1358,8 +1410,8 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
     const bool flooded = yNew > yMax;
     const bool plain = !isSurcharged && !canPond && !flooded && fullVolume == 0.0 && !isStorage;
     if (k >= 1) {                                      // fast-path cache for the next iteration
-        if (plain) p.yRaw[i] = yRaw;
-        p.dirty[i] = plain ? 2 : 0;
+        if (plain) SWX_NST(yRaw, yRaw);
+        p.dirty[i] = plain ? 2 : 0;                    // (iterations >= 2 read it only from the compact copy)
     }
     if (flooded) {                                     // getFloodedDepth dynwave.c:766-795
         double newVolume;
@@ -1373,20 +1425,20 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
             overflow = (newVolume - gmax(oldVolume, fullVolume)) / dt;
         }
         if (overflow < 0.0001) overflow = 0.0;
-        p.nNewVolume[i] = newVolume;
+        SWX_NST(nNewVolume, newVolume);
     } else if (kStorage && isStorage) {
         p.nNewVolume[i] = devStorageVolume(p, i, yNew);
     } else {
-        p.nNewVolume[i] = (fullDepth > 0.0) ? fullVolume * (yNew / fullDepth) : 0.0;
+        SWX_NST(nNewVolume, (fullDepth > 0.0) ? fullVolume * (yNew / fullDepth) : 0.0);
     }
-    p.overflow[i] = overflow;
-    p.nNewDepth[i] = yNew;        // Xnode.dYdT = |yNew - yOld| / dt: formed at the step end
+    SWX_NST(overflow, overflow);
+    SWX_NST(nNewDepth, yNew);     // Xnode.dYdT = |yNew - yOld| / dt: formed at the step end
     int c = (fabs(yLast - yNew) > p.headTol) ? 0 : 1;  // dynwave.c:615-621
-    p.conv[i] = c;
+    SWX_NST(conv, c);
     if (p.convW) convWord(p, i, k, c);
     if (k >= 1 && k + 1 < p.maxTrials && p.freeze && plain && c && !(nf & (NF_SHARED | NF_DEFER | NF_REPLICA)) &&
         freezable(p, yNew, yRaw, yMax, yCrown)) {
-        p.frz[i] = (unsigned char)(k + 1);
+        SWX_NST(frz, (unsigned char)(k + 1));
         return c | 2;                                  // bit 1: frozen by this update
     }
     return c;
@@ -1463,6 +1515,9 @@ __device__ __forceinline__ void outfallPrologue(const Params& p, const double* c
         double prev = 0.0;
         uint32_t nfo = 0;
         OutfallOps ops{0.0, 0.0, 0.0};
+        // a compact step's iterations k >= 2: the outfall's compact copy too
+        const bool mirror = p.cOutDepth && kProbeK >= 2;
+        int oc = 0;
         if (j >= 0) {
             x = loadGeomEager(p, j, f);
             q = kCoherentQ ? loadFlowAgent(p, j) : p.lNewFlow[j];
@@ -1473,6 +1528,7 @@ __device__ __forceinline__ void outfallPrologue(const Params& p, const double* c
                 prev = p.nNewDepth[o];
                 nfo = p.nflags[o];
                 ops = loadOutfallOps(p, o, j, f);
+                if (mirror) oc = p.cmCid[o];
             }
         }
         const bool cond = (j >= 0) && !(f & LF_NC);
@@ -1522,7 +1578,9 @@ __device__ __forceinline__ void outfallPrologue(const Params& p, const double* c
         if (j >= 0 && w == 0) {
             if (kFirst) p.nOldDepth[o] = prev;             // node_setOldHydState before the update
             if (p.nNC) p.nPrevDepth[o] = prev;
-            p.nNewDepth[o] = outfallCombine(p, o, nfo, ops, yn, sh->yc[lane]);
+            const double yo = outfallCombine(p, o, nfo, ops, yn, sh->yc[lane]);
+            p.nNewDepth[o] = yo;
+            if (mirror) p.cOutDepth[oc] = yo;
         }
         sync();
     }
@@ -1585,12 +1643,29 @@ __device__ __forceinline__ double ldAgent(const double* a)
 {
     return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-template <bool kFirst, bool kGeneral, bool kCoh = false>
+// where a node's gather reads its row and its links' values: the Params' own
+// arrays, or (the compact graph) the compact copies or the global arrays
+struct GatherSrc {
+    const int* csr;
+    const double *q, *sa1, *sa2, *dqdh, *evap, *seep;
+    const uint32_t* lf;
+};
+__device__ __forceinline__ GatherSrc gatherSrcOf(const Params& p)
+{
+    return GatherSrc{p.csr, p.lNewFlow, p.sa1, p.sa2, p.dqdh, p.evapLoss, p.seepLoss, p.lflags};
+}
+// kWT (the compact graph): p's node arrays are the compact copies, i the
+// compact index, ig the global one (write-through stores, SWX_NST); gsp: the
+// gather's source (rowIn then holds its row bounds)
+template <bool kFirst, bool kGeneral, bool kCoh = false, bool kWT = false>
 __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double dt, NodePre pre, bool& listMe,
                                          int2& row, bool& anyUnconv, int& gathered, int& live, int& fast,
-                                         bool& alive, int2 rowIn = make_int2(-1, -1))
+                                         bool& alive, int2 rowIn = make_int2(-1, -1),
+                                         const GatherSrc* gsp = nullptr, int ig = 0)
 {
     constexpr bool kStorage = kGeneral;
+    static_assert(!(kWT && (kFirst || kGeneral || kCoh)), "the compact graph: iterations >= 2, no storage units");
+    const GatherSrc gs = gsp ? *gsp : gatherSrcOf(p);
         const uint32_t nf = pre.nf;
         int type = (int)(nf & NF_TYPE);
         // an outfall's depth is written by the prologue above: not read here
@@ -1610,11 +1685,11 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
                 if (cache & 1) {
                     yLast = frozenDepth(p, i, fz, k - 1);
                     haveYLast = true;
-                    p.frz[i] = 0;
+                    SWX_NST(frz, (unsigned char)0);
                 } else {
                     if (k == p.maxTrials - 1) {            // the last possible iteration
-                        p.nNewDepth[i] = frozenDepth(p, i, fz, k);
-                        p.frz[i] = 0;
+                        SWX_NST(nNewDepth, frozenDepth(p, i, fz, k));
+                        SWX_NST(frz, (unsigned char)0);
                     }
                     alive = false;
                     done = true;
@@ -1630,13 +1705,13 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
                     double yNew = (1.0 - omega) * yLast2 + omega * yRaw;
                     if (yNew < 0) yNew = 0.0;
                     if (!(yNew > yMax)) {
-                        p.nNewDepth[i] = yNew;
+                        SWX_NST(nNewDepth, yNew);
                         int c = (fabs(yLast2 - yNew) > p.headTol) ? 0 : 1;
-                        p.conv[i] = c;
+                        SWX_NST(conv, c);
                         if (p.convW) convWord(p, i, k, c);
                         if (!c) { anyUnconv = true; listMe = true; }
                         else if (p.freeze && k + 1 < p.maxTrials && freezable(p, yNew, yRaw, yMax, yCrown)) {
-                            p.frz[i] = (unsigned char)(k + 1);
+                            SWX_NST(frz, (unsigned char)(k + 1));
                             alive = false;
                         }
                         done = true;
@@ -1730,32 +1805,32 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
                 double qv[kGather], sav[kGather], dqv[kGather];
                 uint32_t lfv[kGather];
 #pragma unroll
-                for (int t = 0; t < kGather; t++) ent[t] = (eb + t < e1) ? p.csr[eb + t] : 0;
+                for (int t = 0; t < kGather; t++) ent[t] = (eb + t < e1) ? gs.csr[eb + t] : 0;
 #pragma unroll
                 for (int t = 0; t < kGather; t++) {
                     if (eb + t < e1) {
                         const int l = ent[t] & 0x7FFFFFFF;
-                        qv[t] = kCoh ? ldAgent(&p.lNewFlow[l]) : p.lNewFlow[l];
-                        lfv[t] = p.lflags[l];
-                        const double* sp = (ent[t] < 0) ? &p.sa2[l] : &p.sa1[l];
+                        qv[t] = kCoh ? ldAgent(&gs.q[l]) : gs.q[l];
+                        lfv[t] = gs.lf[l];
+                        const double* sp = (ent[t] < 0) ? &gs.sa2[l] : &gs.sa1[l];
                         sav[t] = kCoh ? ldAgent(sp) : *sp;
-                        dqv[t] = kCoh ? ldAgent(&p.dqdh[l]) : p.dqdh[l];
+                        dqv[t] = kCoh ? ldAgent(&gs.dqdh[l]) : gs.dqdh[l];
                     }
                 }
 #pragma unroll
                 for (int t = 0; t < kGather; t++) {
                     if (eb + t >= e1) break;
                     const int l = ent[t] & 0x7FFFFFFF;
-                    const double lossSum = (lfv[t] & LF_SEEP) ? (kCoh ? ldAgent(&p.evapLoss[l]) + ldAgent(&p.seepLoss[l])
-                                                                      : p.evapLoss[l] + p.seepLoss[l])
+                    const double lossSum = (lfv[t] & LF_SEEP) ? (kCoh ? ldAgent(&gs.evap[l]) + ldAgent(&gs.seep[l])
+                                                                      : gs.evap[l] + gs.seep[l])
                                                               : 0.0;
                     addEntry(ent[t], qv[t], lfv[t], sav[t], dqv[t], lossSum);
                 }
             }
-            p.inflow[i] = inflow;
-            p.outflow[i] = outflow;
-            p.nSurf[i] = surf;
-            p.nDqdh[i] = sumdqdh;
+            SWX_NST(inflow, inflow);
+            SWX_NST(outflow, outflow);
+            SWX_NST(nSurf, surf);
+            SWX_NST(nDqdh, sumdqdh);
             if (!kFirst && k >= 2) p.dirty[i] = 0;
             gathered++;
         }
@@ -1765,7 +1840,7 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
             // conduit sums written above; k_nc adds the non-conduit links
             // and updates the depth
         } else {
-            const int r = nodeUpdate<kStorage>(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh);
+            const int r = nodeUpdate<kStorage, kWT>(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh, ig);
             if (!(r & 1)) {
                 anyUnconv = true;
                 listMe = true;
@@ -1788,7 +1863,9 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
     __shared__ int sBase;
     const ListSink<true> su{&p.ucount[k], p.ulist + (size_t)(k & 1) * p.nN, p.ulistRow + (size_t)(k & 1) * p.nN,
                             &ldsU};
-    const ListSink<true> sv{&p.vcount[1], p.vlist + p.nN, p.vlistRow + p.nN, &ldsV};
+    // (a compact step: the live nodes' membership stamps and compact ids too)
+    const ListSink<true> sv{&p.vcount[1], p.vlist + p.nN, p.vlistRow + p.nN, &ldsV,
+                            p.cmStamp, p.cmCid, iterStamp(p, 1)};
     const bool listV = !kFirst && k == 1 && p.buildVlist;
     if (!kFirst) {
         sinkInit(su);
@@ -2314,6 +2391,378 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
 }
 
 // ---------------------------------------------------------------------------
+// The compact graph (GM_COMPACT): Picard iterations k >= 2 over contiguous
+// copies of the live sub-network.
+//
+// After iteration 1 almost every junction of a large network is frozen
+// (converged, plain, relaxing toward its cached depth).  The list graph's
+// iterations k >= 2 chase list -> CSR row -> conduit -> end nodes through a
+// dozen scattered SoA arrays: about five dependent memory rounds per launch,
+// each touching one line per array per node.  Here k_cgather copies, once
+// per step, the live nodes L1 of iteration 1 (vlist(1)) and every conduit
+// incident to one of them (E_C) into compact arrays, each node's row as
+// compact conduit ids.  Every iteration k >= 2 is then
+//   k_cwalk(k)  one thread per compact conduit slot: the conduit is updated
+//               unless both ends converged in iteration k-1
+//               (findBypassedLinks, dynwave.c:335-345; an outfall never
+//               converges) -- the slot's words, then both ends' state, then
+//               dwflow_findConduitFlow (the same conduitFlow code);
+//   k_cnode(k)  one thread per compact node: findNodeDepths / setNodeDepth
+//               (dynwave.c:593-762, the same nodeItem code) with the gather
+//               over its compact row, and block 0 the outfall depths
+//               (link_setOutfallDepth, link.c:728-766) as k_node does.
+// No lists are built in iterations k >= 2 and no atomics run but for growth.
+//
+// Write-through: every store to a compact copy also goes to the global array
+// (SWX_LST / SWX_NST), so the global arrays hold the canonical state at every
+// kernel boundary and a reader may take either; the step end, quality and
+// k_unfreeze read the global arrays as in every other graph.  (A node's
+// `dirty` word is read in iterations k >= 2 only, and there only from the
+// compact copy: it is not written through.)
+//
+// Growth.  A node outside the compact set is frozen: L1 holds every node not
+// frozen after iteration 1, and every node that wakes joins.  When an updated
+// conduit has such an end, the walk claims it (CAS of its membership stamp
+// cmStamp to iterStamp(k)) and appends it; k_cnode(k) copies the fresh node,
+// appends its conduits not yet in E_C (CAS of lStamp) and updates it with the
+// gather over its global row (its compact row is never built).  An appended
+// conduit names its ends outside the compact set by ~global id and reads them
+// from the global arrays (canonical: write-through).  Every node k_node(k)
+// would update is therefore in the compact set, every conduit k_link(k) would
+// update is in E_C, each update is the same code on the same operands, and
+// the results are bitwise those of every other graph.
+//
+// Slots.  A conduit of L1 is owned by its lower-numbered end in L1 (or its
+// only end in L1) and sits in slot S c + r, c the owner's compact id and r its
+// position in the owner's row; the other end finds the slot from the owner's
+// compact id and otherPos (its position in the owner's row, static), so
+// k_cgather needs no atomics.  S = the network's largest row (at most
+// kCompactMaxDeg).  Grown conduits take slots past S |L1|.
+// Single GPU, no pumps / regulators, no cold conduits, no storage units,
+// freezing on (host-checked: Router::init, compactOk).
+constexpr int kCompactMaxDeg = 8;
+struct CView {
+    int S;
+    int seep;                    // some conduit has LF_SEEP (its depth, volume and losses are copied)
+    int* cnt;                    // [0] compact nodes, [1] compact conduit slots, [2] nodes grown (run total)
+    unsigned* lStamp;            // per global link: iterStamp of the iteration it joined E_C
+    const int* otherPos;         // per CSR entry: the link's position in its other end's row
+    int *node, *link;            // compact -> global (link -1: an empty slot)
+    int* deg;                    // per compact node: its row length; -1 gathers over the global row; -2 fresh
+    int* csr;                    // [S per node] compact conduit id | (1 << 31: the node is its node2)
+    int2* ends;                  // per slot: its end nodes, compact id (>= 0) or ~global id
+    // node copies, by compact id
+    uint32_t* nflags;
+    unsigned char *dirty, *frz;
+    int* conv;
+    double *nNewDepth, *yRaw, *yCrown, *yMaxNP, *nOldDepth, *newLat, *inflow, *outflow, *nSurf, *nDqdh;
+    double *fullDepth, *pondedArea, *oldNetInflow, *surDepth, *oldSurfArea, *fullVolume, *nOldVolume;
+    double *nNewVolume, *overflow;                // written only
+    // conduit copies, by slot; optional groups are null when no conduit needs them
+    uint32_t* lflags;
+    int* lstate;
+    double *lNewFlow, *lOldFlow, *q1, *setting, *inv1, *inv2, *a2, *modLength, *length, *roughFactor, *beta;
+    double *sa1, *sa2, *dqdh;
+    double *a1, *froude, *lNewDepth, *lNewVolume, *evapLoss, *seepLoss;   // written (copied with LF_SEEP)
+    double *cIn, *cOut, *cAvg;                    // LF_LOSSES
+    double* qLimit;                               // LF_QLIMIT
+    double *seepRate, *lOldDepth;                 // LF_SEEP
+    double *yFull, *wMax, *ywMax, *aFull, *rFull, *sFull, *sMax, *yBot, *aBot, *sBot, *rBot;   // not kFast
+};
+
+// the Params conduitFlow / nodeItem see in the compact kernels: node and
+// conduit arrays on the compact copies, write-through to the global ones
+__device__ __forceinline__ Params compactView(const Params& p, const CView& v)
+{
+    Params q = p;
+    q.wt = Params::WThrough{p.lNewFlow, p.lNewDepth, p.lNewVolume, p.a1, p.q1, p.dqdh, p.froude, p.sa1, p.sa2,
+                            p.evapLoss, p.seepLoss, p.lstate, p.nNewDepth, p.yRaw, p.oldSurfArea, p.inflow,
+                            p.outflow, p.nSurf, p.nDqdh, p.nNewVolume, p.overflow, p.conv, p.frz};
+    q.lflags = v.lflags; q.lstate = v.lstate;
+    q.lNewFlow = v.lNewFlow; q.lOldFlow = v.lOldFlow; q.q1 = v.q1; q.setting = v.setting;
+    q.inv1 = v.inv1; q.inv2 = v.inv2; q.a1 = v.a1; q.a2 = v.a2;
+    q.modLength = v.modLength; q.length = v.length; q.roughFactor = v.roughFactor; q.beta = v.beta;
+    q.sa1 = v.sa1; q.sa2 = v.sa2; q.dqdh = v.dqdh; q.froude = v.froude;
+    q.lNewDepth = v.lNewDepth; q.lNewVolume = v.lNewVolume; q.lOldDepth = v.lOldDepth;
+    q.evapLoss = v.evapLoss; q.seepLoss = v.seepLoss; q.seepRate = v.seepRate;
+    q.cIn = v.cIn; q.cOut = v.cOut; q.cAvg = v.cAvg; q.qLimit = v.qLimit;
+    q.yFull = v.yFull; q.wMax = v.wMax; q.ywMax = v.ywMax; q.aFull = v.aFull; q.rFull = v.rFull;
+    q.sFull = v.sFull; q.sMax = v.sMax; q.yBot = v.yBot; q.aBot = v.aBot; q.sBot = v.sBot; q.rBot = v.rBot;
+    q.lTabOff = nullptr;                          // basic shapes only
+    q.nflags = v.nflags; q.dirty = v.dirty; q.frz = v.frz; q.conv = v.conv;
+    q.nNewDepth = v.nNewDepth; q.yRaw = v.yRaw; q.yCrown = v.yCrown; q.yMaxNP = v.yMaxNP;
+    q.nOldDepth = v.nOldDepth; q.newLat = v.newLat; q.inflow = v.inflow; q.outflow = v.outflow;
+    q.nSurf = v.nSurf; q.nDqdh = v.nDqdh; q.fullDepth = v.fullDepth; q.pondedArea = v.pondedArea;
+    q.oldNetInflow = v.oldNetInflow; q.surDepth = v.surDepth; q.oldSurfArea = v.oldSurfArea;
+    q.fullVolume = v.fullVolume; q.nOldVolume = v.nOldVolume; q.nNewVolume = v.nNewVolume;
+    q.overflow = v.overflow;
+    q.csr = v.csr;
+    q.rowptr = nullptr;                           // rows come with each item
+    q.convW = nullptr;
+    return q;
+}
+
+// node g's state into compact node c
+__device__ __forceinline__ void copyNode(const Params& p, const CView& v, int g, int c)
+{
+    const uint32_t nf = p.nflags[g];
+    const unsigned char dy = p.dirty[g], fz = p.frz[g];
+    const int cn = p.conv[g];
+    const double a0 = p.nNewDepth[g], a1 = p.yRaw[g], a2 = p.yCrown[g], a3 = p.yMaxNP[g], a4 = p.nOldDepth[g];
+    const double a5 = p.newLat[g], a6 = p.inflow[g], a7 = p.outflow[g], a8 = p.nSurf[g], a9 = p.nDqdh[g];
+    const double b0 = p.fullDepth[g], b1 = p.pondedArea[g], b2 = p.oldNetInflow[g], b3 = p.surDepth[g];
+    const double b4 = p.oldSurfArea[g], b5 = p.fullVolume[g], b6 = p.nOldVolume[g];
+    v.nflags[c] = nf; v.dirty[c] = dy; v.frz[c] = fz; v.conv[c] = cn;
+    v.nNewDepth[c] = a0; v.yRaw[c] = a1; v.yCrown[c] = a2; v.yMaxNP[c] = a3; v.nOldDepth[c] = a4;
+    v.newLat[c] = a5; v.inflow[c] = a6; v.outflow[c] = a7; v.nSurf[c] = a8; v.nDqdh[c] = a9;
+    v.fullDepth[c] = b0; v.pondedArea[c] = b1; v.oldNetInflow[c] = b2; v.surDepth[c] = b3;
+    v.oldSurfArea[c] = b4; v.fullVolume[c] = b5; v.nOldVolume[c] = b6;
+}
+// conduit l's state into compact slot m
+__device__ __forceinline__ void copyLink(const Params& p, const CView& v, int l, int m)
+{
+    const uint32_t f = p.lflags[l];
+    const int st = p.lstate[l];
+    const double a0 = p.lNewFlow[l], a1 = p.lOldFlow[l], a2 = p.q1[l], a3 = p.setting[l], a4 = p.inv1[l];
+    const double a5 = p.inv2[l], a6 = p.a2[l], a7 = p.modLength[l], a8 = p.length[l], a9 = p.roughFactor[l];
+    const double b0 = p.beta[l], b1 = p.sa1[l], b2 = p.sa2[l], b3 = p.dqdh[l];
+    v.lflags[m] = f; v.lstate[m] = st;
+    v.lNewFlow[m] = a0; v.lOldFlow[m] = a1; v.q1[m] = a2; v.setting[m] = a3; v.inv1[m] = a4;
+    v.inv2[m] = a5; v.a2[m] = a6; v.modLength[m] = a7; v.length[m] = a8; v.roughFactor[m] = a9;
+    v.beta[m] = b0; v.sa1[m] = b1; v.sa2[m] = b2; v.dqdh[m] = b3;
+    if (v.cIn) { v.cIn[m] = p.cIn[l]; v.cOut[m] = p.cOut[l]; v.cAvg[m] = p.cAvg[l]; }
+    if (v.qLimit) v.qLimit[m] = p.qLimit[l];
+    if (v.seep) {
+        v.seepRate[m] = p.seepRate[l]; v.lOldDepth[m] = p.lOldDepth[l];
+        v.lNewDepth[m] = p.lNewDepth[l]; v.lNewVolume[m] = p.lNewVolume[l];
+        v.evapLoss[m] = p.evapLoss[l]; v.seepLoss[m] = p.seepLoss[l];
+    }
+    if (v.yFull) {
+        v.yFull[m] = p.yFull[l]; v.wMax[m] = p.wMax[l]; v.ywMax[m] = p.ywMax[l]; v.aFull[m] = p.aFull[l];
+        v.rFull[m] = p.rFull[l]; v.sFull[m] = p.sFull[l]; v.sMax[m] = p.sMax[l]; v.yBot[m] = p.yBot[l];
+        v.aBot[m] = p.aBot[l]; v.sBot[m] = p.sBot[l]; v.rBot[m] = p.rBot[l];
+    }
+}
+
+// After k_node(1) of a compact step: L1 (vlist(1), whose entries k_node(1)
+// stamped with their list position = compact id) and the conduits it owns
+// (see "Slots") into the compact arrays.  One thread per L1 node; its row's
+// words, then the other ends' membership, then the copies.
+__global__ __launch_bounds__(kBlock) void k_cgather(Params p, CView v)
+{
+    const int vc = p.vcount[1];
+    if (p.unconv[1] == 0) return;                 // converged at iteration 1: no iteration k >= 2 runs
+    const int S = v.S;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        v.cnt[0] = vc;
+        v.cnt[1] = S * vc;
+    }
+    const unsigned s1 = iterStamp(p, 1);
+    const int* vl = p.vlist + p.nN;
+    const int2* vr = p.vlistRow + p.nN;
+    for (int t = blockIdx.x * kBlock + threadIdx.x; t < vc; t += gridDim.x * kBlock) {
+        const int g = vl[t];
+        const int2 rb = vr[t];
+        int ent[kCompactMaxDeg], o[kCompactMaxDeg], op[kCompactMaxDeg];
+#pragma unroll
+        for (int r = 0; r < kCompactMaxDeg; r++) {
+            const bool in = r < S && rb.x + r < rb.y;
+            ent[r] = in ? p.csr[rb.x + r] : 0;
+            o[r] = in ? p.csrOther[rb.x + r] : -1;
+            op[r] = in ? v.otherPos[rb.x + r] : 0;
+        }
+        copyNode(p, v, g, t);
+        v.node[t] = g;
+        v.deg[t] = rb.y - rb.x;
+        unsigned ost[kCompactMaxDeg];
+        int oc[kCompactMaxDeg];
+#pragma unroll
+        for (int r = 0; r < kCompactMaxDeg; r++) {
+            ost[r] = (o[r] >= 0) ? p.cmStamp[o[r]] : 0u;
+            oc[r] = (o[r] >= 0) ? p.cmCid[o[r]] : 0;
+        }
+#pragma unroll
+        for (int r = 0; r < kCompactMaxDeg; r++) {
+            if (r >= S) break;
+            const int s = S * t + r;
+            int lnk = -1;
+            if (o[r] >= 0) {
+                const int l = ent[r] & 0x7FFFFFFF;
+                const bool oIn = ost[r] == s1;
+                const bool mine = !oIn || g < o[r];
+                if (mine) {
+                    lnk = l;
+                    copyLink(p, v, l, s);
+                    const int oe = oIn ? oc[r] : ~o[r];
+                    v.ends[s] = (ent[r] < 0) ? make_int2(oe, t) : make_int2(t, oe);
+                    v.lStamp[l] = s1;
+                }
+                v.csr[s] = (mine ? s : S * oc[r] + op[r]) | (ent[r] & (int)0x80000000);
+            }
+            v.link[s] = lnk;
+        }
+    }
+}
+
+// an end node's state as the walk reads it: a compact node's copy, or (~g)
+// the global arrays and g's membership stamp
+struct CEnd {
+    double y, yr;
+    int fz, conv;
+    unsigned st;
+};
+__device__ __forceinline__ CEnd cEnd(const Params& p, const CView& v, int e)
+{
+    CEnd r;
+    if (e >= 0) {
+        r.y = v.nNewDepth[e];
+        r.yr = v.yRaw[e];
+        r.fz = v.frz[e];
+        r.conv = v.conv[e];
+        r.st = 0u;
+    } else {
+        const int g = ~e;
+        r.y = p.nNewDepth[g];
+        r.yr = p.yRaw[g];
+        r.fz = p.frz[g];
+        r.conv = p.conv[g];
+        r.st = p.cmStamp[g];
+    }
+    return r;
+}
+// an end of a conduit updated in iteration k: its sums are stale (dirty); an
+// end outside the compact set (frozen) is woken: claimed and appended
+__device__ __forceinline__ void cWake(const Params& p, const CView& v, int e, unsigned st, unsigned s1, unsigned sK)
+{
+    if (e >= 0) {
+        v.dirty[e] = 1;
+        return;
+    }
+    const int g = ~e;
+    if (st >= s1) {
+        if (st < sK) v.dirty[p.cmCid[g]] = 1;     // joined in an earlier launch
+        return;                                    // (sK: claimed in this launch, its claimer marks it)
+    }
+    if (atomicCAS(&p.cmStamp[g], st, sK) != st) return;   // claimed by another thread of this launch
+    const int c = atomicAdd(&v.cnt[0], 1);
+    v.node[c] = g;
+    v.deg[c] = -2;                                 // fresh: k_cnode(k) copies and updates it
+    p.cmCid[g] = c;
+    atomicAdd(&v.cnt[2], 1);
+}
+
+template <bool kFast>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kLinkWavesDefault))) void k_cwalk(Params p,
+                                                                                                       CView v,
+                                                                                                       int k)
+{
+    const int n = v.cnt[1];                       // loads with the flag below
+    if (p.unconv[k - 1] == 0) return;             // converged: dynwave.c:249-251
+    if (blockIdx.x * kBlock >= n) return;         // a workgroup with no first-round slot has none (uniform)
+    probeMark(p, k, PR_L_IN);
+    const int tid = blockIdx.x * kBlock + threadIdx.x, nthr = gridDim.x * kBlock;
+    __shared__ double ct[kFast ? kCtFast : 5 * SWX_CIRC_N];
+    stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
+    probeMark(p, k, PR_L_STAGED);
+    const Params pc = compactView(p, v);
+    const double dt = p.ctl->dt;
+    const unsigned s1 = iterStamp(p, 1), sK = iterStamp(p, k);
+    int work = 0;
+    for (int m = tid; m < n; m += nthr) {
+        const int l = v.link[m];
+        const uint32_t f = v.lflags[m];
+        const int2 en = v.ends[m];
+        if (l < 0) continue;                      // an empty slot
+        const CEnd a = cEnd(p, v, en.x), b = cEnd(p, v, en.y);
+        const bool listed1 = (f & LF_N1_OUTFALL) || !a.conv, listed2 = (f & LF_N2_OUTFALL) || !b.conv;
+        if (!listed1 && !listed2) continue;       // both ends converged: bypassed
+        const double y1 = frozenDepthV(a.y, a.yr, a.fz, k - 1);
+        const double y2 = frozenDepthV(b.y, b.yr, b.fz, k - 1);
+        conduitFlow<false, false, kFast, true>(pc, m, f, make_int2(0, 0), k, dt, ct, y1, y2, l);
+        cWake(p, v, en.x, a.st, s1, sK);
+        cWake(p, v, en.y, b.st, s1, sK);
+        work++;
+    }
+    probeMark(p, k, PR_L_WORK);
+    probeMark(p, k, PR_L_OUT);
+    if (p.countWork) {                            // measurement only
+        for (int off = 32; off > 0; off >>= 1) work += __shfl_down(work, off, 64);
+        if ((threadIdx.x & 63) == 0 && work) atomicAdd(&p.work[k], (unsigned long long)work);
+    }
+}
+
+// a fresh node (woken by the walk of this iteration): its copy, then its
+// conduits not yet in E_C (each appended by one of its fresh ends); returns
+// its flag words for the update
+__device__ __forceinline__ NodePre cFresh(const Params& p, const CView& v, int g, int c, unsigned s1, unsigned sK)
+{
+    copyNode(p, v, g, c);
+    v.dirty[c] = 1;                               // an incident conduit was updated
+    v.deg[c] = -1;                                // gathers over its global row from now on
+    const int e0 = p.rowptr[g], e1 = p.rowptr[g + 1];
+    for (int e = e0; e < e1; e++) {
+        const int ent = p.csr[e], l = ent & 0x7FFFFFFF;
+        const unsigned ls = v.lStamp[l];
+        if (ls >= s1) continue;                   // in E_C already (or appended in this launch)
+        if (atomicCAS(&v.lStamp[l], ls, sK) != ls) continue;
+        const int m = atomicAdd(&v.cnt[1], 1);
+        copyLink(p, v, l, m);
+        v.link[m] = l;
+        const int oe = ~p.csrOther[e];
+        v.ends[m] = (ent < 0) ? make_int2(oe, c) : make_int2(c, oe);
+    }
+    return NodePre{p.nflags[g], 1, p.frz[g]};
+}
+
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_cnode(Params p, CView v, int k)
+{
+    const int n = v.cnt[0];                       // loads with the flag below
+    if (p.unconv[k - 1] == 0) return;
+    probeMark(p, k, PR_N_IN);
+    probeMark(p, k, PR_N_LAST_IN);
+    // block 0: the outfall depths of this iteration (as k_node), also into
+    // their compact copies (Params::cOutDepth)
+    const bool proOnly = p.nOutLinks > 0 && p.nOutLinks <= 64 && gridDim.x > 1;
+    if (blockIdx.x * 64 < p.nOutLinks) {
+        __shared__ OutfallLds sh;
+        outfallPrologue<false, false>(p, p.gTables, &sh, false, k);
+        if (blockIdx.x == 0) probeMark(p, k, PR_N_PRO);
+        if (proOnly) {
+            probeMark(p, k, PR_N_OUT);
+            probeMark(p, k, PR_N_B0);
+            return;
+        }
+    }
+    const int b = (int)blockIdx.x - (proOnly ? 1 : 0);
+    const int nt = ((int)gridDim.x - (proOnly ? 1 : 0)) * kBlock;
+    if (b * kBlock >= n) return;                  // uniform
+    const Params pc = compactView(p, v);
+    const GatherSrc gc{v.csr, v.lNewFlow, v.sa1, v.sa2, v.dqdh, v.evapLoss, v.seepLoss, v.lflags};
+    const GatherSrc gg = gatherSrcOf(p);
+    const double dt = p.ctl->dt;
+    const unsigned s1 = iterStamp(p, 1), sK = iterStamp(p, k);
+    bool anyUnconv = false;
+    int gathered = 0, live = 0, fast = 0;
+    for (int c = b * kBlock + (int)threadIdx.x; c < n; c += nt) {
+        int deg = v.deg[c];
+        const int g = v.node[c];
+        NodePre pre{v.nflags[c], v.dirty[c], v.frz[c]};
+        if (deg == -2) {
+            pre = cFresh(p, v, g, c, s1, sK);
+            deg = -1;
+        }
+        const bool own = deg >= 0;
+        const int2 rowIn = own ? make_int2(v.S * c, v.S * c + deg) : make_int2(p.rowptr[g], p.rowptr[g + 1]);
+        bool listMe = false, alive = true;
+        int2 row = make_int2(0, 0);
+        nodeItem<false, false, false, true>(pc, k, c, dt, pre, listMe, row, anyUnconv, gathered, live, fast, alive,
+                                            rowIn, own ? &gc : &gg, g);
+    }
+    nodePassEnd(p, k, anyUnconv, gathered, live, fast, true);
+    probeMark(p, k, PR_N_OUT);
+}
+
+// ---------------------------------------------------------------------------
 // k_fused: Picard iteration k >= 2 in ONE launch (the fused graph, GM_FUSED).
 // The list graph's two launches per iteration (walk, then node update) are
 // latency chains of ~13 and ~19 us on the surcharged 1M grid; here every node
@@ -2383,6 +2832,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
         // lookups are dependent loads, and the memory system is busy here
         __shared__ OutfallLds sh;
         for (int t = threadIdx.x; t < p.nOutLinks; t += kBlock) (void)pollStamp(p, &p.lstamp[outLinkAt(p, t)], stamp);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);       // (as in phase 2 below)
         __syncthreads();
         probeMark(p, k, PR_N_PRO);
         if (p.nOutLinks > 0) outfallPrologue<false, kGeneral, 6, BlockSync, true>(p, ct, &sh, true, k);
@@ -2560,6 +3010,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
                     __hip_atomic_load(&p.ctl->tailErr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                     break;
             }
+            // (ordering: the producers' stores went through the L2 and were
+            // drained before their stamps, and the values are read at agent
+            // scope below; this compiler barrier keeps those reads after the
+            // stamps were seen.  The graph relies on gfx9's in-order
+            // write-through of agent-scope stores, not on a release/acquire
+            // pair, whose L2 writeback measured too slow: it stays opt-in,
+            // DESIGN §4)
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
             NodePre pre = loadNodePre(p, n, k);
             if (need) pre.cache = 1;                     // an incident conduit was updated (the walk's mark)
             nodeItem<false, kGeneral, true>(p, k, n, dt, pre, listMe, rowOut, anyUnconv, gathered, live, fast, alive,
@@ -3662,7 +4120,7 @@ struct Router::Impl {
     bool sparseOk = false;
     double sparseMax = 6000.0;
     double liveAvg = 0.0;            // moving average of the live-list length after iteration 1
-    long long modeSteps[5] = {0, 0, 0, 0, 0};   // steps launched per graph (unrolled, k_tail, sparse, list, fused)
+    long long modeSteps[6] = {0, 0, 0, 0, 0, 0};   // steps launched per graph (unrolled, k_tail, sparse, list, fused, compact)
     hipGraphExec_t graphList = nullptr;   // iterations k >= 2 as list-driven k_walk / k_node_list pairs
     // iterations k >= 2 as one k_fused launch each (fusedGrid > 0 only:
     // built for SWMM5_SPARSE = 4 (then always used) or SWMM5_FUSED = 1 / 2
@@ -3672,6 +4130,16 @@ struct Router::Impl {
     bool fusedAuto = false;
     unsigned* convW = nullptr;       // Params::convW while a fused step is launched
     double listMax = 200000.0;       // auto: the list graph while the live lists average at most this
+    // iterations k >= 2 over the compact copies of the live sub-network
+    // (k_cgather, then k_cwalk / k_cnode per iteration): compactOk when the
+    // network qualifies (SWMM5_SPARSE = 5: always; SWMM5_COMPACT = 0: never in
+    // the auto choice, where it takes the list graph's place)
+    hipGraphExec_t graphCompact = nullptr;
+    bool compactOk = false, compactAuto = true;
+    CView cv{};
+    unsigned* cmStamp = nullptr;
+    int* cmCid = nullptr;
+    int gridCWalk = 1, gridCNode = 1, gridCGather = 1;
     bool useGraph = true;
     bool timing = false;
     int gridL = 1, gridN = 1, gridEnd = 1, gridC = 1;
@@ -3749,6 +4217,7 @@ Router::~Router()
         if (d_->graphSparse) (void)hipGraphExecDestroy(d_->graphSparse);
         if (d_->graphList) (void)hipGraphExecDestroy(d_->graphList);
         if (d_->graphFused) (void)hipGraphExecDestroy(d_->graphFused);
+        if (d_->graphCompact) (void)hipGraphExecDestroy(d_->graphCompact);
         for (auto& t : d_->tslots) {
             for (auto e : t.ev) (void)hipEventDestroy(e);
             for (auto e : t.evHot) (void)hipEventDestroy(e);
@@ -4014,7 +4483,9 @@ static TailFn sparseKernel(bool fast, bool general)
 // (d->sparseOk only)
 // GM_FUSED: iterations k >= 2 as one k_fused launch each, then k_unfreeze
 // (d->fusedGrid > 0 only)
-enum { GM_UNROLLED = 0, GM_TAIL = 1, GM_SPARSE = 2, GM_LIST = 3, GM_FUSED = 4 };
+// GM_COMPACT: k_cgather, then iterations k >= 2 as k_cwalk / k_cnode pairs
+// over the compact copies, then k_unfreeze (d->compactOk only)
+enum { GM_UNROLLED = 0, GM_TAIL = 1, GM_SPARSE = 2, GM_LIST = 3, GM_FUSED = 4, GM_COMPACT = 5 };
 typedef void (*FusedFn)(Params, int);
 static FusedFn fusedKernel(bool fast, bool general)
 {
@@ -4030,9 +4501,18 @@ static int launchStep(Router::Impl* d, int mode = GM_UNROLLED)
     Params& p = d->p;
     const int defer = p.deferPro;
     p.convW = (mode == GM_FUSED) ? d->convW : nullptr;
-    if (mode == GM_FUSED) p.deferPro = 0;
+    if (mode == GM_FUSED || mode == GM_COMPACT) p.deferPro = 0;
+    // the compact graph: k_node(1) stamps the live nodes' membership, and the
+    // outfall prologue of iterations k >= 2 writes the compact copies too
+    const bool compact = mode == GM_COMPACT;
+    p.cmStamp = compact ? d->cmStamp : nullptr;
+    p.cmCid = compact ? d->cmCid : nullptr;
+    p.cOutDepth = compact ? d->cv.nNewDepth : nullptr;
     const int r = launchStepImpl(d, mode);
     p.convW = nullptr;
+    p.cmStamp = nullptr;
+    p.cmCid = nullptr;
+    p.cOutDepth = nullptr;
     p.deferPro = defer;
     return r;
 }
@@ -4040,7 +4520,7 @@ static int launchStepImpl(Router::Impl* d, int mode)
 {
     Params& p = d->p;
     // k_node(1) lists the live nodes only for the list-driven graphs
-    p.buildVlist = (mode == GM_SPARSE || mode == GM_LIST || mode == GM_FUSED) ? 1 : 0;
+    p.buildVlist = (mode == GM_SPARSE || mode == GM_LIST || mode == GM_FUSED || mode == GM_COMPACT) ? 1 : 0;
     const bool multi = d->part.active();
     const int base = 4 * p.maxTrials;
     hipEvent_t* ev = d->timing ? d->curEv : nullptr;
@@ -4083,6 +4563,18 @@ static int launchStepImpl(Router::Impl* d, int mode)
         for (int k = 2; k < p.maxTrials; k++)
             launchTimed(d, fusedKernel(d->fastLinks, d->general), dim3(d->fusedGrid), ev ? ev[4 * k] : nullptr,
                         d->timing ? d->curHot[k] : nullptr, p, k);
+        launchTimed(d, k_unfreeze, dim3(d->gridN), (hipEvent_t) nullptr, (hipEvent_t) nullptr, p);
+    } else if (mode == GM_COMPACT) {
+        for (int k = 0; k < 2; k++)
+            if (int r = launchIteration(d, k)) return r;
+        // (timing: the gather is counted with iteration 2's walk)
+        launchTimed(d, k_cgather, dim3(d->gridCGather), ev ? ev[8] : nullptr, (hipEvent_t) nullptr, p, d->cv);
+        for (int k = 2; k < p.maxTrials; k++) {
+            launchTimed(d, d->fastLinks ? k_cwalk<true> : k_cwalk<false>, dim3(d->gridCWalk),
+                        (ev && k > 2) ? ev[4 * k] : nullptr, d->timing ? d->curHot[k] : nullptr, p, d->cv, k);
+            launchTimed(d, k_cnode, dim3(d->gridCNode), ev ? ev[4 * k + 1] : nullptr, ev ? ev[4 * k + 2] : nullptr,
+                        p, d->cv, k);
+        }
         launchTimed(d, k_unfreeze, dim3(d->gridN), (hipEvent_t) nullptr, (hipEvent_t) nullptr, p);
     } else {
         for (int k = 0; k < p.maxTrials; k++)
@@ -5127,6 +5619,103 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         HIPCHECK(hipGraphInstantiate(&d->graphFused, g, nullptr, nullptr, 0));
         (void)hipGraphDestroy(g);
     }
+    // the compact graph: the list graph's conditions, plus freezing on (L1 is
+    // the nodes not frozen after iteration 1), no cold conduits, no storage
+    // units (the compact node update is nodeItem<.., kGeneral = false>), rows
+    // of at most kCompactMaxDeg entries (the slots) and no conduit from a node
+    // to itself (maxRowDeg is huge then)
+    {
+        const char* cm = getenv("SWMM5_COMPACT");
+        d->compactAuto = !(cm && atoi(cm) == 0);
+        const bool asked = d->sparseMode == 5 || d->compactAuto;
+        d->compactOk = asked && d->sparseOk && p.freeze && p.nCold == 0 && !d->general && maxRowDeg >= 1 &&
+                       maxRowDeg <= kCompactMaxDeg;
+    }
+    if (d->compactOk) {
+        CView& v = d->cv;
+        const int S = maxRowDeg;
+        const size_t capN = std::max<size_t>(nN, 1), capL = (size_t)S * nN + (size_t)nL + 1;
+        bool losses = false, qlim = false, seep = false;
+        for (int j = 0; j < nOwn; j++) {
+            const uint32_t f = (uint32_t)lflags[j];
+            losses = losses || (f & LF_LOSSES);
+            qlim = qlim || (f & LF_QLIMIT);
+            seep = seep || (f & LF_SEEP);
+        }
+        v.S = S;
+        v.seep = seep ? 1 : 0;
+        // per CSR entry: the link's position in its other end's row
+        std::vector<int> pos1(nL, 0), pos2(nL, 0), other((size_t)d->nE, 0);
+        for (int i = 0; i < nN; i++)
+            for (int e2 = rowptr[i]; e2 < rowptr[i + 1]; e2++) {
+                const int l = csr[e2] & 0x7FFFFFFF;
+                (csr[e2] < 0 ? pos2 : pos1)[l] = e2 - rowptr[i];
+            }
+        for (int i = 0; i < nN; i++)
+            for (int e2 = rowptr[i]; e2 < rowptr[i + 1]; e2++) {
+                const int l = csr[e2] & 0x7FFFFFFF;
+                other[e2] = (csr[e2] < 0) ? pos1[l] : pos2[l];
+            }
+        int* op;
+        UPI(op, other, other.size());
+        v.otherPos = op;
+        hipError_t ea = hipSuccess;
+        auto aD = [&](double*& ptr, size_t n) { if (ea == hipSuccess) ptr = devAlloc<double>(d, n, &ea); };
+        auto aI = [&](int*& ptr, size_t n) { if (ea == hipSuccess) ptr = devAlloc<int>(d, n, &ea); };
+        auto aU = [&](uint32_t*& ptr, size_t n) { if (ea == hipSuccess) ptr = devAlloc<uint32_t>(d, n, &ea); };
+        auto aB = [&](unsigned char*& ptr, size_t n) { if (ea == hipSuccess) ptr = devAlloc<unsigned char>(d, n, &ea); };
+        aI(v.cnt, 4);
+        aU(v.lStamp, std::max<size_t>(nL, 1));
+        aU(d->cmStamp, capN);
+        aI(d->cmCid, capN);
+        aI(v.node, capN);
+        aI(v.deg, capN);
+        aI(v.csr, (size_t)S * capN);
+        aI(v.link, capL);
+        if (ea == hipSuccess) v.ends = devAlloc<int2>(d, capL, &ea);
+        aU(v.nflags, capN);
+        aB(v.dirty, capN);
+        aB(v.frz, capN);
+        aI(v.conv, capN);
+        for (double** a : {&v.nNewDepth, &v.yRaw, &v.yCrown, &v.yMaxNP, &v.nOldDepth, &v.newLat, &v.inflow, &v.outflow,
+                           &v.nSurf, &v.nDqdh, &v.fullDepth, &v.pondedArea, &v.oldNetInflow, &v.surDepth,
+                           &v.oldSurfArea, &v.fullVolume, &v.nOldVolume, &v.nNewVolume, &v.overflow})
+            aD(*a, capN);
+        aU(v.lflags, capL);
+        aI(v.lstate, capL);
+        for (double** a : {&v.lNewFlow, &v.lOldFlow, &v.q1, &v.setting, &v.inv1, &v.inv2, &v.a2, &v.modLength,
+                           &v.length, &v.roughFactor, &v.beta, &v.sa1, &v.sa2, &v.dqdh, &v.a1, &v.froude,
+                           &v.lNewDepth, &v.lNewVolume, &v.evapLoss, &v.seepLoss})
+            aD(*a, capL);
+        if (losses) for (double** a : {&v.cIn, &v.cOut, &v.cAvg}) aD(*a, capL);
+        if (qlim) aD(v.qLimit, capL);
+        if (seep) for (double** a : {&v.seepRate, &v.lOldDepth}) aD(*a, capL);
+        if (!d->fastLinks)
+            for (double** a : {&v.yFull, &v.wMax, &v.ywMax, &v.aFull, &v.rFull, &v.sFull, &v.sMax, &v.yBot, &v.aBot,
+                               &v.sBot, &v.rBot})
+                aD(*a, capL);
+        if (ea == hipSuccess) ea = hipMemset(v.cnt, 0, 4 * sizeof(int));
+        if (ea == hipSuccess) ea = hipMemset(v.lStamp, 0, std::max<size_t>(nL, 1) * sizeof(unsigned));
+        if (ea == hipSuccess) ea = hipMemset(d->cmStamp, 0, capN * sizeof(unsigned));
+        if (ea != hipSuccess) { fail(std::string("compact graph: ") + hipGetErrorString(ea)); return err_; }
+        // the walk: two workgroups per CU (one thread per slot, S |L1| slots);
+        // the node pass and the gather: two per CU (one thread per node)
+        const int cus = std::max(prop.multiProcessorCount, 1);
+        d->gridCWalk = 2 * cus;
+        d->gridCNode = 2 * cus;
+        d->gridCGather = 2 * cus;
+        if (const char* gw = getenv("SWMM5_CWALK_GRID")) d->gridCWalk = std::max(1, (int)(atof(gw) * cus));
+        if (const char* gn2 = getenv("SWMM5_CNODE_GRID")) d->gridCNode = std::max(2, (int)(atof(gn2) * cus));
+        HIPCHECK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
+        if (launchStep(d, GM_COMPACT)) {
+            (void)hipStreamEndCapture(d->stream, &g);
+            fail(d->xerrMsg);
+            return err_;
+        }
+        HIPCHECK(hipStreamEndCapture(d->stream, &g));
+        HIPCHECK(hipGraphInstantiate(&d->graphCompact, g, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(g);
+    }
     HIPCHECK(hipStreamSynchronize(d->stream));
     ok_ = true;
     return 0;
@@ -5313,9 +5902,13 @@ static int chooseGraph(Router::Impl* d)
     if (d->sparseOk && d->sparseMode == 1) return GM_SPARSE;
     if (d->sparseOk && d->sparseMode == 3) return GM_LIST;
     if (d->fusedGrid > 0 && d->sparseMode == 4) return GM_FUSED;
+    if (d->compactOk && d->sparseMode == 5) return GM_COMPACT;
     if (d->tailGrid > 0 && (d->tailMode == 1 || fresh || d->itersAvg <= kTailIters)) return GM_TAIL;
     if (d->sparseOk && !fresh && d->liveAvg <= d->sparseMax) return GM_SPARSE;
-    if (d->sparseOk && !fresh && d->liveAvg <= d->listMax) return (d->fusedGrid > 0 && d->fusedAuto) ? GM_FUSED : GM_LIST;
+    if (d->sparseOk && !fresh && d->liveAvg <= d->listMax) {
+        if (d->compactOk && d->compactAuto) return GM_COMPACT;
+        return (d->fusedGrid > 0 && d->fusedAuto) ? GM_FUSED : GM_LIST;
+    }
     return GM_UNROLLED;
 }
 
@@ -5409,11 +6002,12 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
     } else if (d->useGraph) {
         const int mode = chooseGraph(d);
         d->modeSteps[mode]++;
-        HIPCHECK(hipGraphLaunch(mode == GM_SPARSE  ? d->graphSparse
-                                : mode == GM_LIST  ? d->graphList
-                                : mode == GM_FUSED ? d->graphFused
-                                : mode == GM_TAIL  ? d->graphTail
-                                                   : d->graph,
+        HIPCHECK(hipGraphLaunch(mode == GM_SPARSE    ? d->graphSparse
+                                : mode == GM_LIST    ? d->graphList
+                                : mode == GM_FUSED   ? d->graphFused
+                                : mode == GM_COMPACT ? d->graphCompact
+                                : mode == GM_TAIL    ? d->graphTail
+                                                     : d->graph,
                                 d->stream));
     } else if (launchStep(d)) {                   // eager (host-transport exchange)
         fail(d->xerrMsg);
@@ -6179,13 +6773,20 @@ void Router::timedWork(double* updated, double* hot, double* gathered, double* g
     *gatherIters = d_->gatherCnt;
 }
 
-void Router::graphStats(long long out[7])
+void Router::graphStats(long long out[9])
 {
     flushTiming(d_);
     out[0] = d_->itersTimed1;
     for (int m = 0; m < 4; m++) out[1 + m] = d_->modeSteps[m];
     out[5] = d_->p.deferPro;
     out[6] = d_->modeSteps[GM_FUSED];
+    out[7] = d_->modeSteps[GM_COMPACT];
+    // nodes the compact walks added to the compact sets (growth; a diagnostic:
+    // synchronous read)
+    int c[4] = {0, 0, 0, 0};
+    if (d_->cv.cnt && hipStreamSynchronize(d_->stream) == hipSuccess)
+        (void)hipMemcpy(c, d_->cv.cnt, sizeof(c), hipMemcpyDeviceToHost);
+    out[8] = c[2];
 }
 
 int Router::kernelTimes(double* out, int n)

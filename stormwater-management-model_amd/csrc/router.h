@@ -47,7 +47,7 @@ public:
     void timedWork(double* updated, double* hot, double* gathered, double* gatherIters);
     // timed iterations k >= 1 that ran; steps launched with the unrolled,
     // k_tail, k_sparse and list step graphs
-    void graphStats(long long out[7]);
+    void graphStats(long long out[9]);   // timed iterations, steps per graph, deferred outfalls, compact growth
     // Sum (op 0) or min (op 1) of n host doubles over the ranks (no-op on one GPU).
     int allreduceHost(double* buf, int n, int op);
     // average duration (us) of `reps` back-to-back launches of kernel `which`

@@ -275,12 +275,12 @@ class SWMM:
         return err, t.value
 
     def counters(self):
-        a = (ctypes.c_longlong * 17)()
-        self.L.swmmx_getCounters(a, 17)
+        a = (ctypes.c_longlong * 19)()
+        self.L.swmmx_getCounters(a, 19)
         keys = ["steps", "iterations", "nonconverged", "last_iterations", "conduits", "nodes",
                 "timed_updated", "streaming_conduits", "timed_gathered", "timed_gather_iters",
                 "timed_iters1", "steps_unrolled", "steps_tail", "steps_sparse", "steps_list", "deferred_outfalls",
-                "steps_fused"]
+                "steps_fused", "steps_compact", "compact_grown"]
         return dict(zip(keys, list(a)))
 
     def set_timing(self, on: bool):

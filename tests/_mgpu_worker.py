@@ -8,6 +8,11 @@ Runs the engine on one rank of a partitioned network.  Transport:
 Writes the owned part of the final state to an .npz (and, with
 WORKER_SAVE=1, the binary results file next to it, rank 0 only).
 
+With WORKER_OUT0=<path>, rank 0 writes its binary results there instead
+(e.g. /dev/full: every write fails) and the worker expects an error: it runs
+start / steps / end, writes the error codes each returned (and the message)
+to the .npz and exits 0 when some call failed.
+
 usage: python _mgpu_worker.py INP STEPS OUT.npz TRANSPORT     (env: RANK, WORLD_SIZE, MASTER_*)
 """
 import os
@@ -41,6 +46,20 @@ def main():
         assert world == 1
         s.set_partition(0, 1, s.nccl_unique_id())
     tag = os.path.splitext(out)[0]      # <out>.rpt / <out>.out: one pair per run and rank
+    out0 = os.environ.get("WORKER_OUT0")
+    if out0:                            # an error is expected: report which call failed, on every rank
+        assert s.open(inp, tag + ".rpt", out0 if rank == 0 else tag + ".out") == 0, s.getError()
+        codes = [s.start(True), 0, 0]
+        if codes[0] == 0:
+            codes[1] = s.run_steps(steps)[0]
+            codes[2] = s.end()
+        msg = s.getError()
+        s.close()
+        np.savez(out, codes=np.array(codes), msg=np.frombuffer(str(msg).encode(), dtype=np.uint8))
+        if transport == "host":
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        sys.exit(0 if any(codes) else 3)
     assert s.open(inp, tag + ".rpt", tag + ".out") == 0, s.getError()
     # WORKER_SAVE=1: swmm_start(1), the binary results file (rank 0 writes it)
     assert s.start(os.environ.get("WORKER_SAVE") == "1") == 0, s.getError()

@@ -224,6 +224,16 @@ def make(name):
                 if k in x and x[k].shape == d[k].shape:
                     env_k = np.maximum(env_k, np.abs(d[k].astype(np.float64) - x[k].astype(np.float64)))
                 d["env." + k] = env_k
+        # per recorded step and link: 1 where the FMA or the x87 build's flow
+        # class differs from this build's (the (link, step) pairs where the
+        # reference itself flips a class; the parity test exempts the
+        # class-selected coefficients only there)
+        k = "s.link.flowClass"
+        flip = np.zeros(d[k].shape, dtype=np.uint8)
+        for b in (e, x):
+            n = min(len(b[k]), len(d[k]))
+            flip[:n] |= (b[k][:n] != d[k][:n]).astype(np.uint8)
+        d["env.link.classFlip"] = flip
         d["env.x87.run.counts"] = x["run.counts"]
         d["env.x87.run.massbal"] = x["run.massbal"]
         for k in ("run.counts", "run.massbal"):

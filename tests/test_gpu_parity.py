@@ -20,16 +20,18 @@ exactly those steps.  There the engine must match at 1e-6 up to the first step w
 two reference builds part; afterwards the trajectories (the reference's
 builds' among them) are different solutions of the same discrete decisions
 -- a flow class flips where a node head sits on a conduit's offset crest --
-so every (object, step) value of every state array must stay within ten
-times the largest build-to-build spread of the reference itself after that
-step ("env.*" in the fixture: its plain vs FMA vs x87 builds) plus the
+so every (object, step) value of every state array must stay within twice
+the largest build-to-build spread of the reference itself after that step
+("env.*" in the fixture: its plain vs FMA vs x87 builds) plus the
 tolerance, and the non-convergence count and the continuity error within
-the same ten times the builds' spread;
+the same twice the builds' spread;
 flow classes must agree on >= 99.5 % of (link, step) pairs there.  The
 coefficients a flow class selects (surface areas, dq/dh, Froude number:
-dwflow.c:417-550) jump when the class flips, so at the (link, step) pairs
-whose class differs from the reference's -- at most 0.5 % -- they are exempt
-from the bound; everything else, and every depth, flow and volume, is not.  Elsewhere
+dwflow.c:417-550) jump when the class flips, so at a (link, step) pair whose
+class differs from the reference's they are exempt from the bound -- but
+only where the reference's own FMA or x87 build flips that link's class at
+that step too ("env.link.classFlip"); everything else, and every depth,
+flow and volume, is not.  Elsewhere
 discrete flow classes must agree on >= 99.9 %
 of (link, step) pairs, the Picard non-convergence count must match, and the
 binary .out file must have the reference's exact layout with values within
@@ -44,6 +46,10 @@ import _golden
 import swmm5
 
 RTOL, ATOL = 1e-6, 1e-9
+# ill-conditioned cases: the bound is ENV_K times the reference builds' own
+# spread (DESIGN.md §2 names any case that needs more)
+ENV_K = 2.0
+ENV_K_CASE = {}
 # regulator networks: pumps switch and orifices / weirs carry near-zero flows,
 # where libm ulps leave absolute differences of a few 1e-9 (cfs, ft)
 ATOL_CASE = {"example_regulators_var_qual": 1e-8}
@@ -72,13 +78,22 @@ def _run(name, tmp_path):
     dev = {}
 
     CLASS_DEP = {"link.surfArea1", "link.surfArea2", "link.dqdh", "link.froude"}
+    K = ENV_K_CASE.get(name, ENV_K)
+    flips = {"engine": 0, "exempt": 0}
 
     def check(a, b, key, msg, same_class=None):
         if env and rec >= e0:                       # ill-conditioned: a hard envelope on every value
-            bound = ATOL + RTOL * np.abs(b) + 10.0 * float(d["env." + key][e0:].max())
+            bound = ATOL + RTOL * np.abs(b) + K * float(d["env." + key][e0:].max())
             dev_ = np.abs(a - b) / bound
             if key in CLASS_DEP and same_class is not None:
-                dev_ = np.where(same_class, dev_, 0.0)   # a flipped class selects other coefficients
+                # a flipped class selects other coefficients: exempt where the
+                # reference's own builds flip this link's class at this step
+                ref_flip = d["env.link.classFlip"][rec] != 0
+                exempt = ~same_class & ref_flip
+                if key == "link.dqdh":
+                    flips["engine"] += int((~same_class).sum())
+                    flips["exempt"] += int(exempt.sum())
+                dev_ = np.where(exempt, 0.0, dev_)
             ratio = float(np.max(dev_, initial=0.0))
             dev[key] = max(dev.get(key, 0.0), ratio)
             assert ratio <= 1.0, (msg, ratio, float(d["env." + key][e0:].max()))
@@ -113,8 +128,10 @@ def _run(name, tmp_path):
     c = s.counters()
     assert c["steps"] == int(d["run.counts"][1])        # routing steps (a stride makes several)
     if env:
-        print(name, "envelope use (max |engine - ref| / bound):",
-              ", ".join("%s %.3g" % (k, v) for k, v in sorted(dev.items())))
+        print(name, "envelope use (max |engine - ref| / bound, K = %g):" % K,
+              ", ".join("%s %.3g" % (k, v) for k, v in sorted(dev.items())),
+              "| class flips after the builds part: %d, exempt (the reference builds flip too): %d"
+              % (flips["engine"], flips["exempt"]))
         ref_nc = int(d["run.counts"][0])
         spread_nc = max(abs(int(d[k][0]) - ref_nc) for k in ("env.run.counts", "env.x87.run.counts"))
         assert abs(c["nonconverged"] - ref_nc) <= spread_nc + 1
@@ -124,7 +141,10 @@ def _run(name, tmp_path):
     _, ferr, _ = s.getMassBalErr()
     spread = max(abs(d[k][1] - d["run.massbal"][1]) for k in ("env.run.massbal", "env.x87.run.massbal")) \
         if env else 0.0
-    assert abs(ferr - d["run.massbal"][1]) < 1e-3 + 1e-3 * abs(d["run.massbal"][1]) + 10.0 * spread
+    if env:
+        print(name, "continuity error %.6g, reference %.6g, builds' spread %.3g"
+              % (ferr, d["run.massbal"][1], spread))
+    assert abs(ferr - d["run.massbal"][1]) < 1e-3 + 1e-3 * abs(d["run.massbal"][1]) + K * spread
     s.close()
     assert fc_agree >= (0.995 if env else 0.999) * fc_total, (fc_agree, fc_total)
     return out
@@ -151,13 +171,17 @@ def test_gpu_matches_reference_every_step(name, tmp_path):
     # period timestamps are float64; compare everything as float32 words with tolerance
     if name in _golden.ENVELOPE:
         # up to the first word where the reference's two builds part: 1e-5;
-        # after it: within ten times their largest difference (the state
+        # after it: within K times their largest difference (the state
         # arrays' envelope)
+        K = ENV_K_CASE.get(name, ENV_K)
         e = _out_floats(_golden.fma_out(name)[start:-24])
         spread = np.abs(e.astype(np.float64) - b)
         k = int(np.argmax(spread > 1e-6 + 1e-5 * np.abs(b))) if (spread > 1e-6 + 1e-5 * np.abs(b)).any() \
             else a.size
         np.testing.assert_allclose(a[:k], b[:k], rtol=1e-5, atol=1e-6)
-        assert np.max(np.abs(a[k:].astype(np.float64) - b[k:]), initial=0.0) <= 10.0 * spread.max() + 1e-6
+        tail = np.max(np.abs(a[k:].astype(np.float64) - b[k:]), initial=0.0)
+        print(name, ".out tail: max |engine - ref| %.4g, builds' spread %.4g (use %.3g of K = %g)"
+              % (tail, spread.max(), tail / (spread.max() + 1e-300), K))
+        assert tail <= K * spread.max() + 1e-6
     else:
         np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)

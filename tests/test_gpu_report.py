@@ -36,6 +36,9 @@ SECTIONS = ["Highest Continuity Errors", "Time-Step Critical Elements",
 RANKED = {"Highest Continuity Errors", "Time-Step Critical Elements", "Highest Flow Instability Indexes",
           "Most Frequent Nonconverging Nodes"}
 NUM = re.compile(r"^[-+]?(\d+\.?\d*|\.\d+)(e[-+]?\d+)?%?$", re.I)
+# an ill-conditioned case's printed value may lie this many times the
+# reference builds' own spread outside their range (plus one printed digit)
+RPT_K = 1.0
 
 
 def _sections(text):
@@ -87,7 +90,7 @@ def _tok_equal(a, b):
 
 def _spread_equal(x, y, zs):
     """x within the envelope of the reference builds (y, and the other builds
-    zs: FMA, and x87 where stored) widened by ten times its width on each
+    zs: FMA, and x87 where stored) widened by RPT_K times its width on each
     side, plus one printed digit.  The envelope is anchored on all the builds rather than
     on the plain build alone: a chaotic value such as a node's flow balance
     error in an ill-conditioned case lands anywhere inside the builds' range."""
@@ -102,7 +105,7 @@ def _spread_equal(x, y, zs):
     lo, hi = min([fy] + fz), max([fy] + fz)
     w = hi - lo
     tol = 1.01 * 10.0 ** (-dec) + 1e-12 * max(abs(fx), abs(fy))
-    return lo - 10.0 * w - tol <= fx <= hi + 10.0 * w + tol
+    return lo - RPT_K * w - tol <= fx <= hi + RPT_K * w + tol
 
 
 def _same_layout(a, b):

@@ -279,7 +279,7 @@ def test_partition_keeps_regulator_nodes_on_one_rank(tmp_path):
             assert sum(int(n in set(L["lnode"])) for L in lay) == 1, (world, n)
 
 
-def _run_workers(inp, steps, tmp_path, world, transport, tag, save=False):
+def _run_workers(inp, steps, tmp_path, world, transport, tag, save=False, extra_env=None, timeout=600):
     port = _free_port()
     procs = []
     outs = []
@@ -287,12 +287,19 @@ def _run_workers(inp, steps, tmp_path, world, transport, tag, save=False):
         out = str(tmp_path / ("%s_r%d.npz" % (tag, r)))
         outs.append(out)
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0",
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORKER_SAVE="1" if save else "0")
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORKER_SAVE="1" if save else "0",
+                   **(extra_env or {}))
         procs.append(subprocess.Popen([sys.executable, WORKER, inp, str(steps), out, transport],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
-    for p in procs:
-        o, _ = p.communicate(timeout=600)
-        assert p.returncode == 0, o.decode()[-3000:]
+    try:
+        for p in procs:
+            o, _ = p.communicate(timeout=timeout)
+            assert p.returncode == 0, o.decode()[-3000:]
+    finally:
+        for p in procs:                 # a hung rank must not outlive the test
+            if p.poll() is None:
+                p.kill()
+                p.wait()
     return [dict(np.load(o)) for o in outs]
 
 
@@ -416,6 +423,22 @@ def test_ranks_write_one_gpu_results_and_hotstart(world, pollutants, tmp_path):
         assert not os.path.exists(str(tmp_path / ("many_r%d.out" % r)))
     st, its, nonconv = runs["one"][0][0]["counters"]
     assert nonconv > 0 and its / st > 2.5, (st, its, nonconv)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [30, 6])
+def test_rank0_write_error_stops_every_rank(n, tmp_path):
+    """Rank 0 alone writes the binary results file; when its writes fail
+    (/dev/full: the header at swmm_start on the 30 x 30 grid, a reporting
+    period's record on the 6 x 6 one, whose header fits stdio's buffer) every
+    rank returns an error from the same call instead of going on into a
+    collective rank 0 never reaches (api.cpp syncError)."""
+    inp = _grid(tmp_path, n, n, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.3)
+    parts = _run_workers(inp, 100000, tmp_path, 2, "host", "werr", extra_env={"WORKER_OUT0": "/dev/full"},
+                         timeout=300)
+    codes = [tuple(int(c) for c in p["codes"]) for p in parts]
+    assert codes[0] == codes[1] and any(codes[0]), codes
+    assert {c for c in codes[0] if c} <= {307, 309}, codes
 
 
 @pytest.mark.gpu
