@@ -113,12 +113,19 @@ def pmc_record(workload, backend):
     return _record("pmc_traffic.json", workload, backend)
 
 
+def same_regime(rec_window, window):
+    """A profile record taken over another timed window of the same regime:
+    the same spin-up (the window's surcharge level), any steps / warm-up (the
+    driver runs --steps 20 --warmup 5, the profiles may be longer)"""
+    return rec_window is None or (len(rec_window) == 3 and rec_window[0] == window[0])
+
+
 def timing_record(workload, window, backend):
     """profiles/kernel_timing.json entry (tools/rocprof_summary.py): the
-    in-graph k_link<first> duration over this workload's timed window (the
-    same window only)"""
+    in-graph k_link<first> duration over a timed window of this workload in
+    the same regime (same_regime)"""
     rec = _record("kernel_timing.json", workload, backend)
-    if not rec or rec.get("window") != list(window):
+    if not rec or not same_regime(rec.get("window"), window):
         return None
     return rec
 
@@ -185,6 +192,8 @@ def main():
     ap.add_argument("--rccl-1rank", action="store_true",
                     help="one GPU through the partitioned RCCL code path (captured neighbour send/recv and "
                          "flag all-reduce every Picard iteration): the in-graph cost of the collectives")
+    ap.add_argument("--no-stream", dest="stream", action="store_false",
+                    help="skip the STREAM-triad measurement of the achievable HBM bandwidth")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per link-momentum launch from rocprofv3 PMC (profiles/)")
     args = ap.parse_args()
@@ -305,6 +314,9 @@ def main():
     b2b_us = s.time_kernel(0, args.kernel_reps) if args.kernel_reps > 0 else 0.0
     s.end()
     s.close()
+    # the achievable HBM bandwidth of this GPU: STREAM triad over
+    # three 512 MB fp64 arrays, HIP events, outside any profiler
+    stream = s.stream_triad(64 << 20, 20) if args.stream else None
 
     workload = "%s: manhattan_grid_%dx%d_DYNWAVE_%s_D%gft_q%gcfs_P%d" % (
         args.config, rows, cfg["grid"],
@@ -328,8 +340,9 @@ def main():
     trec = timing_record(workload, [cfg["spinup"], args.warmup, args.steps], backend)
     if trec:                               # the graph launches' own duration (rocprofv3, same window)
         first_us = trec["avg_launch_us"]
-        timing = ("in-graph: rocprofv3 --kernel-trace average of the %d graph launches of %s in this "
-                  "workload's timed window (%s)" % (trec["launches"], trec["kernel"], trec["source"]))
+        timing = ("in-graph: rocprofv3 --kernel-trace average of the %d graph launches of %s in a timed "
+                  "window of this workload (spin-up, warm-up, steps = %s; %s)"
+                  % (trec["launches"], trec["kernel"], trec.get("window"), trec["source"]))
     achieved = first_bytes / (first_us * 1e-6) / 1e9
     it_n = tw["timed_iters1"]               # timed iterations >= 1 (either step graph)
     n0 = kt["link_momentum_first"][0]
@@ -352,13 +365,22 @@ def main():
             step_bytes = rec.get("step_bytes")
             # the PMC pass must have measured this same window (same steps, same
             # regime); otherwise its per-step bytes describe another workload
-            if rec.get("window") not in (None, [cfg["spinup"], args.warmup, args.steps]) or \
+            if not same_regime(rec.get("window"), [cfg["spinup"], args.warmup, args.steps]) or \
                     abs(rec.get("iterations_per_step", 0) - iters / args.steps) > 1e-6:
                 step_bytes = None
     step_s = elapsed / args.steps
     roof = {
         "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
+        # the achievable peak on this box (STREAM triad, best of 20 launches)
+        # and the kernel's fraction of it
+        "peak_measured": None if not stream else round(stream["triad_best_GBs"], 1),
+        "frac_measured": None if not stream else round(achieved / stream["triad_best_GBs"], 4),
+        "stream": None if not stream else {
+            "triad_best_GBs": round(stream["triad_best_GBs"], 1), "triad_avg_GBs": round(stream["triad_avg_GBs"], 1),
+            "copy_best_GBs": round(stream["copy_best_GBs"], 1),
+            "kernel": "a[i] = b[i] + s c[i], fp64, 16-byte lanes, 3 x 512 MB arrays, 8 workgroups per CU "
+                      "(stormwater-management-model_amd/csrc/stream.hip)"},
         "traffic": traffic,
         "traffic_source": traffic_src,
         # whole step: PMC HBM bytes per routing step of the same timed window

@@ -94,6 +94,14 @@ int    DLLEXPORT swmmx_getIterationStats(double *out, int n);
  * (every later swmm_step / swmm_stride returns error 500). */
 int    DLLEXPORT swmmx_timeKernel(int which, int reps, double *avgUs);
 
+/* The achievable HBM bandwidth: a STREAM triad
+ * a[i] = b[i] + s c[i] over three arrays of nDoubles fp64 values (16-byte
+ * lanes, arrays far beyond the MALL), `reps` launches timed with HIP events on
+ * the current device.  out[0] triad GB/s (best launch), out[1] triad GB/s
+ * (average), out[2] copy GB/s (best), out[3] bytes per triad launch.
+ * Returns 0 or a negated HIP error. */
+int    DLLEXPORT swmmx_streamTriad(long nDoubles, int reps, double *out);
+
 /* Name of the compute backend ("hip:gfx950:<device name>" or "none"). */
 int    DLLEXPORT swmmx_getBackend(char *buf, int size);
 

@@ -139,6 +139,10 @@ struct StepCtl {
     unsigned tailBar;             // k_tail's grid-barrier arrivals (zeroed by k_link<first>)
     int tailErr;                  // k_tail gave up waiting at a barrier (never expected)
     int qualPar;                  // quality buffer holding the latest concentrations (Params::nQual)
+    // SKIP_STEADY_STATE (routing.c:383-395): steadyOk -- the previous step's
+    // flow error was within SYS_FLOW_TOL (k_finalize); steadyChanged -- a
+    // lateral or outfall inflow changed by more than LAT_FLOW_TOL (k_steady)
+    int steadyOk, steadyChanged;
     double stepRed[kNumPartials];     // this step's reduced block partials (k_finalize)
     // run statistics (stats.c): report-period step count / span, max system
     // outfall flow, routing time-step statistics (stats_updateTimeStepStats)
@@ -360,7 +364,19 @@ struct Params {
     unsigned* cmStamp;
     int* cmCid;
     double* cOutDepth;
+    int* cCnt;                    // CView::cnt: k_unfreeze zeroes the next gather's counters ([1], [3])
+    // SKIP_STEADY_STATE: a step in steady state routes no flow (routing.c:
+    // 236-244; StepCtl::steadyOk / steadyChanged, stepIsSteady)
+    int skipSteady;
+    double sysFlowTol, latFlowTol;
 };
+// this step is skipped as steady (isInSteadyState, routing.c:383-395): read by
+// the launches of Picard iterations 0 and 1 (the later ones see iteration 1's
+// convergence flag, which a skipped step leaves at 0)
+__device__ __forceinline__ bool stepIsSteady(const Params& p)
+{
+    return p.skipSteady && p.ctl->steadyOk && !p.ctl->steadyChanged;
+}
 
 // ===========================================================================
 //  device helpers
@@ -620,23 +636,52 @@ __device__ __forceinline__ int flowClassOf(const Params& p, int j, const Geom& x
         if (kWT) p.wt.arr[ig] = v_;                      \
     } while (0)
 
-// dwflow.c:57-293 -- one conduit, one Picard iteration.
+// A conduit's inputs of an iteration k >= 1, loaded ahead of the
+// bypass decision (the compact walk: they travel with the slot's own words in
+// one round instead of a dependent round after the filter)
+struct LinkIn {
+    Geom x;
+    double oldFlow, qLast, setting, inv1, inv2, aOld, modLength, len0, roughFactor, beta;
+    int lstate;
+};
+template <bool kFast>
+__device__ __forceinline__ LinkIn loadLinkIn(const Params& p, int j, uint32_t f, const double* ct)
+{
+    LinkIn r;
+    r.x = loadGeom<kFast>(p, j, f, ct);
+    r.oldFlow = p.lOldFlow[j];
+    r.qLast = p.q1[j];
+    r.setting = p.setting[j];
+    r.inv1 = p.inv1[j];
+    r.inv2 = p.inv2[j];
+    r.aOld = p.a2[j];
+    r.modLength = p.modLength[j];
+    r.len0 = p.length[j];
+    r.roughFactor = p.roughFactor[j];
+    r.beta = p.beta[j];
+    r.lstate = p.lstate[j];
+    return r;
+}
+
+// dwflow.c:57-293 -- one conduit, one Picard iteration.  pre: its inputs,
+// already loaded (loadLinkIn; iterations k >= 1 only)
 template <bool kFirst, bool kCold, bool kFast = false, bool kWT = false>
 __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, int2 nn, int steps,
-                                            double dt, const double* ct, double yn1, double yn2, int jg = 0)
+                                            double dt, const double* ct, double yn1, double yn2, int jg = 0,
+                                            const LinkIn* pre = nullptr)
 {
     static_assert(!(kWT && kFirst), "write-through only in iterations k >= 2");
     const double omega = 0.5;
     (void)nn;                     // end-node depths arrive as yn1 / yn2
     const double off1 = kCold ? p.off1[j] : 0.0;     // hot links: both offsets are 0
     const double off2 = kCold ? p.off2[j] : 0.0;
-    Geom x = loadGeom<kFast>(p, j, f, ct);
+    Geom x = pre ? pre->x : loadGeom<kFast>(p, j, f, ct);
     double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
 
     // iteration 0: link_setOldHydState (link.c:564-583), a2 <- a1 (dynwave.c:292)
-    double newFlowPrev = p.lNewFlow[j];
     double oldFlow, oldDepth;
     if (kFirst) {
+        double newFlowPrev = p.lNewFlow[j];
         oldFlow = newFlowPrev;
         oldDepth = p.lNewDepth[j];
         p.lOldFlow[j] = oldFlow;
@@ -645,14 +690,14 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         double a1v = p.a1[j];
         p.a2[j] = a1v;
     } else {
-        oldFlow = p.lOldFlow[j];
+        oldFlow = pre ? pre->oldFlow : p.lOldFlow[j];
     }
-    bool isClosed = (p.setting[j] == 0);
+    bool isClosed = ((pre ? pre->setting : p.setting[j]) == 0);
     double qOld = (barrels == 1.0) ? oldFlow : oldFlow / barrels;   // x / 1 == x
-    double qLast = p.q1[j];
+    double qLast = pre ? pre->qLast : p.q1[j];
     double evapRate = 0.0, seepRate = 0.0;
 
-    double inv1 = p.inv1[j], inv2 = p.inv2[j];
+    double inv1 = pre ? pre->inv1 : p.inv1[j], inv2 = pre ? pre->inv2 : p.inv2[j];
     double z1 = inv1 + off1;
     double z2 = inv2 + off2;
     double h1 = yn1 + inv1;
@@ -667,9 +712,9 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         y1 = gmin(y1, x.yFull);
         y2 = gmin(y2, x.yFull);
     }
-    double aOld = kFirst ? p.a1[j] : p.a2[j];
+    double aOld = kFirst ? p.a1[j] : (pre ? pre->aOld : p.a2[j]);
     aOld = gmax(aOld, 0.0001);
-    double length = p.modLength[j];
+    double length = pre ? pre->modLength : p.modLength[j];
 
     // ---- findSurfArea (dwflow.c:417-550) ----
     int fc;
@@ -747,7 +792,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     double aMid = areaAt<kCold>(x, yMid, wSlot, ct);
     double rMid = hydRadAt<kCold>(x, yMid, ct);
     bool isFull = (y1 >= x.yFull && y2 >= x.yFull);
-    double len0 = p.length[j];
+    double len0 = pre ? pre->len0 : p.length[j];
 
     if (fc == F_DRY || fc == F_UP_DRY || fc == F_DN_DRY || isClosed || aMid <= 0.0001) {
         double a1n = 0.5 * (a1 + a2);
@@ -762,7 +807,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
             SWX_LST(evapLoss, 0.0);
             SWX_LST(seepLoss, 0.0);
         }
-        int old = p.lstate[j];
+        int old = pre ? pre->lstate : p.lstate[j];
         SWX_LST(lstate, (old & ~0xF) | fc);   // fullState / normalFlow / inletControl untouched (dwflow.c:165-180)
         return;
     }
@@ -796,7 +841,8 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     // culverts, offsets) amplify a last-bit difference into a chaotic value
     // -- with the short form example_shapes' final stored volume moved 1.1 %,
     // where all three reference builds agree
-    else dq1 = dt * p.roughFactor[j] / (kFast ? swxPowFriction(rWtd) : pow(rWtd, 1.33333)) * fabs(v);
+    else dq1 = dt * (pre ? pre->roughFactor : p.roughFactor[j]) / (kFast ? swxPowFriction(rWtd) : pow(rWtd, 1.33333)) *
+               fabs(v);
     double dq2 = dt * 32.2 * aWtd * (h2 - h1) / length;
     double dq3 = 0.0, dq4 = 0.0;
     if (sigma > 0.0) {
@@ -848,7 +894,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
                 }
             }
             if (check) {
-                double qNorm = p.beta[j] * a1 * (kFast ? swxPowTwoThirds(r1) : pow(r1, 2. / 3.));
+                double qNorm = (pre ? pre->beta : p.beta[j]) * a1 * (kFast ? swxPowTwoThirds(r1) : pow(r1, 2. / 3.));
                 if (qNorm < q) {
                     normalFlow = 1;
                     q = qNorm;
@@ -895,7 +941,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         SWX_LST(evapLoss, evapRate);
         SWX_LST(seepLoss, seepRate);
     }
-    int old = p.lstate[j];
+    int old = pre ? pre->lstate : p.lstate[j];
     SWX_LST(lstate, (old & (1 << 9)) | fc | (fs << 4) | (normalFlow << 8) | (inletCtl << 10));
 }
 
@@ -1146,6 +1192,7 @@ void k_link(Params p, int k)
 {
     const int tid = blockIdx.x * kBlock + threadIdx.x, nthr = gridDim.x * kBlock;
     const int cnt = (!kFirst && k >= 2) ? p.ucount[k - 1] : 0;   // loads with the flag below
+    if (k < 2 && stepIsSteady(p)) return;            // SKIP_STEADY_STATE: no flow routing this step
     if (k >= 2 && p.unconv[k - 1] == 0) {            // converged: dynwave.c:249-251
         // the first launch after the step converged (iteration k-1 ran)
         if (p.freeze && (k == 2 || p.unconv[k - 2] != 0)) finalizeFrozen(p, k - 1, tid, nthr);
@@ -1301,6 +1348,7 @@ template <bool kFirst, bool kWake = false>
 __global__ __launch_bounds__(kBlock) void k_link_cold(Params p, int k)
 {
     if (k >= 2 && p.unconv[k - 1] == 0) return;
+    if (k < 2 && stepIsSteady(p)) return;            // SKIP_STEADY_STATE
     __shared__ double ct[5 * SWX_CIRC_N];
     stageTables(ct, p.gTables);
     (void)coldConduits<kFirst, kWake>(p, k, p.ctl->dt, ct, blockIdx.x * kBlock + threadIdx.x, gridDim.x * kBlock,
@@ -1357,23 +1405,54 @@ __device__ __forceinline__ bool freezable(const Params& p, double yNew, double y
     return true;
 }
 
+// A node's inputs of an iteration k >= 2, loaded in one round ahead of its
+// update (the compact node pass: no load waits for the flag words)
+struct NodeIn {
+    double y, yRaw, yCrown, yMaxNP, yOld, lat, inflow, outflow, surf, dqdh;
+    double fullDepth, pondedArea, oldNetInflow, surDepth, oldSurfArea, fullVolume, oldVolume;
+};
+__device__ __forceinline__ NodeIn loadNodeIn(const Params& p, int i)
+{
+    NodeIn r;
+    r.y = p.nNewDepth[i];
+    r.yRaw = p.yRaw[i];
+    r.yCrown = p.yCrown[i];
+    r.yMaxNP = p.yMaxNP[i];
+    r.yOld = p.nOldDepth[i];
+    r.lat = p.newLat[i];
+    r.inflow = p.inflow[i];
+    r.outflow = p.outflow[i];
+    r.surf = p.nSurf[i];
+    r.dqdh = p.nDqdh[i];
+    r.fullDepth = p.fullDepth[i];
+    r.pondedArea = p.pondedArea[i];
+    r.oldNetInflow = p.oldNetInflow[i];
+    r.surDepth = p.surDepth[i];
+    r.oldSurfArea = p.oldSurfArea[i];
+    r.fullVolume = p.fullVolume[i];
+    r.oldVolume = p.nOldVolume[i];
+    return r;
+}
+// node i's value of field F: preloaded (nin) or from its array
+#define SWX_NIN(F, arr) (nin ? nin->F : p.arr[i])
+
 // setNodeDepth (dynwave.c:636-762) for node i given its summed inflow,
 // outflow, surface area and dq/dh; returns 1 when converged (dynwave.c:615-621)
 template <bool kStorage = true, bool kWT = false>
 __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_t nf, double dt,
                                           double yLast, double yOld, double inflow, double outflow,
-                                          double surf, double sumdqdh, int ig = 0)
+                                          double surf, double sumdqdh, int ig = 0, const NodeIn* nin = nullptr)
 {
     static_assert(!(kWT && kStorage), "the compact graph has no storage units");
     const double omega = 0.5;
     bool canPond = (nf & NF_CANPOND) != 0;
-    double fullDepth = p.fullDepth[i];
+    double fullDepth = SWX_NIN(fullDepth, fullDepth);
     bool isPonded = (canPond && yLast > fullDepth);
-    double yCrown = p.yCrown[i];
+    double yCrown = SWX_NIN(yCrown, yCrown);
     double overflow = 0.0;
     double surfArea = gmax(surf, p.minSurfArea);
     double dQ = inflow - outflow;
-    double dV = 0.5 * (p.oldNetInflow[i] + dQ) * dt;
+    double dV = 0.5 * (SWX_NIN(oldNetInflow, oldNetInflow) + dQ) * dt;
     const bool isStorage = kStorage && (int)(nf & NF_TYPE) == STORAGE;
     bool isSurcharged = false;
     if (p.surchargeMethod == SUR_EXTRAN) {
@@ -1395,7 +1474,7 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
         double denom = sumdqdh;
         if (yLast < 1.25 * yCrown) {
             double fr = (yLast - yCrown) / yCrown;
-            denom += (p.oldSurfArea[i] / dt - sumdqdh) * exp(-15.0 * fr);
+            denom += (SWX_NIN(oldSurfArea, oldSurfArea) / dt - sumdqdh) * exp(-15.0 * fr);
         }
         if (denom == 0.0) dy = 0.0;
         else dy = corr * dQ / denom;
@@ -1405,8 +1484,8 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
     }
     if (yNew < 0) yNew = 0.0;
     double yMax = fullDepth;
-    if (!canPond) yMax += p.surDepth[i];
-    double fullVolume = p.fullVolume[i];
+    if (!canPond) yMax += SWX_NIN(surDepth, surDepth);
+    double fullVolume = SWX_NIN(fullVolume, fullVolume);
     const bool flooded = yNew > yMax;
     const bool plain = !isSurcharged && !canPond && !flooded && fullVolume == 0.0 && !isStorage;
     if (k >= 1) {                                      // fast-path cache for the next iteration
@@ -1420,7 +1499,7 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
             newVolume = fullVolume;
             yNew = yMax;
         } else {
-            double oldVolume = p.nOldVolume[i];
+            double oldVolume = SWX_NIN(oldVolume, nOldVolume);
             newVolume = gmax((oldVolume + dV), fullVolume);
             overflow = (newVolume - gmax(oldVolume, fullVolume)) / dt;
         }
@@ -1661,7 +1740,8 @@ template <bool kFirst, bool kGeneral, bool kCoh = false, bool kWT = false>
 __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double dt, NodePre pre, bool& listMe,
                                          int2& row, bool& anyUnconv, int& gathered, int& live, int& fast,
                                          bool& alive, int2 rowIn = make_int2(-1, -1),
-                                         const GatherSrc* gsp = nullptr, int ig = 0)
+                                         const GatherSrc* gsp = nullptr, int ig = 0, const NodeIn* nin = nullptr,
+                                         const int* entPre = nullptr)
 {
     constexpr bool kStorage = kGeneral;
     static_assert(!(kWT && (kFirst || kGeneral || kCoh)), "the compact graph: iterations >= 2, no storage units");
@@ -1683,12 +1763,12 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
                 // read); once one is updated it is live again from its
                 // depth at the last iteration
                 if (cache & 1) {
-                    yLast = frozenDepth(p, i, fz, k - 1);
+                    yLast = nin ? frozenDepthV(nin->y, nin->yRaw, fz, k - 1) : frozenDepth(p, i, fz, k - 1);
                     haveYLast = true;
                     SWX_NST(frz, (unsigned char)0);
                 } else {
                     if (k == p.maxTrials - 1) {            // the last possible iteration
-                        SWX_NST(nNewDepth, frozenDepth(p, i, fz, k));
+                        SWX_NST(nNewDepth, nin ? frozenDepthV(nin->y, nin->yRaw, fz, k) : frozenDepth(p, i, fz, k));
                         SWX_NST(frz, (unsigned char)0);
                     }
                     alive = false;
@@ -1697,7 +1777,8 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
             } else if (type != OUTFALL && !(nf & (NF_SHARED | NF_DEFER)) && cache == 2) {
                 // plain clean junction: the relaxation step of setNodeDepth
                 // (dynwave.c:700-715) on the cached unrelaxed depth
-                double yLast2 = p.nNewDepth[i], yCrown = p.yCrown[i], yRaw = p.yRaw[i], yMax = p.yMaxNP[i];
+                double yLast2 = SWX_NIN(y, nNewDepth), yCrown = SWX_NIN(yCrown, yCrown), yRaw = SWX_NIN(yRaw, yRaw),
+                       yMax = SWX_NIN(yMaxNP, yMaxNP);
                 row = (rowIn.x >= 0) ? rowIn : make_int2(p.rowptr[i], p.rowptr[i + 1]);
                 bool sur = p.surchargeMethod == SUR_EXTRAN && yCrown > 0.0 && yLast2 > yCrown;
                 if (!sur) {
@@ -1727,7 +1808,7 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
         // reuse test): one dependent round trip fewer before the gather
         const int e0 = (rowIn.x >= 0) ? rowIn.x : p.rowptr[i], e1 = (rowIn.x >= 0) ? rowIn.y : p.rowptr[i + 1];
         row = make_int2(e0, e1);
-        if (!haveYLast) yLast = (type == OUTFALL) ? 0.0 : p.nNewDepth[i];
+        if (!haveYLast) yLast = (type == OUTFALL) ? 0.0 : SWX_NIN(y, nNewDepth);
         double yOld, lat;
         if (kFirst) {
             // routing.c:328-332, node.c:293-304, 325-341 -- step-begin rotation
@@ -1747,23 +1828,23 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
                 p.nExfilVol[i] = xv;
             }
         } else {
-            yOld = p.nOldDepth[i];
-            lat = p.newLat[i];
+            yOld = SWX_NIN(yOld, nOldDepth);
+            lat = SWX_NIN(lat, newLat);
         }
         double inflow, outflow, surf, sumdqdh;
         const bool reuse = !kFirst && k >= 2 && !(nf & (NF_CANPOND | NF_SHARED | NF_DEFER)) &&
                            type != STORAGE && !(pre.cache & 1);
         if (reuse) {
-            inflow = p.inflow[i];
-            outflow = p.outflow[i];
-            surf = p.nSurf[i];
-            sumdqdh = p.nDqdh[i];
+            inflow = SWX_NIN(inflow, inflow);
+            outflow = SWX_NIN(outflow, outflow);
+            surf = SWX_NIN(surf, nSurf);
+            sumdqdh = SWX_NIN(dqdh, nDqdh);
         } else {
             // initNodeStates (dynwave.c:297-331)
             bool canPond = (nf & NF_CANPOND) != 0;
-            double fullDepth = p.fullDepth[i];
+            double fullDepth = SWX_NIN(fullDepth, fullDepth);
             surf = 0.0;
-            if (canPond && yLast > fullDepth) surf = p.pondedArea[i];
+            if (canPond && yLast > fullDepth) surf = SWX_NIN(pondedArea, pondedArea);
             inflow = 0.0;
             outflow = 0.0;                        // node losses are 0 for non-storage nodes
             if (kStorage && type == STORAGE) {
@@ -1805,7 +1886,8 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
                 double qv[kGather], sav[kGather], dqv[kGather];
                 uint32_t lfv[kGather];
 #pragma unroll
-                for (int t = 0; t < kGather; t++) ent[t] = (eb + t < e1) ? gs.csr[eb + t] : 0;
+                for (int t = 0; t < kGather; t++)
+                    ent[t] = (eb + t < e1) ? (entPre ? entPre[eb - e0 + t] : gs.csr[eb + t]) : 0;
 #pragma unroll
                 for (int t = 0; t < kGather; t++) {
                     if (eb + t < e1) {
@@ -1829,8 +1911,10 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
             }
             SWX_NST(inflow, inflow);
             SWX_NST(outflow, outflow);
-            SWX_NST(nSurf, surf);
-            SWX_NST(nDqdh, sumdqdh);
+            // (the gather-reuse sums are read by the iterations k >= 2 of this
+            // step only: in the compact graph from the compact copy)
+            p.nSurf[i] = surf;
+            p.nDqdh[i] = sumdqdh;
             if (!kFirst && k >= 2) p.dirty[i] = 0;
             gathered++;
         }
@@ -1840,7 +1924,8 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
             // conduit sums written above; k_nc adds the non-conduit links
             // and updates the depth
         } else {
-            const int r = nodeUpdate<kStorage, kWT>(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh, ig);
+            const int r = nodeUpdate<kStorage, kWT>(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh, ig,
+                                                    nin);
             if (!(r & 1)) {
                 anyUnconv = true;
                 listMe = true;
@@ -1909,6 +1994,51 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
     nodePassEnd(p, k, anyUnconv, gathered, live, fast, !kFirst && k >= 2);
 }
 
+// SKIP_STEADY_STATE, a step in steady state: initSystemInflows /
+// addSystemInflows (routing.c:312-333, 358-365) -- the lateral inflows rotate
+// and storage units take their losses at the unchanged depth and volume;
+// nothing else of the node state moves (node_setOldHydState runs in routeFlow)
+template <bool kGeneral>
+__device__ __forceinline__ void steadyNodes(const Params& p, int tid, int nthr)
+{
+    for (int i = tid; i < p.nN; i += nthr) {
+        p.oldLat[i] = p.newLat[i];
+        p.newLat[i] = p.latIn[i];
+        if (kGeneral && (int)(p.nflags[i] & NF_TYPE) == STORAGE) {
+            double ev = 0.0, xv = 0.0;
+            p.nLosses[i] = devStorageLosses(p, i, p.nNewDepth[i], p.nNewVolume[i], p.ctl->dt, &ev, &xv);
+            p.nEvapVol[i] = ev;
+            p.nExfilVol[i] = xv;
+        }
+    }
+}
+
+// SKIP_STEADY_STATE: inflowHasChanged (routing.c:775-808) -- a node's lateral
+// inflow (this step's against the last one), or an outfall's or terminal
+// node's inflow (against the one before the last routed step), changed by
+// more than LAT_FLOW_TOL.  Any such node marks StepCtl::steadyChanged (reset
+// by k_finalize), which with steadyOk decides the step (stepIsSteady).
+__device__ __forceinline__ bool flowChanged(double qOld, double qNew, double tol)
+{
+    double diff;
+    if (fabs(qOld) > 1e-6) diff = (qNew / qOld) - 1.0;            // TINY (consts.h)
+    else if (fabs(qNew) > 1e-6) diff = 1.0;
+    else diff = 0.0;
+    return fabs(diff) > tol;
+}
+__global__ __launch_bounds__(kBlock) void k_steady(Params p)
+{
+    if (!p.ctl->steadyOk) return;                  // the step routes flow anyway
+    bool changed = false;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
+        changed = changed || flowChanged(p.newLat[i], p.latIn[i], p.latFlowTol);
+        const uint32_t nf = p.nflags[i];
+        if ((int)(nf & NF_TYPE) == OUTFALL || (nf & NF_DEG0))
+            changed = changed || flowChanged(p.oldFlowInflow[i], p.inflow[i], p.latFlowTol);
+    }
+    if (__any(changed) && (threadIdx.x & 63) == 0) p.ctl->steadyChanged = 1;
+}
+
 template <bool kFirst, bool kGeneral, bool kProbe = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral ? 3 : 4))) void k_node(Params p, int k)
 {
@@ -1924,6 +2054,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
     const int tidX = (xcdBlock() - (proOnly ? 1 : 0)) * kBlock + (int)threadIdx.x;
     const NodePre pre0 = loadNodePre(p, tidX, kFirst ? 0 : k);
     if (k >= 2 && p.unconv[k - 1] == 0) return;
+    if (k < 2 && stepIsSteady(p)) {
+        // SKIP_STEADY_STATE: no flow routing this step (routing.c:239-241);
+        // what routing_execute still does per node is initSystemInflows /
+        // addSystemInflows' lateral-inflow rotation and node_getLosses
+        // (routing.c:312-333, 358-365), from the unchanged state
+        if (kFirst) steadyNodes<kGeneral>(p, blockIdx.x * kBlock + threadIdx.x, gridDim.x * kBlock);
+        return;
+    }
     probeMark(p, k, PR_N_IN);
     probeMark(p, k, PR_N_LAST_IN);
     // prologue: outfall depths (link_setOutfallDepth, findNodeDepths
@@ -2392,26 +2530,30 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
 
 // ---------------------------------------------------------------------------
 // The compact graph (GM_COMPACT): Picard iterations k >= 2 over contiguous
-// copies of the live sub-network.
+// copies of the live sub-network, each kernel two dependent memory rounds.
 //
 // After iteration 1 almost every junction of a large network is frozen
 // (converged, plain, relaxing toward its cached depth).  The list graph's
 // iterations k >= 2 chase list -> CSR row -> conduit -> end nodes through a
 // dozen scattered SoA arrays: about five dependent memory rounds per launch,
-// each touching one line per array per node.  Here k_cgather copies, once
-// per step, the live nodes L1 of iteration 1 (vlist(1)) and every conduit
-// incident to one of them (E_C) into compact arrays, each node's row as
-// compact conduit ids.  Every iteration k >= 2 is then
-//   k_cwalk(k)  one thread per compact conduit slot: the conduit is updated
-//               unless both ends converged in iteration k-1
-//               (findBypassedLinks, dynwave.c:335-345; an outfall never
-//               converges) -- the slot's words, then both ends' state, then
-//               dwflow_findConduitFlow (the same conduitFlow code);
-//   k_cnode(k)  one thread per compact node: findNodeDepths / setNodeDepth
-//               (dynwave.c:593-762, the same nodeItem code) with the gather
-//               over its compact row, and block 0 the outfall depths
+// each touching one line per array per node.  Here, once per step, the live
+// nodes L1 of iteration 1 (vlist(1)) and the frozen neighbours of its
+// unconverged nodes (the "ring": the junctions iteration 2 wakes) are copied
+// into dense compact node arrays (k_cgather1), and every conduit incident to
+// one of them into dense compact conduit arrays, each node's row as compact
+// conduit ids (k_cgather2).  Every iteration k >= 2 is then
+//   k_cwalk(k)  one thread per compact conduit: its words and every input of
+//               its momentum update in one round (loadLinkIn), both ends'
+//               state in the second; the conduit is updated unless both
+//               ends converged in iteration k-1 (findBypassedLinks,
+//               dynwave.c:335-345; an outfall never converges) by the same
+//               conduitFlow code (dwflow_findConduitFlow);
+//   k_cnode(k)  one thread per compact node: its state and row in one round
+//               (loadNodeIn), its conduits' values in the second, then
+//               findNodeDepths / setNodeDepth (dynwave.c:593-762, the same
+//               nodeItem code); block 0 the outfall depths
 //               (link_setOutfallDepth, link.c:728-766) as k_node does.
-// No lists are built in iterations k >= 2 and no atomics run but for growth.
+// No lists are built in iterations k >= 2.
 //
 // Write-through: every store to a compact copy also goes to the global array
 // (SWX_LST / SWX_NST), so the global arrays hold the canonical state at every
@@ -2420,37 +2562,38 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
 // `dirty` word is read in iterations k >= 2 only, and there only from the
 // compact copy: it is not written through.)
 //
-// Growth.  A node outside the compact set is frozen: L1 holds every node not
-// frozen after iteration 1, and every node that wakes joins.  When an updated
-// conduit has such an end, the walk claims it (CAS of its membership stamp
-// cmStamp to iterStamp(k)) and appends it; k_cnode(k) copies the fresh node,
-// appends its conduits not yet in E_C (CAS of lStamp) and updates it with the
-// gather over its global row (its compact row is never built).  An appended
-// conduit names its ends outside the compact set by ~global id and reads them
-// from the global arrays (canonical: write-through).  Every node k_node(k)
-// would update is therefore in the compact set, every conduit k_link(k) would
-// update is in E_C, each update is the same code on the same operands, and
-// the results are bitwise those of every other graph.
+// Growth.  A node outside the compact set is frozen: the set holds every node
+// not frozen after iteration 1, and every node that wakes joins.  When an
+// updated conduit has such an end, the walk claims it (CAS of its membership
+// stamp cmStamp to iterStamp(k)) and appends it; k_cnode(k) copies the fresh
+// node, appends its conduits not yet in the set (CAS of lStamp) and updates it
+// with the gather over its global row.  An end outside the set at gather time
+// is named by ~global id and read from the global arrays (canonical:
+// write-through).  Every node k_node(k) would update is therefore in the
+// compact set, every conduit k_link(k) would update is in it, each update is
+// the same code on the same operands, and the results are bitwise those of
+// every other graph.
 //
-// Slots.  A conduit of L1 is owned by its lower-numbered end in L1 (or its
-// only end in L1) and sits in slot S c + r, c the owner's compact id and r its
-// position in the owner's row; the other end finds the slot from the owner's
-// compact id and otherPos (its position in the owner's row, static), so
-// k_cgather needs no atomics.  S = the network's largest row (at most
-// kCompactMaxDeg).  Grown conduits take slots past S |L1|.
+// Conduit ids.  A conduit is copied by its lower-numbered end in the set (or
+// its only end in it); k_cgather2 numbers them densely (a workgroup prefix
+// sum, one atomic per workgroup).  A row entry whose conduit the other end
+// copied holds its global id (kUnresolved) until k_cnode resolves it (lCid).
 // Single GPU, no pumps / regulators, no cold conduits, no storage units,
-// freezing on (host-checked: Router::init, compactOk).
+// freezing on, rows of at most kCompactMaxDeg entries (host-checked:
+// Router::init, compactOk).
 constexpr int kCompactMaxDeg = 8;
+constexpr int kUnresolved = 1 << 30;      // row entry: global conduit id, compact id not yet looked up
 struct CView {
-    int S;
     int seep;                    // some conduit has LF_SEEP (its depth, volume and losses are copied)
-    int* cnt;                    // [0] compact nodes, [1] compact conduit slots, [2] nodes grown (run total)
-    unsigned* lStamp;            // per global link: iterStamp of the iteration it joined E_C
-    const int* otherPos;         // per CSR entry: the link's position in its other end's row
-    int *node, *link;            // compact -> global (link -1: an empty slot)
-    int* deg;                    // per compact node: its row length; -1 gathers over the global row; -2 fresh
-    int* csr;                    // [S per node] compact conduit id | (1 << 31: the node is its node2)
-    int2* ends;                  // per slot: its end nodes, compact id (>= 0) or ~global id
+    int* cnt;                    // [0] compact nodes, [1] compact conduits, [2] nodes grown (run total),
+                                 // [3] ring nodes ([1], [3] zeroed by k_unfreeze: Params::cCnt)
+    unsigned* lStamp;            // per global link: iterStamp of the iteration it joined
+    int* lCid;                   // per global link: its compact id (with lStamp)
+    int *node, *link;            // compact -> global
+    int* deg;                    // per compact node: its row length; -1 gathers over its global row; -2 fresh
+    int* csr;                    // [kCompactMaxDeg per node] compact conduit id (or kUnresolved | global
+                                 // id) | (1 << 31: the node is its node2)
+    int2* ends;                  // per compact conduit: its end nodes, compact id (>= 0) or ~global id
     // node copies, by compact id
     uint32_t* nflags;
     unsigned char *dirty, *frz;
@@ -2458,7 +2601,7 @@ struct CView {
     double *nNewDepth, *yRaw, *yCrown, *yMaxNP, *nOldDepth, *newLat, *inflow, *outflow, *nSurf, *nDqdh;
     double *fullDepth, *pondedArea, *oldNetInflow, *surDepth, *oldSurfArea, *fullVolume, *nOldVolume;
     double *nNewVolume, *overflow;                // written only
-    // conduit copies, by slot; optional groups are null when no conduit needs them
+    // conduit copies, by compact id; optional groups are null when no conduit needs them
     uint32_t* lflags;
     int* lstate;
     double *lNewFlow, *lOldFlow, *q1, *setting, *inv1, *inv2, *a2, *modLength, *length, *roughFactor, *beta;
@@ -2518,7 +2661,7 @@ __device__ __forceinline__ void copyNode(const Params& p, const CView& v, int g,
     v.fullDepth[c] = b0; v.pondedArea[c] = b1; v.oldNetInflow[c] = b2; v.surDepth[c] = b3;
     v.oldSurfArea[c] = b4; v.fullVolume[c] = b5; v.nOldVolume[c] = b6;
 }
-// conduit l's state into compact slot m
+// conduit l's state into compact conduit m
 __device__ __forceinline__ void copyLink(const Params& p, const CView& v, int l, int m)
 {
     const uint32_t f = p.lflags[l];
@@ -2544,92 +2687,136 @@ __device__ __forceinline__ void copyLink(const Params& p, const CView& v, int l,
     }
 }
 
-// After k_node(1) of a compact step: L1 (vlist(1), whose entries k_node(1)
-// stamped with their list position = compact id) and the conduits it owns
-// (see "Slots") into the compact arrays.  One thread per L1 node; its row's
-// words, then the other ends' membership, then the copies.
-__global__ __launch_bounds__(kBlock) void k_cgather(Params p, CView v)
+// After k_node(1) of a compact step.  Threads [0, vc): the live nodes L1
+// (vlist(1); k_node(1) stamped them with their list position = compact id)
+// copied into the compact node arrays.  Threads [vc, vc + 4 uc): four per
+// unconverged node of iteration 1 (ulist(1)) over its row: a frozen neighbour
+// is claimed (CAS of its stamp) and appended after L1 (the ring; one atomic
+// per wave on cnt[3]).
+__global__ __launch_bounds__(kBlock) void k_cgather1(Params p, CView v)
 {
-    const int vc = p.vcount[1];
+    const int vc = p.vcount[1], uc = p.ucount[1];
     if (p.unconv[1] == 0) return;                 // converged at iteration 1: no iteration k >= 2 runs
-    const int S = v.S;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        v.cnt[0] = vc;
-        v.cnt[1] = S * vc;
-    }
     const unsigned s1 = iterStamp(p, 1);
     const int* vl = p.vlist + p.nN;
-    const int2* vr = p.vlistRow + p.nN;
-    for (int t = blockIdx.x * kBlock + threadIdx.x; t < vc; t += gridDim.x * kBlock) {
-        const int g = vl[t];
-        const int2 rb = vr[t];
-        int ent[kCompactMaxDeg], o[kCompactMaxDeg], op[kCompactMaxDeg];
-#pragma unroll
-        for (int r = 0; r < kCompactMaxDeg; r++) {
-            const bool in = r < S && rb.x + r < rb.y;
-            ent[r] = in ? p.csr[rb.x + r] : 0;
-            o[r] = in ? p.csrOther[rb.x + r] : -1;
-            op[r] = in ? v.otherPos[rb.x + r] : 0;
+    const int* ul = p.ulist + p.nN;
+    const int2* ur = p.ulistRow + p.nN;
+    const int items = vc + 4 * uc;
+    for (int t0 = blockIdx.x * kBlock; t0 < items; t0 += gridDim.x * kBlock) {   // (uniform per wave)
+        const int t = t0 + (int)threadIdx.x;
+        if (t < vc) {
+            const int g = vl[t];
+            copyNode(p, v, g, t);
+            v.node[t] = g;
         }
-        copyNode(p, v, g, t);
-        v.node[t] = g;
-        v.deg[t] = rb.y - rb.x;
+        const int s = t - vc;
+        int2 rb = make_int2(0, 0);
+        if (s >= 0 && t < items) rb = ur[s >> 2];
+        (void)ul;
+        for (int e0 = rb.x + (s & 3); __any(s >= 0 && t < items && e0 < rb.y); e0 += 4) {
+            const bool in = s >= 0 && t < items && e0 < rb.y;
+            int o = -1;
+            bool mine = false;
+            if (in) {
+                o = p.csrOther[e0];
+                const unsigned st = p.cmStamp[o];
+                mine = st != s1 && atomicCAS(&p.cmStamp[o], st, s1) == st;
+            }
+            const unsigned long long m = __ballot(mine);
+            if (m) {
+                const int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1;
+                int base = 0;
+                if (lane == leader) base = atomicAdd(&v.cnt[3], __popcll(m));
+                base = __shfl(base, leader, 64);
+                if (mine) {
+                    const int c = vc + base + __popcll(m & ((1ull << lane) - 1ull));
+                    p.cmCid[o] = c;
+                    v.node[c] = o;
+                    copyNode(p, v, o, c);
+                }
+            }
+        }
+    }
+}
+
+// One thread per compact node of k_cgather1: the conduits of its row that it
+// copies (see "Conduit ids"), numbered densely, and its row as compact ids.
+__global__ __launch_bounds__(kBlock) void k_cgather2(Params p, CView v)
+{
+    const int vc = p.vcount[1], ring = v.cnt[3];
+    if (p.unconv[1] == 0) return;
+    const int nm = vc + ring;
+    if (blockIdx.x == 0 && threadIdx.x == 0) v.cnt[0] = nm;
+    const unsigned s1 = iterStamp(p, 1);
+    __shared__ int wsum[kBlock / 64];
+    __shared__ int sBase;
+    for (int c0 = blockIdx.x * kBlock; c0 < nm; c0 += gridDim.x * kBlock) {      // uniform per workgroup
+        const int c = c0 + (int)threadIdx.x;
+        const bool in = c < nm;
+        int g = 0, e0 = 0, deg = 0;
+        if (in) {
+            g = v.node[c];
+            e0 = p.rowptr[g];
+            deg = p.rowptr[g + 1] - e0;
+        }
+        int ent[kCompactMaxDeg], o[kCompactMaxDeg];
         unsigned ost[kCompactMaxDeg];
         int oc[kCompactMaxDeg];
+#pragma unroll
+        for (int r = 0; r < kCompactMaxDeg; r++) {
+            ent[r] = (r < deg) ? p.csr[e0 + r] : 0;
+            o[r] = (r < deg) ? p.csrOther[e0 + r] : -1;
+        }
 #pragma unroll
         for (int r = 0; r < kCompactMaxDeg; r++) {
             ost[r] = (o[r] >= 0) ? p.cmStamp[o[r]] : 0u;
             oc[r] = (o[r] >= 0) ? p.cmCid[o[r]] : 0;
         }
+        unsigned own = 0;
+#pragma unroll
+        for (int r = 0; r < kCompactMaxDeg; r++)
+            if (o[r] >= 0 && (ost[r] != s1 || g < o[r])) own |= 1u << r;
+        // workgroup exclusive prefix sum of the owned counts -> dense ids
+        const int mineN = __popc(own);
+        int incl = mineN;
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int tot = 0;
+            for (int q = 0; q < kBlock / 64; q++) tot += wsum[q];
+            sBase = tot ? atomicAdd(&v.cnt[1], tot) : 0;
+        }
+        __syncthreads();
+        int before = sBase;
+        for (int q = 0; q < w; q++) before += wsum[q];
+        int id = before + incl - mineN;
+        __syncthreads();                          // (wsum / sBase reused by the next round)
 #pragma unroll
         for (int r = 0; r < kCompactMaxDeg; r++) {
-            if (r >= S) break;
-            const int s = S * t + r;
-            int lnk = -1;
-            if (o[r] >= 0) {
-                const int l = ent[r] & 0x7FFFFFFF;
-                const bool oIn = ost[r] == s1;
-                const bool mine = !oIn || g < o[r];
-                if (mine) {
-                    lnk = l;
-                    copyLink(p, v, l, s);
-                    const int oe = oIn ? oc[r] : ~o[r];
-                    v.ends[s] = (ent[r] < 0) ? make_int2(oe, t) : make_int2(t, oe);
-                    v.lStamp[l] = s1;
-                }
-                v.csr[s] = (mine ? s : S * oc[r] + op[r]) | (ent[r] & (int)0x80000000);
+            if (r >= deg) break;
+            const int l = ent[r] & 0x7FFFFFFF, n2 = ent[r] & (int)0x80000000;
+            if ((own >> r) & 1u) {
+                const int oe = (ost[r] == s1) ? oc[r] : ~o[r];
+                copyLink(p, v, l, id);
+                v.link[id] = l;
+                v.ends[id] = n2 ? make_int2(oe, c) : make_int2(c, oe);
+                v.lStamp[l] = s1;
+                v.lCid[l] = id;
+                v.csr[kCompactMaxDeg * c + r] = id | n2;
+                id++;
+            } else {
+                v.csr[kCompactMaxDeg * c + r] = kUnresolved | l | n2;
             }
-            v.link[s] = lnk;
         }
+        if (in) v.deg[c] = deg;
     }
 }
 
-// an end node's state as the walk reads it: a compact node's copy, or (~g)
-// the global arrays and g's membership stamp
-struct CEnd {
-    double y, yr;
-    int fz, conv;
-    unsigned st;
-};
-__device__ __forceinline__ CEnd cEnd(const Params& p, const CView& v, int e)
-{
-    CEnd r;
-    if (e >= 0) {
-        r.y = v.nNewDepth[e];
-        r.yr = v.yRaw[e];
-        r.fz = v.frz[e];
-        r.conv = v.conv[e];
-        r.st = 0u;
-    } else {
-        const int g = ~e;
-        r.y = p.nNewDepth[g];
-        r.yr = p.yRaw[g];
-        r.fz = p.frz[g];
-        r.conv = p.conv[g];
-        r.st = p.cmStamp[g];
-    }
-    return r;
-}
 // an end of a conduit updated in iteration k: its sums are stale (dirty); an
 // end outside the compact set (frozen) is woken: claimed and appended
 __device__ __forceinline__ void cWake(const Params& p, const CView& v, int e, unsigned st, unsigned s1, unsigned sK)
@@ -2658,7 +2845,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kLinkWav
 {
     const int n = v.cnt[1];                       // loads with the flag below
     if (p.unconv[k - 1] == 0) return;             // converged: dynwave.c:249-251
-    if (blockIdx.x * kBlock >= n) return;         // a workgroup with no first-round slot has none (uniform)
+    if (blockIdx.x * kBlock >= n) return;         // a workgroup with no first-round conduit has none (uniform)
     probeMark(p, k, PR_L_IN);
     const int tid = blockIdx.x * kBlock + threadIdx.x, nthr = gridDim.x * kBlock;
     __shared__ double ct[kFast ? kCtFast : 5 * SWX_CIRC_N];
@@ -2669,18 +2856,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kLinkWav
     const unsigned s1 = iterStamp(p, 1), sK = iterStamp(p, k);
     int work = 0;
     for (int m = tid; m < n; m += nthr) {
+        // round 1: the conduit's words and every input of its update
         const int l = v.link[m];
         const uint32_t f = v.lflags[m];
         const int2 en = v.ends[m];
-        if (l < 0) continue;                      // an empty slot
-        const CEnd a = cEnd(p, v, en.x), b = cEnd(p, v, en.y);
-        const bool listed1 = (f & LF_N1_OUTFALL) || !a.conv, listed2 = (f & LF_N2_OUTFALL) || !b.conv;
+        const LinkIn in = loadLinkIn<kFast>(pc, m, f, ct);
+        // round 2: both ends' state (compact copy, or the global arrays for an
+        // end outside the set: one load each through a selected base)
+        const bool r1 = en.x >= 0, r2 = en.y >= 0;
+        const int i1 = r1 ? en.x : ~en.x, i2 = r2 ? en.y : ~en.y;
+        const double d1 = (r1 ? v.nNewDepth : p.nNewDepth)[i1], d2 = (r2 ? v.nNewDepth : p.nNewDepth)[i2];
+        const double y1r = (r1 ? v.yRaw : p.yRaw)[i1], y2r = (r2 ? v.yRaw : p.yRaw)[i2];
+        const int f1 = (r1 ? v.frz : p.frz)[i1], f2 = (r2 ? v.frz : p.frz)[i2];
+        const int c1 = (r1 ? v.conv : p.conv)[i1], c2 = (r2 ? v.conv : p.conv)[i2];
+        const unsigned st1 = r1 ? 0u : p.cmStamp[i1], st2 = r2 ? 0u : p.cmStamp[i2];
+        const bool listed1 = (f & LF_N1_OUTFALL) || !c1, listed2 = (f & LF_N2_OUTFALL) || !c2;
         if (!listed1 && !listed2) continue;       // both ends converged: bypassed
-        const double y1 = frozenDepthV(a.y, a.yr, a.fz, k - 1);
-        const double y2 = frozenDepthV(b.y, b.yr, b.fz, k - 1);
-        conduitFlow<false, false, kFast, true>(pc, m, f, make_int2(0, 0), k, dt, ct, y1, y2, l);
-        cWake(p, v, en.x, a.st, s1, sK);
-        cWake(p, v, en.y, b.st, s1, sK);
+        const double y1 = frozenDepthV(d1, y1r, f1, k - 1);
+        const double y2 = frozenDepthV(d2, y2r, f2, k - 1);
+        conduitFlow<false, false, kFast, true>(pc, m, f, make_int2(0, 0), k, dt, ct, y1, y2, l, &in);
+        cWake(p, v, en.x, st1, s1, sK);
+        cWake(p, v, en.y, st2, s1, sK);
         work++;
     }
     probeMark(p, k, PR_L_WORK);
@@ -2692,8 +2888,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kLinkWav
 }
 
 // a fresh node (woken by the walk of this iteration): its copy, then its
-// conduits not yet in E_C (each appended by one of its fresh ends); returns
-// its flag words for the update
+// conduits not yet in the set (each appended by one of its fresh ends);
+// returns its flag words for the update
 __device__ __forceinline__ NodePre cFresh(const Params& p, const CView& v, int g, int c, unsigned s1, unsigned sK)
 {
     copyNode(p, v, g, c);
@@ -2703,18 +2899,23 @@ __device__ __forceinline__ NodePre cFresh(const Params& p, const CView& v, int g
     for (int e = e0; e < e1; e++) {
         const int ent = p.csr[e], l = ent & 0x7FFFFFFF;
         const unsigned ls = v.lStamp[l];
-        if (ls >= s1) continue;                   // in E_C already (or appended in this launch)
+        if (ls >= s1) continue;                   // in the set already (or appended in this launch)
         if (atomicCAS(&v.lStamp[l], ls, sK) != ls) continue;
         const int m = atomicAdd(&v.cnt[1], 1);
         copyLink(p, v, l, m);
         v.link[m] = l;
+        v.lCid[l] = m;
         const int oe = ~p.csrOther[e];
         v.ends[m] = (ent < 0) ? make_int2(oe, c) : make_int2(c, oe);
     }
     return NodePre{p.nflags[g], 1, p.frz[g]};
 }
 
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_cnode(Params p, CView v, int k)
+#ifndef SWX_CNODE_WAVES
+#define SWX_CNODE_WAVES 3
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SWX_CNODE_WAVES))) void k_cnode(Params p, CView v,
+                                                                                                      int k)
 {
     const int n = v.cnt[0];                       // loads with the flag below
     if (p.unconv[k - 1] == 0) return;
@@ -2744,19 +2945,42 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     bool anyUnconv = false;
     int gathered = 0, live = 0, fast = 0;
     for (int c = b * kBlock + (int)threadIdx.x; c < n; c += nt) {
+        // round 1: the node's words, state and row
         int deg = v.deg[c];
         const int g = v.node[c];
         NodePre pre{v.nflags[c], v.dirty[c], v.frz[c]};
-        if (deg == -2) {
-            pre = cFresh(p, v, g, c, s1, sK);
-            deg = -1;
+        const NodeIn nin = loadNodeIn(pc, c);
+        int ent[kCompactMaxDeg];
+        {
+            const int4 a = *reinterpret_cast<const int4*>(v.csr + (size_t)kCompactMaxDeg * c);
+            ent[0] = a.x; ent[1] = a.y; ent[2] = a.z; ent[3] = a.w;
+            if (deg > 4) {
+                const int4 q = *reinterpret_cast<const int4*>(v.csr + (size_t)kCompactMaxDeg * c + 4);
+                ent[4] = q.x; ent[5] = q.y; ent[6] = q.z; ent[7] = q.w;
+            } else {
+                ent[4] = ent[5] = ent[6] = ent[7] = 0;
+            }
         }
-        const bool own = deg >= 0;
-        const int2 rowIn = own ? make_int2(v.S * c, v.S * c + deg) : make_int2(p.rowptr[g], p.rowptr[g + 1]);
         bool listMe = false, alive = true;
         int2 row = make_int2(0, 0);
-        nodeItem<false, false, false, true>(pc, k, c, dt, pre, listMe, row, anyUnconv, gathered, live, fast, alive,
-                                            rowIn, own ? &gc : &gg, g);
+        if (deg >= 0) {
+            // row entries whose conduit the other end copied: their compact ids
+#pragma unroll
+            for (int r = 0; r < kCompactMaxDeg; r++)
+                if (r < deg && (ent[r] & kUnresolved)) {
+                    const int n2 = ent[r] & (int)0x80000000;
+                    ent[r] = v.lCid[ent[r] & (kUnresolved - 1)] | n2;
+                    v.csr[(size_t)kCompactMaxDeg * c + r] = ent[r];
+                }
+            // round 2 (in nodeItem's gather): the conduits' compact values
+            nodeItem<false, false, false, true>(pc, k, c, dt, pre, listMe, row, anyUnconv, gathered, live, fast,
+                                                alive, make_int2(0, deg), &gc, g, &nin, ent);
+        } else {
+            // grown: the gather over its global row (a fresh node copied first)
+            if (deg == -2) pre = cFresh(p, v, g, c, s1, sK);
+            nodeItem<false, false, false, true>(pc, k, c, dt, pre, listMe, row, anyUnconv, gathered, live, fast,
+                                                alive, make_int2(p.rowptr[g], p.rowptr[g + 1]), &gg, g);
+        }
     }
     nodePassEnd(p, k, anyUnconv, gathered, live, fast, true);
     probeMark(p, k, PR_N_OUT);
@@ -3042,6 +3266,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
 // graph), from the iteration count the convergence flags give
 __global__ __launch_bounds__(kBlock) void k_unfreeze(Params p)
 {
+    if (p.cCnt && blockIdx.x == 0 && threadIdx.x == 0) {     // a compact step: the next one's gather counters
+        p.cCnt[1] = 0;
+        p.cCnt[3] = 0;
+    }
     if (!p.freeze) return;
     bool converged;
     const int m = stepIterations(p, &converged) - 1;
@@ -3146,6 +3374,7 @@ template <bool kFirst>
 __global__ __launch_bounds__(kBlock) void k_nc(Params p, int k)
 {
     if (k >= 2 && p.unconv[k - 1] == 0) return;
+    if (k < 2 && stepIsSteady(p)) return;            // SKIP_STEADY_STATE
     __shared__ double ct[5 * SWX_CIRC_N];
     __shared__ int anyU;
     stageTables(ct, p.gTables);
@@ -3589,6 +3818,9 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
     bool converged;
     [[maybe_unused]] const int steps = stepIterations(p, &converged);
     const StatsDev& S = p.st;
+    // a step skipped as steady: findLimitedLinks and setNodeDepth's dYdT
+    // belong to dynwave_execute, which did not run (routing.c:239-241)
+    const bool steady = stepIsSteady(p);
     int n = gridDim.x * kBlock;
     int tid = blockIdx.x * kBlock + threadIdx.x;
     // the live count after iteration 1 (blockLive, k_node(1)); 0 when the
@@ -3654,8 +3886,8 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
             continue;
         }
         double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
-        const int skip = p.endSkip;
-        int s = p.lstate[j] & ~(1 << 9);
+        const int skip = p.endSkip | (steady ? 64 : 0);
+        int s = steady ? p.lstate[j] : (p.lstate[j] & ~(1 << 9));
         double a1 = p.a1[j];
         if (!(skip & 64) && a1 >= p.aFull[j]) {
             int2 nn = p.lnodes[j];
@@ -3741,7 +3973,7 @@ __global__ __launch_bounds__(kBlock) void k_step_end(Params p)
             acc[2] += -q;
         }
         const double newDepth = p.nNewDepth[i];
-        if (type != OUTFALL)              // setNodeDepth's last dYdT (dynwave.c:750)
+        if (type != OUTFALL && !steady)   // setNodeDepth's last dYdT (dynwave.c:750)
             p.dYdT[i] = fabs(newDepth - p.nOldDepth[i]) / dt;
         if (p.varStep && type != OUTFALL) {
             double y = newDepth;
@@ -3889,11 +4121,14 @@ __global__ void k_finalize(Params p)
     if (t == 0 && kPhase != 1) {
     double tot[kNumPartials];
     for (int q = 0; q < kNumPartials; q++) tot[q] = c->stepRed[q];
-    c->lastSteps = steps;
+    // a step skipped as steady ran no Picard iteration (routing.c:239-244)
+    const bool steady = p.skipSteady && c->steadyOk && !c->steadyChanged;
+    const int ran = steady ? 0 : steps;
+    c->lastSteps = ran;
     c->totalSteps += 1;
     if (p.P > 0) c->qualPar ^= 1;                      // this step's concentrations become the latest
-    c->totalIters += steps;
-    if (!converged) c->nonConverge += 1;
+    c->totalIters += ran;
+    if (!converged && !steady) c->nonConverge += 1;
     // mass balance: massbal_updateRoutingTotals(dt/2) at both ends of the step
     double half = c->dt / 2.;
     double step[kNumPartials] = {c->latTot[0], c->latTot[1] + tot[2], tot[1], c->latTot[2] + tot[0],
@@ -3902,6 +4137,19 @@ __global__ void k_finalize(Params p)
         c->flowTot[q] += c->prevStepTot[q] * half;
         c->flowTot[q] += step[q] * half;
         c->prevStepTot[q] = step[q];
+    }
+    // SKIP_STEADY_STATE: the next step may be steady when this step's flow
+    // error (massbal_getStepFlowError, massbal.c:995-1017) is within
+    // SYS_FLOW_TOL (isInSteadyState, routing.c:383-395; the next step's
+    // OldRoutingTime is past 0); k_steady then checks the inflows
+    if (p.skipSteady) {
+        const double in = step[0] + step[1], out = step[2] + step[3] + step[4] + step[5];
+        double err;
+        if (fabs(in) > 0.0) err = 1.0 - out / in;
+        else if (fabs(out) > 0.0) err = in / out - 1.0;
+        else err = 0.0;
+        c->steadyOk = fabs(err) <= p.sysFlowTol ? 1 : 0;
+        c->steadyChanged = 0;
     }
     // run statistics of this step (routing.c:255-260): stats_updateFlowStats'
     // system part and stats_updateTimeStepStats (stats.c:449-518)
@@ -3914,15 +4162,19 @@ __global__ void k_finalize(Params p)
             c->routingTimeSpan += dt;
             c->maxOutfallFlow = gmax(c->maxOutfallFlow, tot[7]);
         }
-        if (c->newRoutingTime > 0) {
-            c->tsMin = gmin(c->tsMin, dt);
-            for (int j = 1; j < kTimeLevels; j++)
-                if (dt >= c->tsIntervals[j]) { c->tsCounts[j] += 1; break; }
+        if (steady) {
+            c->tsSteadyTime += dt;
+        } else {
+            if (c->newRoutingTime > 0) {
+                c->tsMin = gmin(c->tsMin, dt);
+                for (int j = 1; j < kTimeLevels; j++)
+                    if (dt >= c->tsIntervals[j]) { c->tsCounts[j] += 1; break; }
+            }
+            c->tsMax = gmax(c->tsMax, dt);
+            c->tsRoutingTime += dt;
+            c->tsCount += 1;
+            c->tsTrials += steps;
         }
-        c->tsMax = gmax(c->tsMax, dt);
-        c->tsRoutingTime += dt;
-        c->tsCount += 1;
-        c->tsTrials += steps;
     }
     // advance the clock (routing.c:301-302)
     c->newRoutingTime = c->newRoutingTime + 1000.0 * c->dt;
@@ -3950,7 +4202,7 @@ __global__ void k_finalize(Params p)
     // next step's dt straight into host memory: the host clock advances
     // without a copy command in the step (totalSteps = index of that step)
     p.hostDt[c->totalSteps % kDtRing] = dtn;
-    p.hostDt[kDtRing + (c->totalSteps - 1) % kDtRing] = (double)steps;   // Picard iterations of this step
+    p.hostDt[kDtRing + (c->totalSteps - 1) % kDtRing] = (double)ran;     // Picard iterations of this step
     // nodes not frozen after iteration 1 (the sparse tail's live list): the
     // host's graph choice for the next steps
     p.hostDt[2 * kDtRing + 1 + (c->totalSteps - 1) % kDtRing] = tot[10];
@@ -4131,15 +4383,15 @@ struct Router::Impl {
     unsigned* convW = nullptr;       // Params::convW while a fused step is launched
     double listMax = 200000.0;       // auto: the list graph while the live lists average at most this
     // iterations k >= 2 over the compact copies of the live sub-network
-    // (k_cgather, then k_cwalk / k_cnode per iteration): compactOk when the
-    // network qualifies (SWMM5_SPARSE = 5: always; SWMM5_COMPACT = 0: never in
-    // the auto choice, where it takes the list graph's place)
+    // (k_cgather1/2, then k_cwalk / k_cnode per iteration): compactOk when the
+    // network qualifies and it was asked for (SWMM5_SPARSE = 5: always;
+    // SWMM5_COMPACT = 1: in the auto choice, in the list graph's place)
     hipGraphExec_t graphCompact = nullptr;
     bool compactOk = false, compactAuto = true;
     CView cv{};
     unsigned* cmStamp = nullptr;
     int* cmCid = nullptr;
-    int gridCWalk = 1, gridCNode = 1, gridCGather = 1;
+    int gridCWalk = 1, gridCNode = 1, gridCGather = 1, gridCGather2 = 1;
     bool useGraph = true;
     bool timing = false;
     int gridL = 1, gridN = 1, gridEnd = 1, gridC = 1;
@@ -4508,11 +4760,13 @@ static int launchStep(Router::Impl* d, int mode = GM_UNROLLED)
     p.cmStamp = compact ? d->cmStamp : nullptr;
     p.cmCid = compact ? d->cmCid : nullptr;
     p.cOutDepth = compact ? d->cv.nNewDepth : nullptr;
+    p.cCnt = compact ? d->cv.cnt : nullptr;
     const int r = launchStepImpl(d, mode);
     p.convW = nullptr;
     p.cmStamp = nullptr;
     p.cmCid = nullptr;
     p.cOutDepth = nullptr;
+    p.cCnt = nullptr;
     p.deferPro = defer;
     return r;
 }
@@ -4522,6 +4776,8 @@ static int launchStepImpl(Router::Impl* d, int mode)
     // k_node(1) lists the live nodes only for the list-driven graphs
     p.buildVlist = (mode == GM_SPARSE || mode == GM_LIST || mode == GM_FUSED || mode == GM_COMPACT) ? 1 : 0;
     const bool multi = d->part.active();
+    if (p.skipSteady)                              // SKIP_STEADY_STATE: this step's inflow test
+        hipLaunchKernelGGL(k_steady, dim3(d->gridN), dim3(kBlock), 0, d->stream, p);
     const int base = 4 * p.maxTrials;
     hipEvent_t* ev = d->timing ? d->curEv : nullptr;
     if (mode == GM_TAIL) {
@@ -4568,7 +4824,8 @@ static int launchStepImpl(Router::Impl* d, int mode)
         for (int k = 0; k < 2; k++)
             if (int r = launchIteration(d, k)) return r;
         // (timing: the gather is counted with iteration 2's walk)
-        launchTimed(d, k_cgather, dim3(d->gridCGather), ev ? ev[8] : nullptr, (hipEvent_t) nullptr, p, d->cv);
+        launchTimed(d, k_cgather1, dim3(d->gridCGather), ev ? ev[8] : nullptr, (hipEvent_t) nullptr, p, d->cv);
+        launchTimed(d, k_cgather2, dim3(d->gridCGather2), (hipEvent_t) nullptr, (hipEvent_t) nullptr, p, d->cv);
         for (int k = 2; k < p.maxTrials; k++) {
             launchTimed(d, d->fastLinks ? k_cwalk<true> : k_cwalk<false>, dim3(d->gridCWalk),
                         (ev && k > 2) ? ev[4 * k] : nullptr, d->timing ? d->curHot[k] : nullptr, p, d->cv, k);
@@ -4688,6 +4945,16 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     p.minRouteStep = prj.opt.minRouteStep;
     p.routeStep = prj.opt.routeStep;
     p.varStep = (prj.opt.courantFactor != 0.0 && prj.opt.routeStep >= 0.001) ? 1 : 0;
+    // SKIP_STEADY_STATE (routing.c:236-244, 383-395): single GPU (the inflow
+    // test and the flow error would need exchanges between the ranks)
+    p.skipSteady = prj.opt.skipSteadyState ? 1 : 0;
+    p.sysFlowTol = prj.opt.sysFlowTol;
+    p.latFlowTol = prj.opt.latFlowTol;
+    if (p.skipSteady && partIn && partIn->active()) {
+        err_ = 200;
+        errMsg_ = "ERROR 200: SKIP_STEADY_STATE is not supported with several GPUs";
+        return err_;
+    }
 
     hipError_t e;
     auto upD = [&](const std::vector<double>& v, size_t n) -> double* {
@@ -5625,16 +5892,18 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     // of at most kCompactMaxDeg entries (the slots) and no conduit from a node
     // to itself (maxRowDeg is huge then)
     {
+        // built on request only (SWMM5_SPARSE=5, or SWMM5_COMPACT=1 for the
+        // auto choice): measured slower than the list graph on the surcharged
+        // 1M grid (0.538 against 0.448 ms/step; DESIGN §4 "Round 5")
         const char* cm = getenv("SWMM5_COMPACT");
-        d->compactAuto = !(cm && atoi(cm) == 0);
+        d->compactAuto = cm && atoi(cm) != 0;
         const bool asked = d->sparseMode == 5 || d->compactAuto;
         d->compactOk = asked && d->sparseOk && p.freeze && p.nCold == 0 && !d->general && maxRowDeg >= 1 &&
                        maxRowDeg <= kCompactMaxDeg;
     }
     if (d->compactOk) {
         CView& v = d->cv;
-        const int S = maxRowDeg;
-        const size_t capN = std::max<size_t>(nN, 1), capL = (size_t)S * nN + (size_t)nL + 1;
+        const size_t capN = std::max<size_t>(nN, 1), capL = (size_t)nL + 1;
         bool losses = false, qlim = false, seep = false;
         for (int j = 0; j < nOwn; j++) {
             const uint32_t f = (uint32_t)lflags[j];
@@ -5642,23 +5911,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
             qlim = qlim || (f & LF_QLIMIT);
             seep = seep || (f & LF_SEEP);
         }
-        v.S = S;
         v.seep = seep ? 1 : 0;
-        // per CSR entry: the link's position in its other end's row
-        std::vector<int> pos1(nL, 0), pos2(nL, 0), other((size_t)d->nE, 0);
-        for (int i = 0; i < nN; i++)
-            for (int e2 = rowptr[i]; e2 < rowptr[i + 1]; e2++) {
-                const int l = csr[e2] & 0x7FFFFFFF;
-                (csr[e2] < 0 ? pos2 : pos1)[l] = e2 - rowptr[i];
-            }
-        for (int i = 0; i < nN; i++)
-            for (int e2 = rowptr[i]; e2 < rowptr[i + 1]; e2++) {
-                const int l = csr[e2] & 0x7FFFFFFF;
-                other[e2] = (csr[e2] < 0) ? pos1[l] : pos2[l];
-            }
-        int* op;
-        UPI(op, other, other.size());
-        v.otherPos = op;
         hipError_t ea = hipSuccess;
         auto aD = [&](double*& ptr, size_t n) { if (ea == hipSuccess) ptr = devAlloc<double>(d, n, &ea); };
         auto aI = [&](int*& ptr, size_t n) { if (ea == hipSuccess) ptr = devAlloc<int>(d, n, &ea); };
@@ -5666,11 +5919,12 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         auto aB = [&](unsigned char*& ptr, size_t n) { if (ea == hipSuccess) ptr = devAlloc<unsigned char>(d, n, &ea); };
         aI(v.cnt, 4);
         aU(v.lStamp, std::max<size_t>(nL, 1));
+        aI(v.lCid, std::max<size_t>(nL, 1));
         aU(d->cmStamp, capN);
         aI(d->cmCid, capN);
         aI(v.node, capN);
         aI(v.deg, capN);
-        aI(v.csr, (size_t)S * capN);
+        aI(v.csr, (size_t)kCompactMaxDeg * capN);
         aI(v.link, capL);
         if (ea == hipSuccess) v.ends = devAlloc<int2>(d, capL, &ea);
         aU(v.nflags, capN);
@@ -5698,12 +5952,14 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (ea == hipSuccess) ea = hipMemset(v.lStamp, 0, std::max<size_t>(nL, 1) * sizeof(unsigned));
         if (ea == hipSuccess) ea = hipMemset(d->cmStamp, 0, capN * sizeof(unsigned));
         if (ea != hipSuccess) { fail(std::string("compact graph: ") + hipGetErrorString(ea)); return err_; }
-        // the walk: two workgroups per CU (one thread per slot, S |L1| slots);
-        // the node pass and the gather: two per CU (one thread per node)
+        // the walk: two workgroups per CU (one thread per compact conduit);
+        // the node pass and the gathers: two per CU (one thread per node, the
+        // first gather four per unconverged node too)
         const int cus = std::max(prop.multiProcessorCount, 1);
         d->gridCWalk = 2 * cus;
         d->gridCNode = 2 * cus;
-        d->gridCGather = 2 * cus;
+        d->gridCGather = 4 * cus;
+        d->gridCGather2 = 2 * cus;
         if (const char* gw = getenv("SWMM5_CWALK_GRID")) d->gridCWalk = std::max(1, (int)(atof(gw) * cus));
         if (const char* gn2 = getenv("SWMM5_CNODE_GRID")) d->gridCNode = std::max(2, (int)(atof(gn2) * cus));
         HIPCHECK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));

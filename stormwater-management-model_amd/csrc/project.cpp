@@ -605,8 +605,6 @@ int Project::readOption(const char* s1, const char* s2)  // project.c:445-769
         else if (k == O_SKIP_STEADY_STATE) opt.skipSteadyState = m;
         else if (k == O_IGNORE_ROUTING) opt.ignoreRouting = m;
         else if (k == O_IGNORE_QUALITY) opt.ignoreQuality = m;
-        if (opt.skipSteadyState)
-            return setError(200, "ERROR 200: SKIP_STEADY_STATE is not supported by the MI355X engine");
         if (opt.ignoreRouting)
             return setError(200, "ERROR 200: IGNORE_ROUTING leaves nothing for the routing engine to do");
         break;

@@ -112,6 +112,7 @@ def load_library(path: str | None = None):
         "swmmx_getPartition": (ctypes.c_long, [c_char_p, P(c_int), ctypes.c_long]),
         "swmmx_xsect": (c_int, [c_int, P(c_dbl), c_dbl, c_int, P(c_dbl), P(c_dbl), c_int, c_int]),
         "swmmx_evapReplay": (ctypes.c_long, [P(c_dbl), ctypes.c_long, P(c_dbl)]),
+        "swmmx_streamTriad": (c_int, [ctypes.c_long, c_int, P(c_dbl)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -319,6 +320,16 @@ class SWMM:
         if rc:
             raise RuntimeError("swmmx_timeKernel failed (%d)" % rc)
         return v.value
+
+    def stream_triad(self, n_doubles: int = 64 << 20, reps: int = 20) -> dict:
+        """The achievable HBM bandwidth: STREAM triad (and copy) GB/s on the
+        current device, HIP-event timed (swmmx_streamTriad)."""
+        out = (ctypes.c_double * 4)()
+        rc = self.L.swmmx_streamTriad(int(n_doubles), int(reps), out)
+        if rc:
+            raise RuntimeError("swmmx_streamTriad failed (%d)" % rc)
+        return {"triad_best_GBs": out[0], "triad_avg_GBs": out[1], "copy_best_GBs": out[2],
+                "bytes_per_launch": out[3], "launches": int(reps)}
 
     def set_device(self, ordinal: int):
         return self.L.swmmx_setDevice(int(ordinal))

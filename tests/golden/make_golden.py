@@ -141,6 +141,16 @@ CASES = {
                                                        evap="FILE:TD3200", options={"REPORT_STEP": "01:00:00"}), 10),
     "example_evap_dly": (netgen.write_example, dict(end_time="02:00:00", route_step=30.0, storage=True,
                                                     evap="TEMPERATURE:DLY0204", options={"REPORT_STEP": "01:00:00"}), 10),
+    # SKIP_STEADY_STATE (routing.c:236-244, 383-395): the hydrograph passes,
+    # the system settles and steps are skipped while the inflows and the
+    # step's flow error stay within LAT_FLOW_TOL / SYS_FLOW_TOL
+    "example_steady": (netgen.write_example, dict(end_time="08:00:00", route_step=10.0,
+                                                  options={"SKIP_STEADY_STATE": "YES"}), 2),
+    "example_steady_var": (netgen.write_example, dict(end_time="08:00:00", route_step=10.0,
+                                                      variable_step=0.75,
+                                                      options={"SKIP_STEADY_STATE": "YES",
+                                                               "SYS_FLOW_TOL": "1",
+                                                               "LAT_FLOW_TOL": "2"}), 2),
     "example_dummy": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, dummy=True,
                                                  pollutants=True), 1),
     "example_dummy_var": (netgen.write_example, dict(end_time="02:00:00", route_step=10.0, variable_step=0.75,

@@ -5,6 +5,8 @@
 //      a small phase kernel),
 //  (b) a grid barrier inside one persistent launch with agent-scope
 //      release / acquire fences (buffer_wbl2 sc1 / buffer_inv sc1 on gfx950),
+//  (c) a forked side kernel joined two phases later (a concurrent graph
+//      branch, e.g. for the outfall depths),
 // each phase writing F bytes of "compact state" (spread over the grid) and
 // reading another workgroup's values of the previous phase (so the data
 // really crosses workgroups / XCDs, and is checked).
@@ -12,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
@@ -21,22 +24,26 @@ struct Ctl {
     int err;
 };
 
-// one phase: thread t (of nthr) owns doubles [t*per, (t+1)*per) of buf; it
-// reads the values another workgroup's thread wrote in the previous phase and
-// writes its own, value = phase + index
+// one phase: thread t (of nthr) owns doubles [t*per, (t+1)*per) of one half
+// of buf (phases alternate halves); it reads the values another workgroup's
+// thread wrote in the previous phase (other half) and writes its own, value =
+// phase + index
 __device__ __forceinline__ int phaseWork(double* buf, int per, int nthr, int tid, int r)
 {
     int bad = 0;
     if (per == 0) return 0;
+    const size_t half = (size_t)per * nthr;
+    const double* in = buf + ((r + 1) & 1) * half;
+    double* out = buf + (r & 1) * half;
     const int src = (tid + 64 * 37 + 1) % nthr;           // another workgroup
     for (int q = 0; q < per; q++) {
         const size_t i = (size_t)src * per + q;
-        const double v = buf[i];
+        const double v = in[i];
         if (r > 0 && v != (double)(r - 1) + (double)i) bad++;
     }
     for (int q = 0; q < per; q++) {
         const size_t i = (size_t)tid * per + q;
-        buf[i] = (double)r + (double)i;
+        out[i] = (double)r + (double)i;
     }
     return bad;
 }
@@ -77,6 +84,58 @@ __global__ void k_phase(double* buf, int per, int r, int* bad)
     if (b) atomicAdd(bad, b);
 }
 
+// (c) fork/join inside a captured graph: a main chain of `rounds` phase
+// kernels, and a side kernel per phase forked after main phase i (on a second
+// stream) and joined before main phase i + 2 -- what a concurrent branch costs
+__global__ void k_side(double* buf, int r, int* bad)
+{
+    if (threadIdx.x == 0 && blockIdx.x == 0 && buf[r & 1023] < -1.0) atomicAdd(bad, 1);
+}
+
+static int forkJoin(hipStream_t s, hipStream_t s2, double* buf, int* bad, int wgs, int per, int rounds, float* msOut,
+                    bool withSide)
+{
+    std::vector<hipEvent_t> fork(rounds), join(rounds);
+    for (int r = 0; r < rounds; r++) {
+        CK(hipEventCreateWithFlags(&fork[r], hipEventDisableTiming));
+        CK(hipEventCreateWithFlags(&join[r], hipEventDisableTiming));
+    }
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    for (int r = 0; r < rounds; r++) {
+        if (withSide && r >= 2) CK(hipStreamWaitEvent(s, join[r - 2], 0));
+        hipLaunchKernelGGL(k_phase, dim3(wgs), dim3(256), 0, s, buf, per, r, bad);
+        if (withSide) {
+            CK(hipEventRecord(fork[r], s));
+            CK(hipStreamWaitEvent(s2, fork[r], 0));
+            hipLaunchKernelGGL(k_side, dim3(1), dim3(64), 0, s2, buf, r, bad);
+            CK(hipEventRecord(join[r], s2));
+        }
+    }
+    if (withSide)
+        for (int r = rounds - 2; r < rounds; r++) CK(hipStreamWaitEvent(s, join[r], 0));
+    CK(hipStreamEndCapture(s, &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float best = 1e30f;
+    for (int rep = 0; rep < 5; rep++) {
+        CK(hipEventRecord(e0, s));
+        CK(hipGraphLaunch(ge, s));
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        best = std::min(best, ms);
+    }
+    *msOut = best;
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(g);
+    return 0;
+}
+
 int main()
 {
     int dev = 0, cus = 0;
@@ -86,7 +145,7 @@ int main()
     Ctl* c;
     double* buf;
     int* bad;
-    const size_t maxBytes = 64ull << 20;
+    const size_t maxBytes = 128ull << 20;      // two halves
     CK(hipMalloc(&c, sizeof(Ctl)));
     CK(hipMalloc(&buf, maxBytes));
     CK(hipMalloc(&bad, sizeof(int)));
@@ -97,6 +156,18 @@ int main()
     CK(hipEventCreate(&e1));
     const int rounds = 64;
     const int blockSz = 256;
+    {
+        hipStream_t s2;
+        CK(hipStreamCreate(&s2));
+        for (int wgs : {64, 256}) {
+            float a = 0, b = 0;
+            if (forkJoin(s, s2, buf, bad, wgs, 4, rounds, &a, false) || forkJoin(s, s2, buf, bad, wgs, 4, rounds, &b, true))
+                return 1;
+            printf("graph chain of %d phases (%d wgs): %.2f us/phase; with a forked side kernel per phase joined two "
+                   "phases later: %.2f us/phase\n", rounds, wgs, 1000.0f * a / rounds, 1000.0f * b / rounds);
+            fflush(stdout);
+        }
+    }
     for (int wgs : {8, 32, 64, 128, 256}) {
         for (size_t foot : {(size_t)0, (size_t)256 << 10, (size_t)2 << 20, (size_t)16 << 20}) {
             const int nthr = wgs * blockSz;
