@@ -4370,6 +4370,10 @@ struct Router::Impl {
     hipGraphExec_t graphSparse = nullptr;
     int sparseMode = 2;
     bool sparseOk = false;
+    // the list graph: sparseOk's conditions without the single-GPU one (its
+    // iterations carry the neighbour exchange and the flag all-reduce as the
+    // unrolled graph's do)
+    bool listOk = false;
     double sparseMax = 6000.0;
     double liveAvg = 0.0;            // moving average of the live-list length after iteration 1
     long long modeSteps[6] = {0, 0, 0, 0, 0, 0};   // steps launched per graph (unrolled, k_tail, sparse, list, fused, compact)
@@ -4809,8 +4813,15 @@ static int launchStepImpl(Router::Impl* d, int mode)
                 launchTimed(d, linkKernel(false, d->linkWaves, d->fastLinks), dim3(d->gridLinkSparse),
                             ev ? ev[4 * k] : nullptr, d->timing ? d->curHot[k] : nullptr, p, k);
             if (p.nCold) (void)hipStreamWaitEvent(d->stream, d->joinEv[k], 0);
+            if (multi) {                           // ghost links' values from their owners (as launchIteration)
+                if (p.nSend) hipLaunchKernelGGL(k_xpack, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
+                if (int r = neighbourExchange(d, p.xF)) return r;
+                if (p.nGhost) hipLaunchKernelGGL(k_xunpack, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
+            }
             launchTimed(d, d->general ? k_node_list<true> : k_node_list<false>, dim3(d->gridNList),
                         ev ? ev[4 * k + 1] : nullptr, ev ? ev[4 * k + 2] : nullptr, p, k);
+            if (multi)
+                if (int r = flagExchange(d, k)) return r;
         }
         launchTimed(d, k_unfreeze, dim3(d->gridN), (hipEvent_t) nullptr, (hipEvent_t) nullptr, p);
     } else if (mode == GM_FUSED) {
@@ -5752,7 +5763,16 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     // ---- capture the step graph ----------------------------------------------
     // (the host-callback test transport synchronises inside the step: eager)
     d->useGraph = !(part.active() && part.transport == XCHG_HOST);
-    if (!d->useGraph) { ok_ = true; return 0; }
+    if (!d->useGraph) {
+        // eager launches: the per-step choice between the unrolled and the
+        // list graph's launch sequences (the others are single-GPU)
+        const char* sm = getenv("SWMM5_SPARSE");
+        d->sparseMode = sm ? atoi(sm) : 2;
+        if (const char* lx = getenv("SWMM5_LIST_MAX")) d->listMax = atof(lx);
+        d->listOk = d->sparseMode != 0 && p.nNC == 0 && p.maxTrials > 2;
+        ok_ = true;
+        return 0;
+    }
     {
         // off by default: on the surcharged 1M grid (round 4) the walk with the
         // prologue took longer than the node launch saved (SWMM5_DEFER_OUTFALL=1
@@ -5815,6 +5835,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (const char* sx = getenv("SWMM5_SPARSE_MAX")) d->sparseMax = atof(sx);
         if (const char* lx = getenv("SWMM5_LIST_MAX")) d->listMax = atof(lx);
         d->sparseOk = d->sparseMode != 0 && !part.active() && !d->comm && p.nNC == 0 && p.maxTrials > 2;
+        d->listOk = d->sparseMode != 0 && p.nNC == 0 && p.maxTrials > 2;
     }
     if (d->sparseOk) {
         HIPCHECK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
@@ -5827,7 +5848,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         HIPCHECK(hipGraphInstantiate(&d->graphSparse, g, nullptr, nullptr, 0));
         (void)hipGraphDestroy(g);
     }
-    if (d->sparseOk) {
+    if (d->listOk) {
         HIPCHECK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
         if (launchStep(d, GM_LIST)) {
             (void)hipStreamEndCapture(d->stream, &g);
@@ -6156,12 +6177,12 @@ static int chooseGraph(Router::Impl* d)
     }
     const bool fresh = d->itersSeen < 0;
     if (d->sparseOk && d->sparseMode == 1) return GM_SPARSE;
-    if (d->sparseOk && d->sparseMode == 3) return GM_LIST;
+    if (d->listOk && d->sparseMode == 3) return GM_LIST;
     if (d->fusedGrid > 0 && d->sparseMode == 4) return GM_FUSED;
     if (d->compactOk && d->sparseMode == 5) return GM_COMPACT;
     if (d->tailGrid > 0 && (d->tailMode == 1 || fresh || d->itersAvg <= kTailIters)) return GM_TAIL;
     if (d->sparseOk && !fresh && d->liveAvg <= d->sparseMax) return GM_SPARSE;
-    if (d->sparseOk && !fresh && d->liveAvg <= d->listMax) {
+    if (d->listOk && !fresh && d->liveAvg <= d->listMax) {
         if (d->compactOk && d->compactAuto) return GM_COMPACT;
         return (d->fusedGrid > 0 && d->fusedAuto) ? GM_FUSED : GM_LIST;
     }
@@ -6265,9 +6286,13 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
                                 : mode == GM_TAIL    ? d->graphTail
                                                      : d->graph,
                                 d->stream));
-    } else if (launchStep(d)) {                   // eager (host-transport exchange)
-        fail(d->xerrMsg);
-        return err_;
+    } else {                                       // eager (host-transport exchange)
+        const int mode = chooseGraph(d);
+        d->modeSteps[mode]++;
+        if (launchStep(d, mode)) {
+            fail(d->xerrMsg);
+            return err_;
+        }
     }
     // completion marker of this step: k_finalize has by then written the next
     // step's dt into the host-mapped ring (Router::launchedDt)

@@ -115,6 +115,8 @@ def load_library(path: str | None = None):
         "swmmx_streamTriad": (c_int, [ctypes.c_long, c_int, P(c_dbl)]),
     }
     for name, (res, args) in sig.items():
+        if not hasattr(L, name) and os.environ.get("SWMM5_LIB"):
+            continue                    # an older build taken for an A/B comparison
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

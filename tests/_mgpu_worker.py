@@ -70,6 +70,7 @@ def main():
         "node_owner": s.owners(swmm5.NODE),
         "link_owner": s.owners(swmm5.LINK),
         "counters": np.array([c["steps"], c["iterations"], c["nonconverged"]]),
+        "graphs": np.array([c["steps_unrolled"], c["steps_list"]]),
     }
     for f in ("newDepth", "newVolume", "inflow", "outflow", "overflow"):
         res["node." + f] = s.get_array("node." + f)

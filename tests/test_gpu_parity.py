@@ -57,10 +57,12 @@ FLIP_WINDOW = 2
 # cases where the engine flips a class-selected coefficient at (link, step)
 # pairs no reference build flips (DESIGN.md §2 names them): at most this many
 # such pairs are exempt, and their depths, flows and volumes are still bound.
-# example_shapes_var: conduit 15's upstream end sits on the 0.0001 ft dry
-# threshold (dwflow.c:399-411) at step 692, after the reference's own builds
-# have parted (their spread in surfArea1 is 35 ft2 from step 194 on)
-FLIPS_UNMIRRORED = {"example_shapes_var": 1}
+# example_shapes_var (after the reference's own builds part at step 194;
+# their spread in surfArea1 is 35 ft2 from there on): conduit 15's upstream
+# end sits on the 0.0001 ft dry threshold at step 692 (UP_DRY against
+# SUBCRITICAL, dwflow.c:399-411), conduit 13's Froude number on 1 at steps
+# 713 and 723 (SUPCRITICAL against SUBCRITICAL, dwflow.c:186)
+FLIPS_UNMIRRORED = {"example_shapes_var": 3}
 # regulator networks: pumps switch and orifices / weirs carry near-zero flows,
 # where libm ulps leave absolute differences of a few 1e-9 (cfs, ft)
 ATOL_CASE = {"example_regulators_var_qual": 1e-8}

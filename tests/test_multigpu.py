@@ -384,6 +384,25 @@ def _grid_with_regulators(tmp_path, n=20):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_ranks_list_graph_bitwise(world, tmp_path):
+    """The list graph (iterations k >= 2 as unconverged-list walks and
+    live-list node passes, each followed by the neighbour exchange and the
+    flag all-reduce) on several ranks: every step runs it and the run is
+    bitwise equal to one GPU's (which runs it too) -- the surcharged,
+    non-converging 30 x 30 grid, host transport."""
+    inp = _grid(tmp_path, 30, 30, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.5)
+    env = {"SWMM5_SPARSE": "3"}
+    one = _run_workers(inp, 250, tmp_path, 1, "host", "one", extra_env=env)[0]
+    st, its, nonconv = one["counters"]
+    assert nonconv > 10 and its / st > 2.5, one["counters"]
+    parts = _run_workers(inp, 250, tmp_path, world, "host", "part", extra_env=env)
+    for part in parts:
+        assert part["graphs"][1] == part["counters"][0], (part["graphs"], part["counters"])
+    _assert_bitwise(parts, one)
+
+
+@pytest.mark.gpu
 def test_regulators_two_ranks_bitwise(tmp_path):
     """An orifice, a weir across the strip boundary and an outlet (k_nc) with
     two ranks: each regulator's end nodes and the links touching them stay on
