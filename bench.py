@@ -452,6 +452,15 @@ def main():
                              "k_link_us": round(1000.0 * r[5] / r[0], 2),
                              "k_node_us": round(1000.0 * r[6] / r[0], 2)})
     roof["per_iteration"] = per_iter
+    if dist:
+        # each rank's sparse work (iterations k >= 2): the load balance of the
+        # strips (the surcharged region sits next to the outlet, on the last one)
+        mine_w = [round(sum(x["conduits_updated"] for x in per_iter if x["k"] >= 2)),
+                  round(sum(x["nodes_updated"] for x in per_iter if x["k"] >= 2))]
+        allw = [None] * world
+        dist.all_gather_object(allw, mine_w)
+        roof["per_rank_sparse_work"] = {"conduits_updated_k>=2": [w[0] for w in allw],
+                                        "nodes_updated_k>=2": [w[1] for w in allw]}
     if cfg["pollutants"]:
         roof["other_kernels"]["k_qual_node+k_qual_link"] = {
             "avg_launch_us": round(avg_us("quality"), 2), "achieved_GBs": round(gbs("quality"), 1)}

@@ -3,6 +3,7 @@
 #include "partition.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <numeric>
 #include <string>
 #include <unordered_map>
@@ -31,9 +32,16 @@ int buildPartition(const Network& net, Partition& part, std::string* msg)
         return 500;
     }
     const int me = part.rank;
-    // nodes: contiguous blocks of the node index
+    // nodes: contiguous blocks of the node index; or (SWMM5_PART_BLOCK = B > 0)
+    // blocks of B nodes dealt to the ranks in turn, so that a hot region (the
+    // synthetic grids' surcharged corner next to the outlet: a 2-rank strip
+    // split gives the last strip 3x the first one's sparse iterations) is
+    // shared by every rank, at the price of more cut links
     part.nodeOwner.assign(nN, 0);
-    for (int i = 0; i < nN; i++) part.nodeOwner[i] = (int)((long long)i * R / nN);
+    long long block = 0;
+    if (const char* b = getenv("SWMM5_PART_BLOCK")) block = atoll(b);
+    for (int i = 0; i < nN; i++)
+        part.nodeOwner[i] = block > 0 ? (int)((i / block) % R) : (int)((long long)i * R / nN);
     // pumps / regulators: their end nodes ("deferred": updated by k_nc from
     // running link-order totals) and every link touching one stay on one rank,
     // the owner of the group's smallest node

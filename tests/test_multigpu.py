@@ -384,15 +384,17 @@ def _grid_with_regulators(tmp_path, n=20):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_ranks_list_graph_bitwise(world, tmp_path):
+@pytest.mark.parametrize("world,block", [(2, 0), (3, 0), (2, 90), (3, 60)])
+def test_ranks_list_graph_bitwise(world, block, tmp_path):
     """The list graph (iterations k >= 2 as unconverged-list walks and
     live-list node passes, each followed by the neighbour exchange and the
     flag all-reduce) on several ranks: every step runs it and the run is
     bitwise equal to one GPU's (which runs it too) -- the surcharged,
-    non-converging 30 x 30 grid, host transport."""
+    non-converging 30 x 30 grid, host transport; with row strips and with
+    node blocks dealt to the ranks in turn (SWMM5_PART_BLOCK: 3 and 2 grid
+    rows per block, every rank holding part of the surcharged corner)."""
     inp = _grid(tmp_path, 30, 30, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.5)
-    env = {"SWMM5_SPARSE": "3"}
+    env = {"SWMM5_SPARSE": "3", "SWMM5_PART_BLOCK": str(block)}
     one = _run_workers(inp, 250, tmp_path, 1, "host", "one", extra_env=env)[0]
     st, its, nonconv = one["counters"]
     assert nonconv > 10 and its / st > 2.5, one["counters"]
