@@ -4370,9 +4370,10 @@ struct Router::Impl {
     hipGraphExec_t graphSparse = nullptr;
     int sparseMode = 2;
     bool sparseOk = false;
-    // the list graph: sparseOk's conditions without the single-GPU one (its
-    // iterations carry the neighbour exchange and the flag all-reduce as the
-    // unrolled graph's do)
+    // the list graph: at least three iterations; partitioned runs and
+    // networks with pumps / regulators too (its iterations carry the
+    // neighbour exchange, k_nc and the flag all-reduce as the unrolled
+    // graph's do)
     bool listOk = false;
     double sparseMax = 6000.0;
     double liveAvg = 0.0;            // moving average of the live-list length after iteration 1
@@ -4820,6 +4821,13 @@ static int launchStepImpl(Router::Impl* d, int mode)
             }
             launchTimed(d, d->general ? k_node_list<true> : k_node_list<false>, dim3(d->gridNList),
                         ev ? ev[4 * k + 1] : nullptr, ev ? ev[4 * k + 2] : nullptr, p, k);
+            // pumps / regulators and their end nodes, as launchIteration: the
+            // end nodes are never frozen (NF_DEFER), so they stay on the live
+            // list and k_node_list rebuilds their conduit sums every
+            // iteration; k_nc adds the non-conduit links in link order,
+            // updates their depths and lists the unconverged ones for the next
+            // walk (the walk skips LF_NC links: k_nc routes them)
+            if (p.nNC > 0) hipLaunchKernelGGL(k_nc<false>, dim3(1), dim3(kBlock), 0, d->stream, p, k);
             if (multi)
                 if (int r = flagExchange(d, k)) return r;
         }
@@ -5769,7 +5777,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         const char* sm = getenv("SWMM5_SPARSE");
         d->sparseMode = sm ? atoi(sm) : 2;
         if (const char* lx = getenv("SWMM5_LIST_MAX")) d->listMax = atof(lx);
-        d->listOk = d->sparseMode != 0 && p.nNC == 0 && p.maxTrials > 2;
+        d->listOk = d->sparseMode != 0 && p.maxTrials > 2;
         ok_ = true;
         return 0;
     }
@@ -5835,7 +5843,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (const char* sx = getenv("SWMM5_SPARSE_MAX")) d->sparseMax = atof(sx);
         if (const char* lx = getenv("SWMM5_LIST_MAX")) d->listMax = atof(lx);
         d->sparseOk = d->sparseMode != 0 && !part.active() && !d->comm && p.nNC == 0 && p.maxTrials > 2;
-        d->listOk = d->sparseMode != 0 && p.nNC == 0 && p.maxTrials > 2;
+        d->listOk = d->sparseMode != 0 && p.maxTrials > 2;
     }
     if (d->sparseOk) {
         HIPCHECK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));

@@ -320,6 +320,79 @@ def test_fused_quality_bitwise(tmp_path, monkeypatch):
     assert runs[0][0].max() > 0.0
 
 
+def _regulator_grid(tmp_path, n=40):
+    """An n x n surcharged variable-step grid in which three conduits become
+    a side orifice, a transverse weir and a functional outlet, and a fourth a
+    type-3 pump (k_nc: link-order running totals of their end nodes)."""
+    import re
+    inp = str(tmp_path / "g.inp")
+    netgen.write_grid(inp, n, n, end_time="02:00:00", route_step=5.0, variable_step=0.75, diameter=1.0, q=0.3)
+    text = open(inp).read()
+    head, rest = text.split("[CONDUITS]", 1)
+    cond, rest = rest.split("[XSECTIONS]", 1)
+    xs, tail = rest.split("\n\n", 1)
+
+    def pick(row_from, row_to):
+        for line in cond.splitlines():
+            m = re.match(r"(C\d+)\s+J(\d+)_(\d+)\s+J(\d+)_(\d+)", line)
+            if m and int(m.group(2)) == row_from and int(m.group(4)) == row_to and 2 <= int(m.group(3)) < n - 2:
+                return line.split()
+        raise AssertionError((row_from, row_to))
+    ori, weir, outl, pump = pick(3, 4), pick(n // 2 - 1, n // 2), pick(3 * n // 4, 3 * n // 4 + 1), pick(n - 3, n - 2)
+    drop = {ori[0], weir[0], outl[0], pump[0]}
+    keep = lambda block: "\n".join(l for l in block.splitlines() if not (l.split() and l.split()[0] in drop))
+    out = head + "[CONDUITS]" + keep(cond) + "[XSECTIONS]" + keep(xs) + "\n"
+    out += "%s CIRCULAR 1.0 0 0 0\n%s RECT_OPEN 1.0 3.0 0 0\n\n" % (ori[0], weir[0])
+    out += "[ORIFICES]\n%s %s %s SIDE 0.0 0.65 NO\n\n" % (ori[0], ori[1], ori[2])
+    out += "[WEIRS]\n%s %s %s TRANSVERSE 0.1 3.33 NO 0 0 YES\n\n" % (weir[0], weir[1], weir[2])
+    out += "[OUTLETS]\n%s %s %s 0.0 FUNCTIONAL/DEPTH 2.0 0.5 NO\n\n" % (outl[0], outl[1], outl[2])
+    out += "[PUMPS]\n%s %s %s PC1 ON 0 0\n\n" % (pump[0], pump[1], pump[2])
+    out += "[CURVES]\nPC1 PUMP3 0.0 2.0\nPC1 2.0 1.0\nPC1 4.0 0.0\n\n"
+    out += tail
+    open(inp, "w").write(out)
+    return inp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["example_regulators", "example_regulators_var_qual", "grid"])
+def test_list_graph_regulators_bitwise(case, tmp_path, monkeypatch):
+    """The list graph for networks with pumps and regulators (k_nc after
+    every k_node_list; their end nodes never freeze, so they stay on the live
+    list): every step runs it, and every node and link field, the pollutant
+    concentrations and every counter are bitwise equal to the unrolled graph's
+    -- the two regulator fixtures and a surcharged 40 x 40 grid with an
+    orifice, a weir, an outlet and a pump (dynwave.c:398-412, 423-524)."""
+    import _golden
+    inp = _regulator_grid(tmp_path) if case == "grid" else _golden.inp(case)
+    runs = []
+    for sparse in ("0", "3"):
+        monkeypatch.setenv("SWMM5_SPARSE", sparse)
+        s = _engine(inp, tmp_path)
+        snaps = []
+        while True:
+            err, t = s.run_steps(100)
+            assert err == 0, s.getError()
+            snaps.append([s.get_array("node." + f) for f in NODE_F] + [s.get_array("link." + f) for f in LINK_F])
+            if "qual" in case:
+                snaps[-1] += [s.get_array("node.newQual"), s.get_array("link.newQual")]
+            if t == 0.0 or len(snaps) >= 12:
+                break
+        c = s.counters()
+        runs.append((snaps, c))
+        s.end()
+        s.close()
+    (a, c0), (b, c3) = runs
+    print(case, "unrolled:", c0, "list:", c3)
+    assert c3["steps_list"] == c3["steps"] and c0["steps_list"] == 0, c3
+    for k in ("steps", "iterations", "nonconverged"):
+        assert c0[k] == c3[k], (k, c0, c3)
+    for x, y in zip(a, b):
+        for u, v in zip(x, y):
+            np.testing.assert_array_equal(u, v)
+    if case == "grid":                          # iterations >= 2 really ran
+        assert c0["iterations"] > 2 * c0["steps"] + 100, c0
+
+
 @pytest.mark.gpu
 def test_sparse_tail_bitwise_1m(tmp_path, monkeypatch):
     """The light-surcharge 1M regime (707 x 707, q = 0.1 cfs: a few thousand

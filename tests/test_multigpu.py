@@ -405,16 +405,26 @@ def test_ranks_list_graph_bitwise(world, block, tmp_path):
 
 
 @pytest.mark.gpu
-def test_regulators_two_ranks_bitwise(tmp_path):
+@pytest.mark.parametrize("sparse", ["0", "3"])
+def test_regulators_two_ranks_bitwise(sparse, tmp_path):
     """An orifice, a weir across the strip boundary and an outlet (k_nc) with
     two ranks: each regulator's end nodes and the links touching them stay on
     one rank, every other node is exchanged as usual; bitwise equal to one
-    GPU."""
+    GPU.  With the unrolled graph, and with the list graph on every step
+    (k_nc after each k_node_list), whose one-GPU run is bitwise equal to the
+    unrolled one's too."""
     inp = _grid_with_regulators(tmp_path)
-    one = _run_workers(inp, 300, tmp_path, 1, "host", "one")[0]
-    parts = _run_workers(inp, 300, tmp_path, 2, "host", "two")
+    env = {"SWMM5_SPARSE": sparse}
+    one = _run_workers(inp, 300, tmp_path, 1, "host", "one", extra_env=env)[0]
+    parts = _run_workers(inp, 300, tmp_path, 2, "host", "two", extra_env=env)
     assert all((p["link_owner"] == r).any() for r, p in enumerate(parts))
     _assert_bitwise(parts, one)
+    if sparse == "3":
+        for run in [one] + parts:
+            assert run["graphs"][1] == run["counters"][0], (run["graphs"], run["counters"])
+        unrolled = _run_workers(inp, 300, tmp_path, 1, "host", "unrolled", extra_env={"SWMM5_SPARSE": "0"})[0]
+        assert unrolled["graphs"][1] == 0, unrolled["graphs"]
+        _assert_bitwise([unrolled], one)
 
 
 @pytest.mark.gpu
