@@ -18,7 +18,7 @@ engine where the fixtures cannot reach:
     - 100 x 100 for one simulated hour: lockstep from the start to step 450,
       then 40-step windows restarted from the engine's own state;
     - 60 x 60 (q = 0.3) and the 707 x 707 benchmark grid itself (after the
-      bench's 400-step spin-up) in windows that start from the engine's own
+      bench's 750-step spin-up) in windows that start from the engine's own
       mid-run state (swmmx_exportState -> oracle_resume), every step compared;
 * 707 x 707 grid: bitwise run-to-run determinism (no atomics in any sum),
   finite state, and the flow-routing continuity error of the whole 5-minute
@@ -397,7 +397,7 @@ def test_list_graph_regulators_bitwise(case, tmp_path, monkeypatch):
 def test_sparse_tail_bitwise_1m(tmp_path, monkeypatch):
     """The light-surcharge 1M regime (707 x 707, q = 0.1 cfs: a few thousand
     live nodes after iteration 1) through the unrolled step graph and through
-    the k_sparse graph: after the 400-step spin-up and 40 more steps every node
+    the k_sparse graph: after the preset's 400-step spin-up and 40 more steps every node
     and link field and every counter is bitwise equal, and the sparse run
     really ran its iterations >= 2 in k_sparse; the same for the list graph,
     and for the unrolled and list graphs without the deferred outfall
@@ -434,7 +434,7 @@ def test_sparse_tail_bitwise_1m(tmp_path, monkeypatch):
 @pytest.mark.gpu
 def test_config4_4m_window(tmp_path):
     """configs[4]'s 4M workload (bench.py's "4m": 1414 x 1414 junctions,
-    3,995,965 conduits, variable step) on one GPU after its 400-step spin-up:
+    3,995,965 conduits, variable step) on one GPU after its 850-step spin-up:
     the next 8 steps of the engine against the oracle continuing from the
     engine's own state (OpenMP on the host's cores), every step and field
     compared at 1e-6, the Picard iteration count equal at every step."""
@@ -456,7 +456,7 @@ def test_config4_4m_window(tmp_path):
 
 @pytest.mark.gpu
 def test_benchmark_regime_window_707(tmp_path):
-    """bench.py's 1m_surcharge workload (BASELINE configs[2]) after its 400-step
+    """bench.py's 1m_surcharge workload (BASELINE configs[2]) after its 750-step
     spin-up: the next 12 steps of the engine against the oracle continuing
     from the engine's own state, every step compared at 1e-6."""
     import bench
@@ -510,7 +510,7 @@ def test_config1_100k_fixed_step_from_start(tmp_path):
 def test_config3_1m_quality_window(tmp_path):
     """BASELINE configs[3] at its own size: bench.py's 1m_quality workload
     (707 x 707 grid, 998,285 conduits, 3 pollutants with first-order decay,
-    variable step) after its 400-step spin-up: the next 12 steps of the engine
+    variable step) after its 750-step spin-up: the next 12 steps of the engine
     against the oracle continuing from the engine's own state (quality
     included, qualrout.c:100-142), every step compared at 1e-6 -- pollutant
     concentrations of every node and link included."""
