@@ -405,6 +405,8 @@ def main():
         "step_traffic_iterations_per_step": None if not step_bytes else rec.get("iterations_per_step"),
         "step_achieved": None if not step_bytes else round(step_bytes / step_s / 1e9, 2),
         "step_frac": None if not step_bytes else round(step_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4),
+        "step_frac_measured": None if not (step_bytes and stream)
+        else round(step_bytes / step_s / 1e9 / stream["triad_best_GBs"], 4),
         "kernel": "k_link<first> (Picard iteration 0 link momentum, dwflow_findConduitFlow, "
                   "every conduit)",
         "avg_launch_us": round(first_us, 2),
