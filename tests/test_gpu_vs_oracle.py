@@ -354,14 +354,19 @@ def _regulator_grid(tmp_path, n=40):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["example_regulators", "example_regulators_var_qual", "grid"])
-def test_list_graph_regulators_bitwise(case, tmp_path, monkeypatch):
-    """The list graph for networks with pumps and regulators (k_nc after
-    every k_node_list; their end nodes never freeze, so they stay on the live
-    list): every step runs it, and every node and link field, the pollutant
-    concentrations and every counter are bitwise equal to the unrolled graph's
-    -- the two regulator fixtures and a surcharged 40 x 40 grid with an
-    orifice, a weir, an outlet and a pump (dynwave.c:398-412, 423-524)."""
+@pytest.mark.parametrize("case", ["example_regulators", "example_regulators_var_qual", "grid",
+                                  "example_storage_var", "example_shapes_var", "example_culverts_var",
+                                  "example_dummy_var", "example_exfil_var", "example_steady_var"])
+def test_list_graph_bitwise_networks(case, tmp_path, monkeypatch):
+    """The list graph beyond the plain grids: networks with pumps and
+    regulators (k_nc after every k_node_list; their end nodes never freeze,
+    so they stay on the live list), storage units with exfiltration, non-basic
+    shapes and culverts (k_link_cold on the side stream, the kGeneral node
+    kernels), DUMMY conduits and steady-state skipping.  Every step runs it,
+    and every node and link field, the pollutant concentrations and every
+    counter are bitwise equal to the unrolled graph's -- the reference
+    fixtures and a surcharged 40 x 40 grid with an orifice, a weir, an outlet
+    and a pump (dynwave.c:398-412, 423-524)."""
     import _golden
     inp = _regulator_grid(tmp_path) if case == "grid" else _golden.inp(case)
     runs = []
