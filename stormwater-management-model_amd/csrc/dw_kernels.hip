@@ -338,6 +338,7 @@ struct Params {
     // flow-class times, 4 link maxima, 8 node volume totals, 16 node
     // statistics, 32 Courant limits, 64 capacity-limited state
     int endSkip;
+    int qualUnfreeze;             // k_qual_node also does k_unfreeze's work (launchStep)
     const int* coldLinks;         // LF_COLD conduits, ascending
     const int* outLinks;          // conduits with an outfall end, ascending
     int outInl0, outInl1, outInl2, outInl3;   // outLinks[0..3] (-1: none), read without a load
@@ -3681,8 +3682,10 @@ __device__ __forceinline__ void qualNode(const Params& p, int i, double dt, cons
             up[t] = (eb + t < e1) && l < p.nL && ((ent[t] < 0) ? (ql[t] < 0.0) : !(ql[t] < 0.0));
             fl[t] = up[t] ? p.lflags[l] : 0u;
             q1v[t] = up[t] ? p.q1[l] : 0.0;
-            sl[t] = up[t] ? p.seepLoss[l] : 0.0;
-            el[t] = up[t] ? p.evapLoss[l] : 0.0;
+            // (0 for a link without LF_SEEP, never rewritten: not loaded
+            // when no held link has losses, p.xF == 4)
+            sl[t] = (up[t] && p.xF > 4) ? p.seepLoss[l] : 0.0;
+            el[t] = (up[t] && p.xF > 4) ? p.evapLoss[l] : 0.0;
             v1v[t] = up[t] ? p.lOldVolume[l] : 0.0;
             v2v[t] = up[t] ? p.lNewVolume[l] : 0.0;
             dl[t] = up[t] ? p.lNewDepth[l] : 0.0;
@@ -3739,8 +3742,21 @@ __global__ __launch_bounds__(kBlock) void k_qual_node(Params p)
     double* nNew = p.nQual[par ^ 1];
     const double* lOld = p.lQual[par];
     double* lNew = p.lQual[par ^ 1];
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock)
+    int m = 0;
+    if (p.qualUnfreeze) {
+        bool converged;
+        m = stepIterations(p, &converged) - 1;
+    }
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
+        if (p.qualUnfreeze) {                         // k_unfreeze's work for this node (qualNode reads only
+            const int fz = p.frz[i];                  // its own node's depth)
+            if (fz) {
+                p.nNewDepth[i] = frozenDepth(p, i, fz, m);
+                p.frz[i] = 0;
+            }
+        }
         qualNode(p, i, dt, nOld, nNew, lOld, lNew);
+    }
 }
 
 // getVariableStep (dynwave.c:799-832) from the uncapped link and node
@@ -4766,7 +4782,12 @@ static int launchStep(Router::Impl* d, int mode = GM_UNROLLED)
     p.cmCid = compact ? d->cmCid : nullptr;
     p.cOutDepth = compact ? d->cv.nNewDepth : nullptr;
     p.cCnt = compact ? d->cv.cnt : nullptr;
+    // the list and fused graphs with a separate quality launch: k_qual_node
+    // gives the frozen junctions their final depth (each node's own thread,
+    // before its quality reads the depth), one full-grid k_unfreeze less
+    p.qualUnfreeze = ((mode == GM_LIST || mode == GM_FUSED) && p.P > 0 && !d->fuseQual && p.freeze) ? 1 : 0;
     const int r = launchStepImpl(d, mode);
+    p.qualUnfreeze = 0;
     p.convW = nullptr;
     p.cmStamp = nullptr;
     p.cmCid = nullptr;
@@ -4831,14 +4852,16 @@ static int launchStepImpl(Router::Impl* d, int mode)
             if (multi)
                 if (int r = flagExchange(d, k)) return r;
         }
-        launchTimed(d, k_unfreeze, dim3(d->gridN), (hipEvent_t) nullptr, (hipEvent_t) nullptr, p);
+        if (!p.qualUnfreeze)
+            launchTimed(d, k_unfreeze, dim3(d->gridN), (hipEvent_t) nullptr, (hipEvent_t) nullptr, p);
     } else if (mode == GM_FUSED) {
         for (int k = 0; k < 2; k++)
             if (int r = launchIteration(d, k)) return r;
         for (int k = 2; k < p.maxTrials; k++)
             launchTimed(d, fusedKernel(d->fastLinks, d->general), dim3(d->fusedGrid), ev ? ev[4 * k] : nullptr,
                         d->timing ? d->curHot[k] : nullptr, p, k);
-        launchTimed(d, k_unfreeze, dim3(d->gridN), (hipEvent_t) nullptr, (hipEvent_t) nullptr, p);
+        if (!p.qualUnfreeze)
+            launchTimed(d, k_unfreeze, dim3(d->gridN), (hipEvent_t) nullptr, (hipEvent_t) nullptr, p);
     } else if (mode == GM_COMPACT) {
         for (int k = 0; k < 2; k++)
             if (int r = launchIteration(d, k)) return r;

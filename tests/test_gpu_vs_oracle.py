@@ -320,13 +320,14 @@ def test_fused_quality_bitwise(tmp_path, monkeypatch):
     assert runs[0][0].max() > 0.0
 
 
-def _regulator_grid(tmp_path, n=40):
+def _regulator_grid(tmp_path, n=40, pollutants=0):
     """An n x n surcharged variable-step grid in which three conduits become
     a side orifice, a transverse weir and a functional outlet, and a fourth a
     type-3 pump (k_nc: link-order running totals of their end nodes)."""
     import re
     inp = str(tmp_path / "g.inp")
-    netgen.write_grid(inp, n, n, end_time="02:00:00", route_step=5.0, variable_step=0.75, diameter=1.0, q=0.3)
+    netgen.write_grid(inp, n, n, end_time="02:00:00", route_step=5.0, variable_step=0.75, diameter=1.0, q=0.3,
+                      pollutants=pollutants)
     text = open(inp).read()
     head, rest = text.split("[CONDUITS]", 1)
     cond, rest = rest.split("[XSECTIONS]", 1)
@@ -354,7 +355,7 @@ def _regulator_grid(tmp_path, n=40):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["example_regulators", "example_regulators_var_qual", "grid",
+@pytest.mark.parametrize("case", ["example_regulators", "example_regulators_var_qual", "grid", "grid_qual",
                                   "example_storage_var", "example_shapes_var", "example_culverts_var",
                                   "example_dummy_var", "example_exfil_var", "example_steady_var"])
 def test_list_graph_bitwise_networks(case, tmp_path, monkeypatch):
@@ -366,9 +367,14 @@ def test_list_graph_bitwise_networks(case, tmp_path, monkeypatch):
     and every node and link field, the pollutant concentrations and every
     counter are bitwise equal to the unrolled graph's -- the reference
     fixtures and a surcharged 40 x 40 grid with an orifice, a weir, an outlet
-    and a pump (dynwave.c:398-412, 423-524)."""
+    and a pump, with two pollutants too (grid_qual: the frozen junctions' final
+    depths then come from the quality kernel, not k_unfreeze;
+    dynwave.c:398-412, 423-524)."""
     import _golden
-    inp = _regulator_grid(tmp_path) if case == "grid" else _golden.inp(case)
+    if case.startswith("grid"):
+        inp = _regulator_grid(tmp_path, pollutants=2 if case == "grid_qual" else 0)
+    else:
+        inp = _golden.inp(case)
     runs = []
     for sparse in ("0", "3"):
         monkeypatch.setenv("SWMM5_SPARSE", sparse)
@@ -394,7 +400,7 @@ def test_list_graph_bitwise_networks(case, tmp_path, monkeypatch):
     for x, y in zip(a, b):
         for u, v in zip(x, y):
             np.testing.assert_array_equal(u, v)
-    if case == "grid":                          # iterations >= 2 really ran
+    if case.startswith("grid"):                 # iterations >= 2 really ran
         assert c0["iterations"] > 2 * c0["steps"] + 100, c0
 
 
