@@ -118,17 +118,26 @@ def _incident(n1, n2, nN):
     return rows
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
-def test_partition_ghost_layout(world, tmp_path):
+@pytest.mark.parametrize("world,block", [(2, 0), (3, 0), (8, 0), (2, 40), (3, 24), (8, 20)])
+def test_partition_ghost_layout(world, block, tmp_path, monkeypatch):
     """Every rank's held nodes see all their conduits -- owned ones and ghosts
     -- in ascending global order (the reference's summation order), and what
-    each owner sends is exactly what the receiver expects, in its order."""
+    each owner sends is exactly what the receiver expects, in its order.  For
+    contiguous strips (block 0) and for node blocks dealt to the ranks in turn
+    (SWMM5_PART_BLOCK: node i, unless an outfall, goes to rank
+    (i // block) % world)."""
+    monkeypatch.setenv("SWMM5_PART_BLOCK", str(block))
     inp = _grid(tmp_path, 24, 20)
     d = _topology(inp, tmp_path)
     n1, n2 = d["link.node1"].astype(int), d["link.node2"].astype(int)
     nN = len(d["node.type"])
     rows = _incident(n1, n2, nN)
-    _, link_owner = _owners(inp, tmp_path, 0, world)
+    node_owner, link_owner = _owners(inp, tmp_path, 0, world)
+    if block:
+        junction = d["node.type"].astype(int) != 1
+        idx = np.arange(nN)[junction]
+        np.testing.assert_array_equal(node_owner[junction], (idx // block) % world)
+        np.testing.assert_array_equal(link_owner, node_owner[n1])
     lay = [_layout(inp, tmp_path, r, world) for r in range(world)]
     for r, L in enumerate(lay):
         loc = np.concatenate([L["llink"], L["lghost"]])          # local -> global link
@@ -147,7 +156,7 @@ def test_partition_ghost_layout(world, tmp_path):
             sent = S["llink"][S["sendLink"][S["sendOff"][ks]:S["sendOff"][ks + 1]]]
             np.testing.assert_array_equal(ghosts, sent)
         assert len(L["lghost"]) == L["recvOff"][-1]
-    if world > 2:                      # strips: only adjacent ranks exchange
+    if world > 2 and not block:        # strips: only adjacent ranks exchange
         for r, L in enumerate(lay):
             assert set(L["nbr"]) <= {r - 1, r + 1}, (r, L["nbr"])
 
