@@ -482,6 +482,20 @@ def test_rank0_write_error_stops_every_rank(n, tmp_path):
 
 
 @pytest.mark.gpu
+def test_steady_state_skipping_rejected_with_ranks(tmp_path):
+    """SKIP_STEADY_STATE runs on one GPU only (its flow-error and inflow tests
+    would need a collective every step): with two ranks swmm_start returns
+    ERROR 200 on both, and neither goes on into a collective."""
+    import _golden
+    inp = _golden.inp("example_steady")
+    parts = _run_workers(inp, 10, tmp_path, 2, "host", "steady",
+                         extra_env={"WORKER_OUT0": str(tmp_path / "steady0.out")}, timeout=300)
+    for p in parts:
+        assert int(p["codes"][0]) == 200, p["codes"]
+        assert "SKIP_STEADY_STATE" in bytes(p["msg"]).decode(), bytes(p["msg"]).decode()
+
+
+@pytest.mark.gpu
 def test_rccl_single_rank_bitwise(tmp_path):
     inp = _grid(tmp_path, 30, 30, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.1)
     one = _run_workers(inp, 80, tmp_path, 1, "host", "plain")[0]
