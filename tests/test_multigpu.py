@@ -4,8 +4,9 @@ CPU (no GPU needed):
   * owner rules of the partition (node blocks, conduit -> node1's rank,
     outfall -> its conduit's rank) checked against a numpy restatement;
   * the engine's own ghost-link layout (swmmx_getPartition) for 2, 3 and 8
-    ranks: every held node's incidence row holds exactly its links in global
-    order, every ghost is sent by its owner in the receiver's order;
+    ranks, row strips and node blocks dealt in turn: every held node's
+    incidence row holds exactly its links in global order, every ghost is
+    sent by its owner in the receiver's order;
   * a world_size-2 gloo job of the neighbour exchange on that layout: each
     rank packs the links it sends (sendLink), exchanges them with its
     neighbours (gloo send / recv), unpacks them into its ghost slots and sums
@@ -14,7 +15,10 @@ GPU:
   * 2 and 3 ranks on the one GPU with the host (gloo) transport against the
     same network on one GPU: owned node / link state BITWISE equal, same
     iteration and non-convergence counts (fixed step; surcharged variable
-    step; 3 pollutants; pumps and regulators);
+    step; 3 pollutants; pumps and regulators; the list graph on every step,
+    with strips, interleaved blocks, pollutants and regulators);
+  * results and hot-start files byte-identical to one GPU's; a write error on
+    rank 0 stops every rank; SKIP_STEADY_STATE refused with several ranks;
   * 1 rank through the RCCL path (captured ncclSend/ncclRecv + flag
     all-reduce): bitwise equal to the single-GPU engine;
   * the 4M-conduit configs[4] network split in two strips, bitwise.
@@ -393,16 +397,18 @@ def _grid_with_regulators(tmp_path, n=20):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,block", [(2, 0), (3, 0), (2, 90), (3, 60)])
-def test_ranks_list_graph_bitwise(world, block, tmp_path):
+@pytest.mark.parametrize("world,block,pollutants", [(2, 0, 0), (3, 0, 0), (2, 90, 0), (3, 60, 0), (2, 0, 2)])
+def test_ranks_list_graph_bitwise(world, block, pollutants, tmp_path):
     """The list graph (iterations k >= 2 as unconverged-list walks and
     live-list node passes, each followed by the neighbour exchange and the
     flag all-reduce) on several ranks: every step runs it and the run is
     bitwise equal to one GPU's (which runs it too) -- the surcharged,
     non-converging 30 x 30 grid, host transport; with row strips and with
     node blocks dealt to the ranks in turn (SWMM5_PART_BLOCK: 3 and 2 grid
-    rows per block, every rank holding part of the surcharged corner)."""
-    inp = _grid(tmp_path, 30, 30, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.5)
+    rows per block, every rank holding part of the surcharged corner); and
+    with two pollutants (the frozen junctions' final depths then come from the
+    quality kernel, after the ghost links' concentrations moved)."""
+    inp = _grid(tmp_path, 30, 30, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.5, pollutants=pollutants)
     env = {"SWMM5_SPARSE": "3", "SWMM5_PART_BLOCK": str(block)}
     one = _run_workers(inp, 250, tmp_path, 1, "host", "one", extra_env=env)[0]
     st, its, nonconv = one["counters"]
