@@ -482,6 +482,40 @@ __device__ __forceinline__ double hydRadAt(const Geom& x, double y, const double
     if (y >= x.yFull) return x.rFull;
     return getRofY<kAll>(x, y, ct);
 }
+// The same relations for a circular section (the kFast instantiation: no
+// slot) given the depth's normalised value yn = normDepth(x, y) and its
+// circular-table index part c = circIdx(yn): the operations of widthAt /
+// areaAt / hydRadAt / linkFroude with the index part computed once per depth
+__device__ __forceinline__ double circWidthAt(const Params& p, const Geom& x, double yn, const CircIdx& c,
+                                              const double* ct)
+{
+    if (yn >= p.crownCutoff)                       // closed section: the width at the crown cutoff
+        return x.wMax * lookup(normDepth(x, p.crownCutoff * x.yFull), SWX_TW(ct), SWX_CIRC_N);
+    return x.wMax * circLookup(c, SWX_TW(ct));
+}
+__device__ __forceinline__ double circAreaAt(const Geom& x, double y, const CircIdx& c, const double* ct)
+{
+    if (y >= x.yFull) return x.aFull + (y - x.yFull) * 0.0;      // (no slot: wSlot = 0)
+    if (y <= 0.0) return 0.0;
+    return x.aFull * circLookup(c, SWX_TA(ct));
+}
+__device__ __forceinline__ double circHydRadAt(const Geom& x, double y, const CircIdx& c, const double* ct)
+{
+    if (y >= x.yFull) return x.rFull;
+    return x.rFull * circLookup(c, SWX_TR(ct));
+}
+// link_getFroude (link.c:847-871) at depth y whose area a = A(y) (y < yFull:
+// the caller's areaAt value) and width w = widthAt(y) were found already: the
+// unclamped top width is w below the crown cutoff, else read again
+__device__ __forceinline__ double circFroude(const Params& p, const Geom& x, double v, double y, double yn,
+                                             const CircIdx& c, double a, double w, const double* ct)
+{
+    if (y <= 0.0001) return 0.0;
+    if (x.yFull - y <= 0.0001) return 0.0;         // closed section
+    const double wy = (yn >= p.crownCutoff) ? x.wMax * circLookup(c, SWX_TW(ct)) : w;
+    const double hy = a / wy;
+    return fabs(v) / sqrt(32.2 * hy);
+}
 
 // link.c:1334-1399 (DW branch); returns total loss rate, sets evap/seep
 template <bool kAll>
@@ -720,8 +754,10 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     // ---- findSurfArea (dwflow.c:417-550) ----
     int fc;
     double sa1 = 0.0, sa2 = 0.0;
+    [[maybe_unused]] double nd1 = 0.0, nd2 = 0.0, ndM = 0.0, dMidF = 0.0, w1F = 0.0, wMidF = 0.0;
+    [[maybe_unused]] CircIdx c1{}, c2{}, cM{};
     {
-        double d1 = y1, d2 = y2, dMid, w1, w2, wMid, fasnh = 1.0;
+        double d1 = y1, d2 = y2, dMid, w1 = 0.0, w2, wMid = 0.0, fasnh = 1.0;
         double yNorm = (d1 + d2) / 2.0;
         double yCrit = yNorm;
         if (d1 >= x.yFull && d2 >= x.yFull) fc = F_SUBCRIT;
@@ -747,15 +783,34 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         case F_DN_DRY: d2 = 0.0001; break;
         default: break;
         }
+        if constexpr (kFast) {
+            // the all-circular instantiation: the circular tables' index
+            // parts at d1, d2 and their mean, shared by every table read at
+            // those depths below (widths, areas, radii, Froude numbers)
+            dMid = 0.5 * (d1 + d2);
+            if (dMid < 0.0001) dMid = 0.0001;
+            nd1 = normDepth(x, d1);
+            nd2 = normDepth(x, d2);
+            ndM = normDepth(x, dMid);
+            c1 = circIdx(nd1);
+            c2 = circIdx(nd2);
+            cM = circIdx(ndM);
+        }
         if (fc == F_DRY) {
             sa1 = 0.0001 * length / 2.0;
             sa2 = sa1;
         } else {
-            dMid = 0.5 * (d1 + d2);
-            if (dMid < 0.0001) dMid = 0.0001;
-            w1 = widthAt<kFast, kCold>(p, x, d1, ct);
-            w2 = widthAt<kFast, kCold>(p, x, d2, ct);
-            wMid = widthAt<kFast, kCold>(p, x, dMid, ct);
+            if constexpr (kFast) {
+                w1 = circWidthAt(p, x, nd1, c1, ct);
+                w2 = circWidthAt(p, x, nd2, c2, ct);
+                wMid = circWidthAt(p, x, ndM, cM, ct);
+            } else {
+                dMid = 0.5 * (d1 + d2);
+                if (dMid < 0.0001) dMid = 0.0001;
+                w1 = widthAt<kFast, kCold>(p, x, d1, ct);
+                w2 = widthAt<kFast, kCold>(p, x, d2, ct);
+                wMid = widthAt<kFast, kCold>(p, x, dMid, ct);
+            }
             switch (fc) {
             case F_SUBCRIT:                                  // dwflow.c:460-472
                 sa1 = (w1 + wMid) * length / 4.;
@@ -779,19 +834,40 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         }
         y1 = d1;
         y2 = d2;
+        if constexpr (kFast) {
+            dMidF = dMid;
+            w1F = w1;
+            wMidF = wMid;
+        }
     }
     SWX_LST(sa1, sa1);
     SWX_LST(sa2, sa2);
 
-    double wSlot = slotWidth<kFast>(p, x, y1);
-    double a1 = areaAt<kCold>(x, y1, wSlot, ct);
-    double r1 = hydRadAt<kCold>(x, y1, ct);
-    wSlot = slotWidth<kFast>(p, x, y2);
-    double a2 = areaAt<kCold>(x, y2, wSlot, ct);
+    double a1, r1, a2, aMid, rMid;
     double yMid = 0.5 * (y1 + y2);
-    wSlot = slotWidth<kFast>(p, x, yMid);
-    double aMid = areaAt<kCold>(x, yMid, wSlot, ct);
-    double rMid = hydRadAt<kCold>(x, yMid, ct);
+    if constexpr (kFast) {
+        // (yMid is dMid: both ends are at least 0.0001, so the floor never
+        // applies; checked, with the index part recomputed otherwise)
+        if (yMid != dMidF) {
+            ndM = normDepth(x, yMid);
+            cM = circIdx(ndM);
+            wMidF = circWidthAt(p, x, ndM, cM, ct);
+        }
+        a1 = circAreaAt(x, y1, c1, ct);
+        r1 = circHydRadAt(x, y1, c1, ct);
+        a2 = circAreaAt(x, y2, c2, ct);
+        aMid = circAreaAt(x, yMid, cM, ct);
+        rMid = circHydRadAt(x, yMid, cM, ct);
+    } else {
+        double wSlot = slotWidth<kFast>(p, x, y1);
+        a1 = areaAt<kCold>(x, y1, wSlot, ct);
+        r1 = hydRadAt<kCold>(x, y1, ct);
+        wSlot = slotWidth<kFast>(p, x, y2);
+        a2 = areaAt<kCold>(x, y2, wSlot, ct);
+        wSlot = slotWidth<kFast>(p, x, yMid);
+        aMid = areaAt<kCold>(x, yMid, wSlot, ct);
+        rMid = hydRadAt<kCold>(x, yMid, ct);
+    }
     bool isFull = (y1 >= x.yFull && y2 >= x.yFull);
     double len0 = pre ? pre->len0 : p.length[j];
 
@@ -815,7 +891,9 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
 
     double v = qLast / aMid;
     if (fabs(v) > 50.) v = 50. * gsgn(qLast);
-    double froude = linkFroude<kCold>(x, v, yMid, ct);
+    double froude;
+    if constexpr (kFast) froude = circFroude(p, x, v, yMid, ndM, cM, aMid, wMidF, ct);
+    else froude = linkFroude<kCold>(x, v, yMid, ct);
     SWX_LST(froude, froude);
     if (fc == F_SUBCRIT && froude > 1.0) fc = F_SUPCRIT;
 
@@ -890,7 +968,9 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
                 if (y1 < y2) check = true;
             if (!check && (p.normalFlowLtd == NFL_FROUDE || p.normalFlowLtd == NFL_BOTH) && !hasOutfall) {
                 if (y1 > 0.0001 && y2 > 0.0001) {
-                    double f1 = linkFroude<kCold>(x, q / a1, y1, ct);
+                    double f1;
+                    if constexpr (kFast) f1 = circFroude(p, x, q / a1, y1, nd1, c1, a1, w1F, ct);
+                    else f1 = linkFroude<kCold>(x, q / a1, y1, ct);
                     if (f1 >= 1.0) check = true;
                 }
             }

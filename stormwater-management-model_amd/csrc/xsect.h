@@ -84,27 +84,45 @@ SWX_HD double amaxRatio(int t)
 }
 SWX_HD int isOpen(int t) { return amaxRatio(t) >= 1.0 ? 1 : 0; }     // xsect.c:204-212
 
+// lookup on the circular tables (n = 51) in two parts: the index part at x
+// (CircIdx: the entry, x - x0 and the quadratic term's factor), which every
+// table evaluated at the same depth shares, and the table part.  The two
+// divisions by the step are divisions by a known constant (divdd.h),
+// bit-identical; on the device lookup() below is circLookup(circIdx(x), t).
+struct CircIdx {
+    int i;
+    double dx;                // x - x0
+    double q;                 // (x - x0)(x - x1) / delta^2 (i < 2)
+};
+SWX_HD CircIdx circIdx(double x)
+{
+    const double delta = kCircDelta;
+    CircIdx c;
+    c.i = (int)divDD(x, delta, kCircDeltaRh, kCircDeltaRl);
+    const double x0 = c.i * delta;
+    const double x1 = ((double)c.i + 1) * delta;
+    c.dx = x - x0;
+    c.q = (c.i < 2) ? divDD((x - x0) * (x - x1), kCircDelta2, kCircDelta2Rh, kCircDelta2Rl) : 0.0;
+    return c;
+}
+SWX_HD double circLookup(const CircIdx& c, const double* t)
+{
+    const int n = SWX_CIRC_N, i = c.i;
+    if (i >= n - 1) return t[n - 1];
+    double y = t[i] + divDD(c.dx * (t[i + 1] - t[i]), kCircDelta, kCircDeltaRh, kCircDeltaRl);
+    if (i < 2) {
+        double y2 = y + c.q * (t[i] / 2.0 - t[i + 1] + t[i + 2] / 2.0);
+        if (y2 > 0.0) y = y2;
+    }
+    if (y < 0.0) y = 0.0;
+    return y;
+}
+
 // xsect.c:1474-1507 -- uniform table lookup, quadratic near the origin
 SWX_HD double lookup(double x, const double* t, int n)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
-    // the circular tables (n = 51): the two divisions by the step are
-    // divisions by a known constant (divdd.h), bit-identical
-    if (n == SWX_CIRC_N) {
-        const double delta = kCircDelta;
-        int i = (int)divDD(x, delta, kCircDeltaRh, kCircDeltaRl);
-        if (i >= n - 1) return t[n - 1];
-        double x0 = i * delta;
-        double x1 = ((double)i + 1) * delta;
-        double y = t[i] + divDD((x - x0) * (t[i + 1] - t[i]), delta, kCircDeltaRh, kCircDeltaRl);
-        if (i < 2) {
-            double y2 = y + divDD((x - x0) * (x - x1), kCircDelta2, kCircDelta2Rh, kCircDelta2Rl) *
-                            (t[i] / 2.0 - t[i + 1] + t[i + 2] / 2.0);
-            if (y2 > 0.0) y = y2;
-        }
-        if (y < 0.0) y = 0.0;
-        return y;
-    }
+    if (n == SWX_CIRC_N) return circLookup(circIdx(x), t);
 #endif
 
     double delta = 1.0 / ((double)n - 1);
