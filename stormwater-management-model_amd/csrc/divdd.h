@@ -31,6 +31,17 @@ SWX_DIV_HD double divDD(double a, double b, double rh, double rl)
     return fma(r, rh, q0);
 }
 
+// the reciprocal pair of b computed in place (device and host): one division
+// and an FMA; rl = (1 - b*rh) * rh carries 1/b - rh to ~2^-105 relative, so
+// divDD's q0 stays within one ulp and its result is RN(a/b) (Markstein);
+// for a divisor several quotients share (tests/c/divdd_check.cpp)
+SWX_DIV_HD void recipDDFast(double b, double* rh, double* rl)
+{
+    const double h = 1.0 / b;
+    *rh = h;
+    *rl = fma(-b, h, 1.0) * h;
+}
+
 // the reciprocal pair of b (host side, at set-up)
 inline void recipDD(double b, double* rh, double* rl)
 {

@@ -922,11 +922,16 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     // where all three reference builds agree
     else dq1 = dt * (pre ? pre->roughFactor : p.roughFactor[j]) / (kFast ? swxPowFriction(rWtd) : pow(rWtd, 1.33333)) *
                fabs(v);
-    double dq2 = dt * 32.2 * aWtd * (h2 - h1) / length;
+    // the three quotients by the conduit's length and the two by the
+    // momentum denominator share a reciprocal pair each (divdd.h
+    // recipDDFast: RN(a / b) exactly, with one division per divisor)
+    double rLh, rLl;
+    recipDDFast(length, &rLh, &rLl);
+    double dq2 = divDD(dt * 32.2 * aWtd * (h2 - h1), length, rLh, rLl);
     double dq3 = 0.0, dq4 = 0.0;
     if (sigma > 0.0) {
         dq3 = 2.0 * v * (aMid - aOld) * sigma;
-        dq4 = dt * v * v * (a2 - a1) / length * sigma;
+        dq4 = divDD(dt * v * v * (a2 - a1), length, rLh, rLl) * sigma;
     }
     double dq5 = 0.0;
     if (f & LF_LOSSES) {                                        // dwflow.c:554-571
@@ -949,8 +954,10 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     }
 
     double denom = 1.0 + dq1 + dq5;
-    double q = (qOld - dq2 + dq3 + dq4 + dq6) / denom;
-    double dqdhV = 1.0 / denom * 32.2 * dt * aWtd / length * barrels;
+    double rDh, rDl;                                   // rDh = 1.0 / denom
+    recipDDFast(denom, &rDh, &rDl);
+    double q = divDD(qOld - dq2 + dq3 + dq4 + dq6, denom, rDh, rDl);
+    double dqdhV = divDD(rDh * 32.2 * dt * aWtd, length, rLh, rLl) * barrels;
 
     int normalFlow = 0, inletCtl = 0;
     const int culvert = kCold ? (int)((f >> LF_CULVERT_SHIFT) & 0x3F) : 0;

@@ -57,6 +57,21 @@ int main(int argc, char** argv)
         check(b, b, rh, rl);
         check(0.5 * b, b, rh, rl);
     }
+    // the in-kernel pair (recipDDFast) for the momentum terms' shared
+    // divisors -- conduit lengths and the momentum denominator -- with
+    // numerators of either sign over many decades
+    std::uniform_real_distribution<double> le(-3.0, 7.0), ae(-30.0, 12.0);
+    for (long i = 0; i < n / 2; i++) {
+        double b = std::pow(10.0, le(g));
+        recipDDFast(b, &rh, &rl);
+        if (rh != 1.0 / b) { printf("recipDDFast rh\n"); return 2; }
+        for (int m = 0; m < 3; m++) {
+            double a = std::pow(10.0, ae(g)) * ((g() & 1) ? -1.0 : 1.0);
+            check(a, b, rh, rl);
+        }
+        check(b * 0.999, b, rh, rl);
+        check(1.0, b, rh, rl);
+    }
     printf("checked %ld quotients, %ld mismatches\n", tried, bad);
     return bad ? 1 : 0;
 }
