@@ -174,6 +174,10 @@ struct StatsDev {
     double *sAvgVol, *sMaxVol, *sMaxVolDate, *sMaxFlow, *sEvap, *sExfil;
 };
 
+struct RareLink {
+    const double *cIn, *cOut, *cAvg, *qLimit;
+    double *evapLoss, *seepLoss;
+};
 struct Params {
     int nN, nL, P, maxTrials;
     // options
@@ -339,6 +343,11 @@ struct Params {
     // statistics, 32 Courant limits, 64 capacity-limited state
     int endSkip;
     int qualUnfreeze;             // k_qual_node also does k_unfreeze's work (launchStep)
+    // the link arrays only conduits with local losses, a flow limit or
+    // seepage touch, behind one pointer: the streaming conduit update reads
+    // them through it inside those branches, so their base addresses are not
+    // held in scalar registers across its loop (kFast)
+    const struct RareLink* rare;
     const int* coldLinks;         // LF_COLD conduits, ascending
     const int* outLinks;          // conduits with an outfall end, ascending
     int outInl0, outInl1, outInl2, outInl3;   // outLinks[0..3] (-1: none), read without a load
@@ -881,8 +890,13 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         SWX_LST(lNewVolume, a1n * len0 * barrels);
         SWX_LST(lNewFlow, 0.0);
         if (f & LF_SEEP) {            // always 0 without LF_SEEP: not rewritten
-            SWX_LST(evapLoss, 0.0);
-            SWX_LST(seepLoss, 0.0);
+            if constexpr (kFast && !kWT) {
+                p.rare->evapLoss[j] = 0.0;
+                p.rare->seepLoss[j] = 0.0;
+            } else {
+                SWX_LST(evapLoss, 0.0);
+                SWX_LST(seepLoss, 0.0);
+            }
         }
         int old = pre ? pre->lstate : p.lstate[j];
         SWX_LST(lstate, (old & ~0xF) | fc);   // fullState / normalFlow / inletControl untouched (dwflow.c:165-180)
@@ -936,9 +950,15 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     double dq5 = 0.0;
     if (f & LF_LOSSES) {                                        // dwflow.c:554-571
         double losses = 0.0, qa = fabs(qLast);
-        if (a1 > 0.0001) losses += p.cIn[j] * (qa / a1);
-        if (a2 > 0.0001) losses += p.cOut[j] * (qa / a2);
-        if (aMid > 0.0001) losses += p.cAvg[j] * (qa / aMid);
+        const double *cIn = p.cIn, *cOut = p.cOut, *cAvg = p.cAvg;
+        if constexpr (kFast && !kWT) {
+            cIn = p.rare->cIn;
+            cOut = p.rare->cOut;
+            cAvg = p.rare->cAvg;
+        }
+        if (a1 > 0.0001) losses += cIn[j] * (qa / a1);
+        if (a2 > 0.0001) losses += cOut[j] * (qa / a2);
+        if (aMid > 0.0001) losses += cAvg[j] * (qa / aMid);
         dq5 = losses / 2.0 / length * dt;
     }
     double dq6 = 0.0;
@@ -996,7 +1016,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         if (q * qLast < 0.0) q = 0.001 * gsgn(q);
     }
     if (f & LF_QLIMIT) {
-        double ql = p.qLimit[j];
+        double ql = (kFast && !kWT) ? p.rare->qLimit[j] : p.qLimit[j];
         if (fabs(q) > ql) q = gsgn(q) * ql;
     }
     // link_setFlapGate (link.c:643-670)
@@ -1026,8 +1046,13 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     SWX_LST(lNewVolume, aAvg * len0 * barrels);
     SWX_LST(lNewFlow, q * barrels);
     if (f & LF_SEEP) {
-        SWX_LST(evapLoss, evapRate);
-        SWX_LST(seepLoss, seepRate);
+        if constexpr (kFast && !kWT) {
+            p.rare->evapLoss[j] = evapRate;
+            p.rare->seepLoss[j] = seepRate;
+        } else {
+            SWX_LST(evapLoss, evapRate);
+            SWX_LST(seepLoss, seepRate);
+        }
     }
     int old = pre ? pre->lstate : p.lstate[j];
     SWX_LST(lstate, (old & (1 << 9)) | fc | (fs << 4) | (normalFlow << 8) | (inletCtl << 10));
@@ -5231,6 +5256,13 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     UPD(p.evapLoss, gl(st.evapLossRate), nL);
     UPD(p.seepLoss, gl(st.seepLossRate), nL);
     UPD(p.setting, gl(st.setting), nL);
+    {                                              // Params::rare
+        const RareLink rl{p.cIn, p.cOut, p.cAvg, p.qLimit, p.evapLoss, p.seepLoss};
+        RareLink* dr = devAlloc<RareLink>(d, 1, &e);
+        if (e == hipSuccess) e = hipMemcpy(dr, &rl, sizeof(RareLink), hipMemcpyHostToDevice);
+        if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+        p.rare = dr;
+    }
     {
         std::vector<int> ls(nL);
         for (int j = 0; j < nL; j++) {

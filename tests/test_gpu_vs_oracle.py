@@ -320,6 +320,52 @@ def test_fused_quality_bitwise(tmp_path, monkeypatch):
     assert runs[0][0].max() > 0.0
 
 
+@pytest.mark.gpu
+def test_fast_conduits_with_losses_match_oracle(tmp_path):
+    """The all-circular streaming conduit update (kFast) on conduits with the
+    rarer terms -- entry / exit / average local losses, seepage (its
+    evaporation and seepage loss rates in the node sums) and a flow limit
+    (dwflow.c:554-571, link.c:1334-1399, dwflow.c:272-276): a 30 x 30
+    variable-step grid with those on every 5th / 7th conduit, lockstep with
+    the oracle from the initial state for 150 steps, every step compared at
+    1e-6."""
+    inp = str(tmp_path / "g.inp")
+    netgen.write_grid(inp, 30, 30, end_time="02:00:00", route_step=5.0, variable_step=0.75, diameter=1.0, q=0.2)
+    text = open(inp).read()
+    head, rest = text.split("[CONDUITS]\n", 1)
+    cond, tail = rest.split("\n\n", 1)
+    lines = cond.splitlines()
+    losses = []
+    for k, line in enumerate(lines):
+        w = line.split()
+        if k % 7 == 3:
+            w[-1] = "1.2"                            # MaxFlow: a flow limit
+        if k % 5 == 1:
+            losses.append("%s 0.5 0.3 0.1 NO %g" % (w[0], 0.2 + 0.1 * (k % 3)))
+        lines[k] = " ".join(w)
+    out = head + "[CONDUITS]\n" + "\n".join(lines) + "\n\n" + tail
+    out += "\n[LOSSES]\n" + "\n".join(losses) + "\n"
+    open(inp, "w").write(out)
+    s = _engine(inp, tmp_path)
+    dump = str(tmp_path / "init.bin")
+    assert s.export_state(dump) == 0
+    d = read_dump(dump)
+    assert (d["link.cLossInlet"] > 0).sum() > 100 and (d["link.qLimit"] > 0).sum() > 100
+    assert (d["link.seepRate"] > 0).sum() > 100
+    o = oracle_from_dump(d)
+    _set_lat(o, 0.2)
+    for k in range(150):
+        it = o.step(o.routing_step(d["opt.d"][0]))
+        err, _ = s.step()
+        assert err == 0, s.getError()
+        assert s.counters()["last_iterations"] == it, k
+        _compare(s, o, "step %d" % k)
+    c = s.counters()
+    assert c["nonconverged"] == o.get("nonConverge")
+    s.end()
+    s.close()
+
+
 def _regulator_grid(tmp_path, n=40, pollutants=0):
     """An n x n surcharged variable-step grid in which three conduits become
     a side orifice, a transverse weir and a functional outlet, and a fourth a
