@@ -192,8 +192,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--timing-steps", type=int, default=10)
     ap.add_argument("--kernel-reps", type=int, default=20)
-    ap.add_argument("--exchange", choices=["rccl", "host"], default="rccl",
-                    help="multi-GPU transport (host = gloo through the host: rehearsal on one GPU)")
+    ap.add_argument("--exchange", choices=["ipc", "rccl", "host"], default="ipc",
+                    help="multi-GPU transport: ipc = each rank's kernels store the ghost-link values, "
+                         "convergence flags and Courant limits into its peers' memory (no collective inside a "
+                         "step; falls back to rccl if its start-up handshake fails); rccl = captured ncclSend/"
+                         "ncclRecv + ncclAllReduce; host = gloo through the host (rehearsal on one GPU)")
     ap.add_argument("--rccl-1rank", action="store_true",
                     help="one GPU through the partitioned RCCL code path (captured neighbour send/recv and "
                          "flag all-reduce every Picard iteration): the in-graph cost of the collectives")
@@ -250,13 +253,17 @@ def main():
         s.set_partition(rank, world, bytes(idt.numpy().tobytes()))
     elif args.rccl_1rank:
         s.set_partition(0, 1, s.nccl_unique_id())
-    if world > 1 and args.exchange == "host":
+    if world > 1 and args.exchange in ("host", "ipc"):
         # host transport (gloo through torch.distributed): the rehearsal of
-        # the multi-rank path with several ranks on one GPU
+        # the multi-rank path with several ranks on one GPU; the IPC transport
+        # is bootstrapped over the same callback (IPC handles at swmm_start,
+        # the result gathers at report times and at swmm_end)
         def xchg(arr, op):
             t = torch.from_numpy(arr)
             dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MIN)
         s.set_exchange(xchg)
+        if args.exchange == "ipc":
+            s.set_transport("ipc")
     tmpd = "/tmp/swmm_bench"
     err = s.open(inp, os.path.join(tmpd, "r%d.rpt" % rank), os.path.join(tmpd, "r%d.out" % rank))
     if err:
@@ -265,6 +272,7 @@ def main():
     if err:
         raise SystemExit("swmm_start failed: %s" % (s.getError(),))
     backend = s.backend()
+    transport = s.transport()
     if not backend.startswith("hip:"):
         raise SystemExit("HIP backend not active: " + backend)
     nL = s.getCount(swmm5.LINK)
@@ -513,13 +521,16 @@ def main():
                        "parallelism": ("link-partitioned x%d (row strips); per Picard iteration "
                                        "%s of the strip neighbours' ghost-link values and an "
                                        "all-reduce(max) of the convergence flag"
-                                       % (world, "RCCL ncclSend/ncclRecv" if args.exchange == "rccl"
-                                          else "host-transport (gloo) exchange"))
+                                       % (world, {"ipc": "device stores into the peers' memory (IPC)",
+                                                  "rccl": "RCCL ncclSend/ncclRecv"}.get(
+                                                      transport.split()[0], "host-transport (gloo) exchange"))
+                                       )
                                       if world > 1 else
                                       ("single rank through the partitioned RCCL path (captured ncclSend/"
                                        "ncclRecv and flag all-reduce every Picard iteration)"
                                        if args.rccl_1rank else "single"),
-                       "backend": backend},
+                       "backend": backend,
+                       "transport": transport},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

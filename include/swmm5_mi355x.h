@@ -129,6 +129,23 @@ int    DLLEXPORT swmmx_setPartition(int rank, int nranks, const void *ncclId, in
  * then run as eager launches.  fn = NULL restores RCCL. */
 int    DLLEXPORT swmmx_setExchange(int (*fn)(double *buf, long n, int op, void *user), void *user);
 
+/* Transport of the per-iteration exchange (after swmmx_setPartition and any
+ * swmmx_setExchange, before swmm_start): 0 RCCL, 1 the host callback, 2 IPC --
+ * each rank's kernels store the ghost links' values, the convergence flag and
+ * the per-step reductions straight into the peers' memory (an uncached region
+ * mapped with hipIpcOpenMemHandle), no collective library inside a step.  IPC
+ * is bootstrapped over the host callback when one is set, else over RCCL; if
+ * its start-up handshake fails on any rank every rank falls back to RCCL (with
+ * a unique id) or the host callback.  Every wait behind an exchange is bounded
+ * (SWMM5_XCHG_TIMEOUT seconds, default 60): a rank that stops answering makes
+ * every rank's swmm_step return error 500 instead of hanging.  Returns 0, or
+ * 500 for an unknown kind (or 1 without a callback). */
+int    DLLEXPORT swmmx_setTransport(int kind);
+
+/* The transport in use after swmm_start ("single", "rccl", "host", "ipc", or
+ * a fallback note), written into buf. */
+int    DLLEXPORT swmmx_getTransport(char *buf, int size);
+
 /* Owning rank of every node (objType swmm_NODE) or link (swmm_LINK) under the
  * current partition; returns the object count. */
 int    DLLEXPORT swmmx_getOwner(int objType, int *out, int n);

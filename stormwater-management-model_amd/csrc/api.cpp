@@ -83,9 +83,21 @@ int syncMirror()
 // step is not covered: that would need an exchange every step.)
 static int syncError()
 {
-    if (!G || !G->router || !G->router->ok() || !G->router->partition().active()) return G ? G->errorCode : 501;
+    if (!G) return 501;
+    if (!gPart.active()) return G->errorCode;
     double e = -(double)G->errorCode;
-    if (G->router->allreduceHost(&e, 1, 1)) return setErr(G->router->lastError(), G->router->lastErrorMsg());
+    // every rank joins, whatever its own state: over the host callback when
+    // one is set (it needs no router), else over the router's communicator;
+    // a rank with neither (RCCL before its communicator exists) cannot reach
+    // the others
+    if (gPart.xchg) {
+        if (gPart.xchg(&e, 1, 1, gPart.xuser))
+            return setErr(500, "ERROR 500: multi-GPU error exchange failed");
+    } else if (G->router && G->router->ok()) {
+        if (G->router->allreduceHost(&e, 1, 1)) return setErr(G->router->lastError(), G->router->lastErrorMsg());
+    } else {
+        return G->errorCode;
+    }
     if (e < 0.0 && !G->errorCode)
         setErr((int)-e, "ERROR " + std::to_string((int)-e) + ": reported by another rank.");
     return G->errorCode;
@@ -192,8 +204,11 @@ int DLLEXPORT swmm_start(int saveFlag)
         if (prj.net.nodeType[j] == STORAGE) prj.stats.stInitVol[j] = prj.st.newVolume[j];
     G->router.reset(new Router());
     int dev = (gDevice >= 0) ? gDevice : defaultDevice();
-    if (G->router->init(prj, dev, gPart.active() ? &gPart : nullptr))
-        return setErr(G->router->lastError(), G->router->lastErrorMsg());
+    if (G->router->init(prj, dev, gPart.active() ? &gPart : nullptr)) {
+        setErr(G->router->lastError(), G->router->lastErrorMsg());
+        if (gPart.active()) syncError();            // the other ranks wait in the same exchange
+        return G->errorCode;
+    }
     if (openFailed) setErr(307, "ERROR 307: cannot open binary results file.");
     if (gPart.active() && syncError()) return G->errorCode;
     G->isStarted = true;
@@ -415,6 +430,9 @@ int DLLEXPORT swmm_stride(int strideStep, double* elapsedTime)   // swmm5.c:466-
     if (G->errorCode) return G->errorCode;
     if (!G->isOpen) return (G->errorCode = 501);
     if (!G->isStarted || G->hostOnly) return (G->errorCode = 502);
+    if (G->stateSpent)
+        return setErr(500, "ERROR 500: the state was advanced by swmmx_timeKernel (measurement only); "
+                           "the run cannot continue.");
     Project& prj = *G->prj;
     double realRouteStep = prj.opt.routeStep;
     const double durPrev = G->routingDuration;           // in force at the last step's end
@@ -549,13 +567,19 @@ int DLLEXPORT swmm_end(void)   // swmm5.c:618-660
             G->router->allreduceHost(G->flowTot, 6, 0);   // per-rank totals (multi-GPU)
             G->flowError = computeFlowError();
             G->out.end(G->errorCode);                   // (output_end: its write errors are not reported)
-            if (!G->errorCode) writeReportSummary();
+            // after swmmx_timeKernel the state is not a routed one: no summary
+            // tables and no hot start file from it (the report says why)
+            if (G->stateSpent && G->rpt)
+                fprintf(G->rpt, "\n  Summary tables and hot start file omitted: the state was advanced by "
+                                "swmmx_timeKernel (measurement only).\n");
+            if (!G->errorCode && !G->stateSpent) writeReportSummary();
             // hotstart_close (swmm5.c:647): the final state as a hot start
             // file (several GPUs: gathered from the owners, written by rank 0)
             const Partition& part = G->router->partition();
             if (part.active()) syncError();
-            if (!G->errorCode && !G->prj->hotstartSave.empty() && part.active()) gatherMirror();
-            if (!G->errorCode && (!part.active() || part.rank == 0) && G->prj->saveHotstart())
+            const bool saveHs = !G->errorCode && !G->stateSpent && !G->prj->hotstartSave.empty();
+            if (saveHs && part.active()) gatherMirror();
+            if (saveHs && !G->errorCode && (!part.active() || part.rank == 0) && G->prj->saveHotstart())
                 setErr(G->prj->errorCode, G->prj->errorMsg);
             if (part.active()) syncError();
         }
@@ -1217,6 +1241,9 @@ int DLLEXPORT swmmx_ncclUniqueId(void* out, int bytes)
 {
     if (!out || bytes < (int)sizeof(ncclUniqueId)) return -1;
     ncclUniqueId id;
+    // the root's bootstrap address: the loopback interface unless the caller
+    // chose one (single node; an unset interface makes RCCL probe the host's)
+    setenv("NCCL_SOCKET_IFNAME", "lo", 0);
     if (ncclGetUniqueId(&id) != ncclSuccess) return -2;
     memcpy(out, &id, sizeof id);
     return (int)sizeof id;
@@ -1242,6 +1269,21 @@ int DLLEXPORT swmmx_setExchange(int (*fn)(double*, long, int, void*), void* user
     gPart.transport = fn ? XCHG_HOST : XCHG_RCCL;
     gPart.xchg = fn;
     gPart.xuser = user;
+    return 0;
+}
+
+int DLLEXPORT swmmx_setTransport(int kind)
+{
+    if (kind < XCHG_RCCL || kind > XCHG_IPC) return 500;
+    if (kind == XCHG_HOST && !gPart.xchg) return 500;
+    gPart.transport = kind;
+    return 0;
+}
+
+int DLLEXPORT swmmx_getTransport(char* buf, int size)
+{
+    std::string s = (G && G->router && G->router->ok()) ? G->router->transport() : std::string("none");
+    if (buf && size > 0) snprintf(buf, (size_t)size, "%s", s.c_str());
     return 0;
 }
 

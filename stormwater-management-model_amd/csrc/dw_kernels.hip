@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstddef>
 #include <map>
 #include <cmath>
@@ -36,6 +37,8 @@
 #include <cstring>
 #include <string>
 #include <vector>
+
+#include <unistd.h>
 
 #include <rccl/rccl.h>
 
@@ -52,6 +55,15 @@ namespace swx {
         hipError_t e_ = (x);                                                         \
         if (e_ != hipSuccess) {                                                      \
             fail(std::string(#x) + ": " + hipGetErrorString(e_));                    \
+            return err_ ? err_ : 500;                                                \
+        }                                                                            \
+    } while (0)
+
+// a bounded wait (waitDone) inside a Router method: its message becomes the router's error
+#define WAITCHECK(x)                                                                 \
+    do {                                                                             \
+        if ((x) != 0) {                                                              \
+            fail(d_->xerrMsg);                                                       \
             return err_ ? err_ : 500;                                                \
         }                                                                            \
     } while (0)
@@ -143,6 +155,11 @@ struct StepCtl {
     // flow error was within SYS_FLOW_TOL (k_finalize); steadyChanged -- a
     // lateral or outfall inflow changed by more than LAT_FLOW_TOL (k_steady)
     int steadyOk, steadyChanged;
+    // several ranks: [0..5] this step's system inflow / outflow rates for the
+    // flow-error test, summed over the ranks between k_finalize's phases;
+    // [6] > 0 when some rank's k_steady saw a changed inflow or a pump to
+    // switch (summed over the ranks before the step's iterations)
+    double steadyIO[8];
     double stepRed[kNumPartials];     // this step's reduced block partials (k_finalize)
     // run statistics (stats.c): report-period step count / span, max system
     // outfall flow, routing time-step statistics (stats_updateTimeStepStats)
@@ -155,6 +172,30 @@ struct StepCtl {
     long long tsCounts[kTimeLevels];
     double tsIntervals[kTimeLevels];
 };
+
+// ---- device-initiated multi-GPU exchange (XCHG_IPC) ----
+// Every rank owns one uncached region (hipDeviceMallocUncached) that its peers
+// map with hipIpcOpenMemHandle and write with 8-byte system-scope stores; the
+// owner polls it.  Each 8-byte word is one granule {seq in the high 32 bits,
+// 32 payload bits} written by ONE store, so a reader that sees the expected
+// seq holds the payload without any fence (cdna guide, Guideline 16 R2); a
+// double travels as two granules.  The sequence numbers live per rank in
+// XCtl, advance identically on every rank (every rank runs the same
+// exchanges: an iteration after convergence skips them everywhere), and pick
+// one of two buffers by parity, so a fast rank can run one exchange ahead
+// of a slow one without overwriting what the slow one has not read.
+struct XCtl {
+    unsigned ghostSeq;            // per-iteration ghost-link exchange (bumped by k_ipc_flag)
+    unsigned qualSeq;             // per-step ghost concentrations (bumped by k_finalize)
+    unsigned flagSeq;             // per-iteration convergence flag (k_ipc_flag)
+    unsigned redSeq;              // small all-reduces (k_ipc_reduce: Courant limits, steady test)
+};
+struct XPeer {                    // a neighbour's receive areas, as mapped into this process
+    unsigned long long *ghost, *qual;
+    int nGhost, pad;
+};
+constexpr int kRedMax = 8;        // doubles per k_ipc_reduce
+enum { XK_GHOST = 1, XK_QUAL, XK_FLAG, XK_RED, XK_HELLO };
 
 // device run statistics (stats.c TNodeStats / TLinkStats / TOutfallStats and
 // massbal.c NodeInflow / NodeOutflow), one SoA array per field
@@ -379,13 +420,34 @@ struct Params {
     // 236-244; StepCtl::steadyOk / steadyChanged, stepIsSteady)
     int skipSteady;
     double sysFlowTol, latFlowTol;
+    // ---- XCHG_IPC (the structs above): ghost links' values, the convergence
+    // flag and the per-step reductions go straight into the peers' memory
+    int ipc;                      // 1: this transport
+    int xRank, xRanks;            // rank and rank count (xRanks <= 64: one wave)
+    const XPeer* xpeer;           // [nbr] the neighbours' ghost / quality areas
+    const int* sendNbr;           // per send entry: neighbour index k
+    const int* sendGi;            // per send entry: ghost index at that neighbour
+    const int* ghostFrom;         // per ghost: sending rank (error reports)
+    unsigned long long* ghostRx;  // [2][2 xF][nGhost] granules received
+    unsigned long long* qualRx;   // [2][2 P][nGhost]
+    unsigned long long* flagRx;   // [2][xRanks]
+    unsigned long long* redRx;    // [2][xRanks][2 kRedMax]
+    unsigned long long* abortW;   // this rank's abort word (any rank sets it)
+    unsigned long long* const* peerFlag;    // [xRanks] every rank's flagRx (own included)
+    unsigned long long* const* peerRed;     // [xRanks] redRx
+    unsigned long long* const* peerAbort;   // [xRanks] abort words
+    XCtl* xctl;
+    int* xerr;                    // host-mapped failure record {code, kind, rank, seq}
+    const int* hostAbort;         // host-mapped: the host gave up waiting
+    long long xTimeout;           // wall-clock ticks a wait may take
+    long long stallStep;          // test hook (SWMM5_XCHG_STALL): from this step on this rank posts nothing
 };
 // this step is skipped as steady (isInSteadyState, routing.c:383-395): read by
 // the launches of Picard iterations 0 and 1 (the later ones see iteration 1's
 // convergence flag, which a skipped step leaves at 0)
 __device__ __forceinline__ bool stepIsSteady(const Params& p)
 {
-    return p.skipSteady && p.ctl->steadyOk && !p.ctl->steadyChanged;
+    return p.skipSteady && p.ctl->steadyOk && !p.ctl->steadyChanged && !(p.ctl->steadyIO[6] > 0.0);
 }
 
 // ===========================================================================
@@ -2139,6 +2201,10 @@ __device__ __forceinline__ bool flowChanged(double qOld, double qNew, double tol
     else diff = 0.0;
     return fabs(diff) > tol;
 }
+// A pump whose on / off depth its inlet node has crossed gets a new setting
+// this step (evaluateControlRules' link_setTargetSetting, routing.c:269-296,
+// link.c:604-640): actionCount > 0, never steady (routing.c:388-391).  The
+// switch itself is made by k_nc<true> as in every routed step.
 __global__ __launch_bounds__(kBlock) void k_steady(Params p)
 {
     if (!p.ctl->steadyOk) return;                  // the step routes flow anyway
@@ -2149,7 +2215,17 @@ __global__ __launch_bounds__(kBlock) void k_steady(Params p)
         if ((int)(nf & NF_TYPE) == OUTFALL || (nf & NF_DEG0))
             changed = changed || flowChanged(p.oldFlowInflow[i], p.inflow[i], p.latFlowTol);
     }
-    if (__any(changed) && (threadIdx.x & 63) == 0) p.ctl->steadyChanged = 1;
+    for (int c = blockIdx.x * kBlock + threadIdx.x; c < p.nNC; c += gridDim.x * kBlock) {
+        const NcLink& L = p.ncL[c];
+        if (L.type != LK_PUMP) continue;
+        const int j = p.ncLinks[c];
+        const double set = p.setting[j], y1 = p.nNewDepth[p.lnodes[j].x];
+        if ((L.yOff > 0.0 && set > 0.0 && y1 < L.yOff) || (L.yOn > 0.0 && set == 0.0 && y1 > L.yOn)) changed = true;
+    }
+    if (__any(changed) && (threadIdx.x & 63) == 0) {
+        p.ctl->steadyChanged = 1;
+        p.ctl->steadyIO[6] = 1.0;                  // several ranks: summed over them (launchStep)
+    }
 }
 
 template <bool kFirst, bool kGeneral, bool kProbe = false>
@@ -3468,6 +3544,209 @@ __global__ __launch_bounds__(kBlock) void k_xunpack_qual(Params p)
             p.lQual[p.ctl->qualPar][(size_t)q * p.nLs + p.nL + g] = p.xrecv[(size_t)p.P * g + q];
 }
 
+// ---- XCHG_IPC kernels (XCtl above) -----------------------------------------
+// Per Picard iteration:  k_link(k) ─ k_ipc_pack ─ k_ipc_unpack ─ k_node(k)
+// ─ [k_nc] ─ k_ipc_flag.  k_ipc_pack stores this rank's sent links' values as
+// granules into each neighbour's ghost area; k_ipc_unpack polls its own area
+// until every ghost value of this exchange has arrived and writes the ghost
+// slots; k_ipc_flag (one wave) posts the iteration's convergence flag to
+// every rank and ORs the flags of all ranks into unconv[k] (dynwave.c:241-256:
+// the loop ends only when every node converged).  No host, no RCCL: two
+// remote-store rounds per iteration.  Every wait is bounded (p.xTimeout);
+// a rank that gives up records why (xerr, host-mapped) and sets every rank's
+// abort word, so the others stop waiting too and every rank's next
+// swmm_step reports the failure.
+__device__ __forceinline__ unsigned long long llLoad(const unsigned long long* w)
+{
+    return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void llStore(unsigned long long* w, unsigned seq, unsigned payload)
+{
+    __hip_atomic_store(w, ((unsigned long long)seq << 32) | payload, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool xAborted(const Params& p)
+{
+    return llLoad(p.abortW) != 0 ||
+           __hip_atomic_load(p.hostAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+// the iteration's launches run (the others exit at once on every rank alike)
+__device__ __forceinline__ bool iterRuns(const Params& p, int k)
+{
+    if (k >= 2 && p.unconv[k - 1] == 0) return false;
+    return !(k < 2 && stepIsSteady(p));
+}
+// test hook: this rank stops posting from step stallStep on (its peers time out)
+__device__ __forceinline__ bool xStalled(const Params& p)
+{
+    return p.stallStep >= 0 && p.ctl->totalSteps >= p.stallStep;
+}
+// poll one granule until it carries seq; false at the deadline or on an abort
+__device__ bool llWait(const Params& p, const unsigned long long* w, unsigned seq, unsigned* payload,
+                       unsigned long long t0)
+{
+    for (unsigned it = 0;; it++) {
+        const unsigned long long v = llLoad(w);
+        if ((unsigned)(v >> 32) == seq) {
+            *payload = (unsigned)v;
+            return true;
+        }
+        if ((it & 15) == 15) {
+            if (xAborted(p)) return false;
+            if ((long long)(wall_clock64() - t0) > p.xTimeout) return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+// a wait gave up: the record for the host (first writer's fields may mix with
+// a concurrent one's; any of them is a true failure) and every rank's abort
+__device__ void xFail(const Params& p, int kind, int peer, unsigned seq)
+{
+    const bool byPeer = xAborted(p);
+    __hip_atomic_store(&p.xerr[1], kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&p.xerr[2], peer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&p.xerr[3], (int)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&p.xerr[0], byPeer ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!byPeer)
+        for (int r = 0; r < p.xRanks; r++) llStore(p.peerAbort[r], 0u, 1u);
+    __threadfence_system();
+}
+__device__ __forceinline__ double llDouble(unsigned lo, unsigned hi)
+{
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <bool kQual>
+__global__ __launch_bounds__(kBlock) void k_ipc_pack(Params p, int k)
+{
+    if (!kQual && !iterRuns(p, k)) return;
+    if (xAborted(p) || xStalled(p)) return;
+    const unsigned seq = (kQual ? p.xctl->qualSeq : p.xctl->ghostSeq) + 1;
+    const int par = seq & 1, F = kQual ? p.P : p.xF;
+    const double* lq = kQual ? p.lQual[p.ctl->qualPar] : nullptr;
+    for (int e = blockIdx.x * kBlock + threadIdx.x; e < p.nSend; e += gridDim.x * kBlock) {
+        const int l = p.sendLink[e];
+        const XPeer X = p.xpeer[p.sendNbr[e]];
+        const int gi = p.sendGi[e];
+        const size_t nG = (size_t)X.nGhost;
+        unsigned long long* b = (kQual ? X.qual : X.ghost) + (size_t)par * 2 * F * nG + gi;
+        for (int f = 0; f < F; f++) {
+            double v;
+            if (kQual) v = lq[(size_t)f * p.nLs + l];
+            else v = f == 0 ? p.lNewFlow[l] : f == 1 ? p.sa1[l] : f == 2 ? p.sa2[l] : f == 3 ? p.dqdh[l]
+                   : f == 4 ? p.evapLoss[l] : p.seepLoss[l];
+            const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
+            llStore(b + (size_t)(2 * f) * nG, seq, (unsigned)bits);
+            llStore(b + (size_t)(2 * f + 1) * nG, seq, (unsigned)(bits >> 32));
+        }
+    }
+}
+template <bool kQual>
+__global__ __launch_bounds__(kBlock) void k_ipc_unpack(Params p, int k)
+{
+    if (!kQual && !iterRuns(p, k)) return;
+    if (xAborted(p)) return;
+    const unsigned seq = (kQual ? p.xctl->qualSeq : p.xctl->ghostSeq) + 1;
+    const int par = seq & 1, F = kQual ? p.P : p.xF;
+    const size_t nG = (size_t)p.nGhost;
+    const unsigned long long t0 = wall_clock64();
+    const unsigned long long* b = (kQual ? p.qualRx : p.ghostRx) + (size_t)par * 2 * F * nG;
+    double* lq = kQual ? p.lQual[p.ctl->qualPar] : nullptr;
+    for (int g = blockIdx.x * kBlock + threadIdx.x; g < p.nGhost; g += gridDim.x * kBlock) {
+        const int l = p.nL + g;
+        for (int f = 0; f < F; f++) {
+            unsigned lo = 0, hi = 0;
+            if (!llWait(p, b + (size_t)(2 * f) * nG + g, seq, &lo, t0) ||
+                !llWait(p, b + (size_t)(2 * f + 1) * nG + g, seq, &hi, t0)) {
+                xFail(p, kQual ? XK_QUAL : XK_GHOST, p.ghostFrom[g], seq);
+                return;
+            }
+            const double v = llDouble(lo, hi);
+            if (kQual) lq[(size_t)f * p.nLs + l] = v;
+            else if (f == 0) p.lNewFlow[l] = v;
+            else if (f == 1) p.sa1[l] = v;
+            else if (f == 2) p.sa2[l] = v;
+            else if (f == 3) p.dqdh[l] = v;
+            else if (f == 4) p.evapLoss[l] = v;
+            else p.seepLoss[l] = v;
+        }
+    }
+}
+// One wave: iteration k's flag from every rank, ORed into unconv[k] (the
+// all-reduce(max) of the RCCL transport); kHello: the start-up handshake
+// (flag exchange number 1 with every rank's flag 1; *out = 1 when it worked)
+template <bool kHello>
+__global__ __launch_bounds__(64) void k_ipc_flag(Params p, int k, int* out)
+{
+    if (!kHello && !iterRuns(p, k)) return;
+    const int t = threadIdx.x;
+    const unsigned seq = p.xctl->flagSeq + 1;
+    const int par = seq & 1, R = p.xRanks;
+    bool ok = !xAborted(p);
+    if (ok && t < R && !(!kHello && xStalled(p))) {
+        const unsigned mine = kHello ? 1u : (p.unconv[k] != 0 ? 1u : 0u);
+        llStore(p.peerFlag[t] + (size_t)par * R + p.xRank, seq, mine);
+    }
+    unsigned v = 0;
+    const unsigned long long t0 = wall_clock64();
+    if (ok && t < R) ok = llWait(p, p.flagRx + (size_t)par * R + t, seq, &v, t0);
+    const unsigned long long m = __ballot(!ok && t < R);
+    const bool any = __any(ok && t < R && v != 0);
+    if (m) {                                       // the lowest failing lane records it
+        if (t == __ffsll((long long)m) - 1) xFail(p, kHello ? XK_HELLO : XK_FLAG, t, seq);
+        if (kHello && t == 0) *out = 0;
+        return;
+    }
+    if (t == 0) {
+        if (kHello) *out = any ? 1 : 0;
+        else p.unconv[k] = any ? 1 : 0;
+        p.xctl->flagSeq = seq;
+        if (!kHello) p.xctl->ghostSeq += 1;        // this iteration's ghost exchange is complete
+    }
+}
+// One wave: n <= kRedMax doubles reduced over the ranks in rank order (op 0
+// sum, 1 min), in place -- the same value on every rank
+__global__ __launch_bounds__(64) void k_ipc_reduce(Params p, double* vals, int n, int op)
+{
+    __shared__ double sv[64][kRedMax];
+    __shared__ int okAll;
+    const int t = threadIdx.x;
+    const unsigned seq = p.xctl->redSeq + 1;
+    const int par = seq & 1, R = p.xRanks;
+    const size_t slot = 2 * kRedMax;
+    bool ok = !xAborted(p);
+    if (ok && t < R && !xStalled(p)) {
+        unsigned long long* w = p.peerRed[t] + ((size_t)par * R + p.xRank) * slot;
+        for (int i = 0; i < n; i++) {
+            const unsigned long long bits = (unsigned long long)__double_as_longlong(vals[i]);
+            llStore(w + 2 * i, seq, (unsigned)bits);
+            llStore(w + 2 * i + 1, seq, (unsigned)(bits >> 32));
+        }
+    }
+    const unsigned long long t0 = wall_clock64();
+    if (ok && t < R) {
+        const unsigned long long* w = p.redRx + ((size_t)par * R + t) * slot;
+        for (int i = 0; i < n && ok; i++) {
+            unsigned lo = 0, hi = 0;
+            ok = llWait(p, w + 2 * i, seq, &lo, t0) && llWait(p, w + 2 * i + 1, seq, &hi, t0);
+            sv[t][i] = llDouble(lo, hi);
+        }
+    }
+    const unsigned long long m = __ballot(!ok && t < R);
+    if (t == 0) okAll = m == 0;
+    __syncthreads();
+    if (!okAll) {
+        if (m && t == __ffsll((long long)m) - 1) xFail(p, XK_RED, t, seq);
+        return;
+    }
+    if (t == 0) {
+        for (int i = 0; i < n; i++) {
+            double a = sv[0][i];
+            for (int r = 1; r < R; r++) a = op ? (sv[r][i] < a ? sv[r][i] : a) : a + sv[r][i];
+            vals[i] = a;
+        }
+        p.xctl->redSeq = seq;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Non-conduit links (findLinkFlows' second loop, dynwave.c:404-412, and
 // findNonConduitFlow / getModPumpFlow / findNonConduitSurfArea /
@@ -4244,13 +4523,18 @@ __global__ void k_finalize(Params p)
         }
         if (t == 0)
             for (int q = 0; q < kNumPartials; q++) c->stepRed[q] = sum[q][0];
+        if (kPhase == 1 && t == 0 && p.skipSteady) {    // this rank's part of the step's flow totals
+            const double* r = c->stepRed;
+            const double s6[6] = {c->latTot[0], c->latTot[1] + r[2], r[1], c->latTot[2] + r[0], r[3], r[4]};
+            for (int q = 0; q < 6; q++) c->steadyIO[q] = s6[q];
+        }
     }
     __syncthreads();
     if (t == 0 && kPhase != 1) {
     double tot[kNumPartials];
     for (int q = 0; q < kNumPartials; q++) tot[q] = c->stepRed[q];
     // a step skipped as steady ran no Picard iteration (routing.c:239-244)
-    const bool steady = p.skipSteady && c->steadyOk && !c->steadyChanged;
+    const bool steady = p.skipSteady && c->steadyOk && !c->steadyChanged && !(c->steadyIO[6] > 0.0);
     const int ran = steady ? 0 : steps;
     c->lastSteps = ran;
     c->totalSteps += 1;
@@ -4271,13 +4555,17 @@ __global__ void k_finalize(Params p)
     // SYS_FLOW_TOL (isInSteadyState, routing.c:383-395; the next step's
     // OldRoutingTime is past 0); k_steady then checks the inflows
     if (p.skipSteady) {
-        const double in = step[0] + step[1], out = step[2] + step[3] + step[4] + step[5];
+        // several ranks: the totals summed over the ranks (k_finalize<1>,
+        // then the exchange); the same decision on every rank
+        const double* sv = (kPhase == 2) ? c->steadyIO : step;
+        const double in = sv[0] + sv[1], out = sv[2] + sv[3] + sv[4] + sv[5];
         double err;
         if (fabs(in) > 0.0) err = 1.0 - out / in;
         else if (fabs(out) > 0.0) err = in / out - 1.0;
         else err = 0.0;
         c->steadyOk = fabs(err) <= p.sysFlowTol ? 1 : 0;
         c->steadyChanged = 0;
+        c->steadyIO[6] = 0.0;
     }
     // run statistics of this step (routing.c:255-260): stats_updateFlowStats'
     // system part and stats_updateTimeStepStats (stats.c:449-518)
@@ -4350,6 +4638,8 @@ __global__ void k_finalize(Params p)
     __syncthreads();
     if (kPhase != 1)                               // the next step's convergence flags
         for (int k = t; k < p.maxTrials; k += kBlock) p.unconv[k] = 0;
+    if (kPhase != 1 && t == 0 && p.ipc && p.P > 0) // XCHG_IPC: this step's concentration exchange is complete
+        p.xctl->qualSeq += 1;
     unsigned long long* g = (unsigned long long*)p.ctl;
     for (int w = t; w < nw; w += kBlock) g[w] = cw[w];
 }
@@ -4476,6 +4766,15 @@ struct Router::Impl {
     double* hostX = nullptr;         // host staging for the test transport
     std::vector<double> slotBuf;     // host transport: global ghost-slot buffer
     std::string xerrMsg;             // last failed collective / transfer
+    // XCHG_IPC: this rank's uncached exchange region and the peers' regions
+    // as mapped here (nullptr: self or unmapped); host-mapped failure record
+    // and abort word; the transport actually in use (after any fallback)
+    void* ipcBase = nullptr;
+    std::vector<void*> ipcPeer;
+    int* xerrHost = nullptr;
+    int* hostAbortH = nullptr;
+    double xTimeoutSec = 60.0;       // SWMM5_XCHG_TIMEOUT: bound of every wait behind an exchange
+    std::string transportName = "single";
     float *resN = nullptr, *resL = nullptr;          // packed period results (device)
     float *resNHost = nullptr, *resLHost = nullptr;  // pinned copies
     float *avgN = nullptr, *avgL = nullptr;          // REPORT AVERAGES: the period's sums
@@ -4619,6 +4918,11 @@ Router::~Router()
         if (d_->avgOLHost) (void)hipHostFree(d_->avgOLHost);
         if (d_->depthHost) (void)hipHostFree(d_->depthHost);
         if (d_->comm) (void)ncclCommDestroy(d_->comm);
+        for (void* q : d_->ipcPeer)
+            if (q) (void)hipIpcCloseMemHandle(q);
+        if (d_->ipcBase) (void)hipFree(d_->ipcBase);
+        if (d_->xerrHost) (void)hipHostFree(d_->xerrHost);
+        if (d_->hostAbortH) (void)hipHostFree(d_->hostAbortH);
         for (auto e : d_->clockEv) if (e) (void)hipEventDestroy(e);
         for (auto e : d_->evapEv) if (e) (void)hipEventDestroy(e);
         if (d_->evapPinned) (void)hipHostFree(d_->evapPinned);
@@ -4698,9 +5002,90 @@ static int hostReduce(Router::Impl* d, double* buf, long n, int op)
     return 0;
 }
 
+// XCHG_IPC: the device's failure record as a message; false when there is none
+static bool ipcFailed(Router::Impl* d, std::string* msg)
+{
+    if (!d->xerrHost) return false;
+    const int code = __atomic_load_n(&d->xerrHost[0], __ATOMIC_ACQUIRE);
+    if (!code) return false;
+    static const char* kinds[] = {"?", "ghost-link", "concentration", "convergence-flag", "reduction",
+                                  "start-up handshake"};
+    const int kind = d->xerrHost[1];
+    const char* kn = (kind >= 0 && kind <= XK_HELLO) ? kinds[kind] : "?";
+    char buf[320];
+    if (code == 2)
+        snprintf(buf, sizeof buf, "multi-GPU exchange aborted on rank %d: another rank gave up waiting "
+                 "(%s exchange %d); the run is stopped on every rank", d->part.rank, kn, d->xerrHost[3]);
+    else
+        snprintf(buf, sizeof buf, "multi-GPU exchange timed out: rank %d waited more than %.0f s for rank %d "
+                 "(%s exchange %d); every rank was told to stop", d->part.rank, d->xTimeoutSec,
+                 d->xerrHost[2], kn, d->xerrHost[3]);
+    *msg = buf;
+    if (d->hostAbortH) __atomic_store_n(d->hostAbortH, 1, __ATOMIC_RELEASE);   // later waits exit at once
+    return true;
+}
+
+// Bounded host waits (every synchronisation of the routing stream or of a
+// step's completion event goes through here).  RCCL: the stream or event is
+// polled together with the communicator's asynchronous error against a
+// deadline (SWMM5_XCHG_TIMEOUT, default 60 s); on an RCCL error or at the
+// deadline the communicator is aborted (ncclCommAbort makes its kernels
+// return) and the router fails with error 500 instead of hanging.  IPC: the
+// device's own waits are bounded; past the deadline the host also sets the
+// host-mapped abort word every device wait polls.  The device's failure
+// record is checked after every wait.
+static int waitDone(Router::Impl* d, hipEvent_t ev)
+{
+    hipError_t e;
+    const bool bounded = d->part.active() && (d->comm || d->part.transport == XCHG_IPC);
+    if (bounded) {
+        const auto t0 = std::chrono::steady_clock::now();
+        bool hostAborted = false;
+        for (;;) {
+            e = ev ? hipEventQuery(ev) : hipStreamQuery(d->stream);
+            if (e != hipErrorNotReady) break;
+            const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (d->comm) {
+                ncclResult_t as = ncclSuccess;
+                if (ncclCommGetAsyncError(d->comm, &as) == ncclSuccess && as != ncclSuccess && as != ncclInProgress) {
+                    (void)ncclCommAbort(d->comm);
+                    d->comm = nullptr;
+                    return xfail(d, std::string("RCCL asynchronous error: ") + ncclGetErrorString(as) +
+                                        "; communicator aborted");
+                }
+                if (s > d->xTimeoutSec) {
+                    (void)ncclCommAbort(d->comm);
+                    d->comm = nullptr;
+                    char buf[160];
+                    snprintf(buf, sizeof buf, "an RCCL collective did not complete within %.0f s on rank %d; "
+                             "communicator aborted", d->xTimeoutSec, d->part.rank);
+                    return xfail(d, buf);
+                }
+            } else if (!hostAborted && s > d->xTimeoutSec + 5.0) {
+                __atomic_store_n(d->hostAbortH, 1, __ATOMIC_RELEASE);
+                hostAborted = true;
+            } else if (hostAborted && s > 2.0 * d->xTimeoutSec + 10.0) {
+                return xfail(d, "multi-GPU exchange: the device did not stop after the host abort");
+            }
+            usleep(20);
+        }
+    } else {
+        e = ev ? hipEventSynchronize(ev) : hipStreamSynchronize(d->stream);
+    }
+    if (e != hipSuccess) return xfail(d, std::string("synchronisation: ") + hipGetErrorString(e));
+    std::string m;
+    if (ipcFailed(d, &m)) return xfail(d, m);
+    return 0;
+}
+
 // In-place all-reduce of n doubles (op 0 sum, 1 min) -- the Courant limits.
 static int exchange(Router::Impl* d, const double* send, double* recv, size_t n, int op)
 {
+    if (d->part.transport == XCHG_IPC) {
+        if (send != recv || n > (size_t)kRedMax) return xfail(d, "IPC reduction: in place, at most 8 values");
+        hipLaunchKernelGGL(k_ipc_reduce, dim3(1), dim3(64), 0, d->stream, d->p, recv, (int)n, op);
+        return 0;
+    }
     if (d->part.transport == XCHG_RCCL)
         return ncclCheck(d, ncclAllReduce(send, recv, n, ncclDouble, op ? ncclMin : ncclSum, d->comm, d->stream),
                          "ncclAllReduce");
@@ -4766,6 +5151,10 @@ static int neighbourExchange(Router::Impl* d, int f)
 static int flagExchange(Router::Impl* d, int k)
 {
     int* flag = d->p.unconv + k;
+    if (d->part.transport == XCHG_IPC) {
+        hipLaunchKernelGGL(k_ipc_flag<false>, dim3(1), dim3(64), 0, d->stream, d->p, k, (int*)nullptr);
+        return 0;
+    }
     if (d->part.transport == XCHG_RCCL)
         return ncclCheck(d, ncclAllReduce(flag, flag, 1, ncclInt32, ncclMax, d->comm, d->stream), "ncclAllReduce");
     int v = 0;
@@ -4778,6 +5167,37 @@ static int flagExchange(Router::Impl* d, int k)
     if (int r = hipCheckX(d, hipMemcpyAsync(flag, &v, sizeof(int), hipMemcpyHostToDevice, d->stream), "flag H2D"))
         return r;
     return hipCheckX(d, hipStreamSynchronize(d->stream), "flag sync");
+}
+
+// Iteration k's ghost-link values from their owners (before the node update):
+// pack, transfer, unpack on the RCCL / host transports; on XCHG_IPC the owners
+// store them straight into this rank's ghost area and k_ipc_unpack waits for
+// them.  qualExchange: the ghost links' concentrations, once per step.
+static int ghostExchange(Router::Impl* d, int k)
+{
+    const Params& p = d->p;
+    if (d->part.transport == XCHG_IPC) {
+        if (p.nSend) hipLaunchKernelGGL(k_ipc_pack<false>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
+        if (p.nGhost) hipLaunchKernelGGL(k_ipc_unpack<false>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
+        return 0;
+    }
+    if (p.nSend) hipLaunchKernelGGL(k_xpack, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
+    if (int r = neighbourExchange(d, p.xF)) return r;
+    if (p.nGhost) hipLaunchKernelGGL(k_xunpack, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
+    return 0;
+}
+static int qualExchange(Router::Impl* d)
+{
+    const Params& p = d->p;
+    if (d->part.transport == XCHG_IPC) {
+        if (p.nSend) hipLaunchKernelGGL(k_ipc_pack<true>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, 0);
+        if (p.nGhost) hipLaunchKernelGGL(k_ipc_unpack<true>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, 0);
+        return 0;
+    }
+    if (p.nSend) hipLaunchKernelGGL(k_xpack_qual, dim3(d->gridX), dim3(kBlock), 0, d->stream, p);
+    if (int r = neighbourExchange(d, p.P)) return r;
+    if (p.nGhost) hipLaunchKernelGGL(k_xunpack_qual, dim3(d->gridX), dim3(kBlock), 0, d->stream, p);
+    return 0;
 }
 
 // Timing mode (eager launches, Router::setTiming): the link and node kernels
@@ -4832,11 +5252,8 @@ static int launchIteration(Router::Impl* d, int k)
         launchTimed(d, linkKernel(k == 0, d->linkWaves, d->fastLinks), dim3(k >= 2 ? d->gridLinkSparse : d->gridL),
                     e0, e1, p, k);
     if (p.nCold) (void)hipStreamWaitEvent(d->stream, d->joinEv[k], 0);
-    if (multi) {                                   // ghost links' values from their owners
-        if (p.nSend) hipLaunchKernelGGL(k_xpack, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
-        if (int r = neighbourExchange(d, p.xF)) return r;
-        if (p.nGhost) hipLaunchKernelGGL(k_xunpack, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
-    }
+    if (multi)                                     // ghost links' values from their owners
+        if (int r = ghostExchange(d, k)) return r;
     e0 = d->timing ? d->curEv[4 * k + 1] : nullptr;
     e1 = d->timing ? d->curEv[4 * k + 2] : nullptr;
     launchTimed(d, nodeKernel(k == 0, d->general), dim3(d->gridN), e0, e1, p, k);
@@ -4914,8 +5331,11 @@ static int launchStepImpl(Router::Impl* d, int mode)
     // k_node(1) lists the live nodes only for the list-driven graphs
     p.buildVlist = (mode == GM_SPARSE || mode == GM_LIST || mode == GM_FUSED || mode == GM_COMPACT) ? 1 : 0;
     const bool multi = d->part.active();
-    if (p.skipSteady)                              // SKIP_STEADY_STATE: this step's inflow test
+    if (p.skipSteady) {                            // SKIP_STEADY_STATE: this step's inflow test
         hipLaunchKernelGGL(k_steady, dim3(d->gridN), dim3(kBlock), 0, d->stream, p);
+        if (multi)                                 // any rank's change makes the step routed everywhere
+            if (int r = exchange(d, &p.ctl->steadyIO[6], &p.ctl->steadyIO[6], 1, 0)) return r;
+    }
     const int base = 4 * p.maxTrials;
     hipEvent_t* ev = d->timing ? d->curEv : nullptr;
     if (mode == GM_TAIL) {
@@ -4947,11 +5367,8 @@ static int launchStepImpl(Router::Impl* d, int mode)
                 launchTimed(d, linkKernel(false, d->linkWaves, d->fastLinks), dim3(d->gridLinkSparse),
                             ev ? ev[4 * k] : nullptr, d->timing ? d->curHot[k] : nullptr, p, k);
             if (p.nCold) (void)hipStreamWaitEvent(d->stream, d->joinEv[k], 0);
-            if (multi) {                           // ghost links' values from their owners (as launchIteration)
-                if (p.nSend) hipLaunchKernelGGL(k_xpack, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
-                if (int r = neighbourExchange(d, p.xF)) return r;
-                if (p.nGhost) hipLaunchKernelGGL(k_xunpack, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
-            }
+            if (multi)                             // ghost links' values from their owners (as launchIteration)
+                if (int r = ghostExchange(d, k)) return r;
             launchTimed(d, d->general ? k_node_list<true> : k_node_list<false>, dim3(d->gridNList),
                         ev ? ev[4 * k + 1] : nullptr, ev ? ev[4 * k + 2] : nullptr, p, k);
             // pumps / regulators and their end nodes, as launchIteration: the
@@ -4992,22 +5409,185 @@ static int launchStepImpl(Router::Impl* d, int mode)
             if (int r = launchIteration(d, k)) return r;
     }
     if (p.P > 0) {                                 // the link part runs in k_step_end
-        if (multi) {                               // ghost links' concentrations (previous step end)
-            if (p.nSend) hipLaunchKernelGGL(k_xpack_qual, dim3(d->gridX), dim3(kBlock), 0, d->stream, p);
-            if (int r = neighbourExchange(d, p.P)) return r;
-            if (p.nGhost) hipLaunchKernelGGL(k_xunpack_qual, dim3(d->gridX), dim3(kBlock), 0, d->stream, p);
-        }
+        if (multi)                                 // ghost links' concentrations (previous step end)
+            if (int r = qualExchange(d)) return r;
         if (!d->fuseQual)
             launchTimed(d, k_qual_node, dim3(d->gridQ), ev ? ev[base] : nullptr, ev ? ev[base + 1] : nullptr, p);
     }
     launchTimed(d, stepEndKernel(d->fastLinks, d->allShapes, d->fuseQual), dim3(d->gridEnd),
                 ev ? ev[base + 2] : nullptr, (hipEvent_t) nullptr, p);
-    if (multi && p.varStep) {                      // global Courant limits (min over ranks)
+    if (multi && (p.varStep || p.skipSteady)) {
         hipLaunchKernelGGL(k_finalize<1>, dim3(1), dim3(kBlock), 0, d->stream, p);
-        if (int r = exchange(d, &p.ctl->stepRed[5], &p.ctl->stepRed[5], 2, 1)) return r;
+        if (p.varStep)                             // global Courant limits (min over ranks)
+            if (int r = exchange(d, &p.ctl->stepRed[5], &p.ctl->stepRed[5], 2, 1)) return r;
+        if (p.skipSteady)                          // the step's system flow totals (sum over ranks)
+            if (int r = exchange(d, &p.ctl->steadyIO[0], &p.ctl->steadyIO[0], 6, 0)) return r;
         launchTimed(d, k_finalize<2>, dim3(1), (hipEvent_t) nullptr, ev ? ev[base + 3] : nullptr, p);
     } else {
         launchTimed(d, k_finalize<0>, dim3(1), (hipEvent_t) nullptr, ev ? ev[base + 3] : nullptr, p);
+    }
+    return 0;
+}
+
+// Start-up exchanges over the bootstrap: the host callback when one is set,
+// else the RCCL communicator (n doubles, op 0 sum / 1 min, in place)
+static int bootReduce(Router::Impl* d, double* buf, long n, int op)
+{
+    if (d->part.xchg) return hostReduce(d, buf, n, op);
+    if (!d->comm) return xfail(d, "no bootstrap (host callback or RCCL communicator)");
+    double* tmp = nullptr;
+    if (hipMalloc(&tmp, n * sizeof(double)) != hipSuccess) return xfail(d, "bootstrap: hipMalloc");
+    hipError_t e = hipMemcpy(tmp, buf, n * sizeof(double), hipMemcpyHostToDevice);
+    ncclResult_t r = ncclSuccess;
+    if (e == hipSuccess) r = ncclAllReduce(tmp, tmp, n, ncclDouble, op ? ncclMin : ncclSum, d->comm, d->stream);
+    if (e == hipSuccess && r == ncclSuccess) {
+        if (int w = waitDone(d, nullptr)) { (void)hipFree(tmp); return w; }
+        e = hipMemcpy(buf, tmp, n * sizeof(double), hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(tmp);
+    if (r != ncclSuccess) return xfail(d, std::string("bootstrap ncclAllReduce: ") + ncclGetErrorString(r));
+    if (e != hipSuccess) return xfail(d, std::string("bootstrap copy: ") + hipGetErrorString(e));
+    return 0;
+}
+
+// XCHG_IPC start-up (Router::init, every rank): allocate this rank's uncached
+// exchange region -- flag slots, reduction slots and the abort word at fixed
+// offsets, then the ghost and concentration areas -- and all-gather over the
+// bootstrap {its IPC handle, its ghost count, where each sender's ghosts start
+// in it}; map every other rank's region (hipIpcOpenMemHandle), derive each
+// send entry's slot in its receiver's area, and run one handshake flag
+// exchange with a 10 s deadline.  Every rank reaches every bootstrap call
+// whatever fails locally.  Returns 0 when the transport works on every rank,
+// 1 when it does not (the caller falls back), 500 on a bootstrap error.
+static int setupIpc(Router::Impl* d)
+{
+    Params& p = d->p;
+    const Partition& part = d->part;
+    const int R = part.nranks, me = part.rank;
+    if (R > 64) return xfail(d, "the IPC transport takes at most 64 ranks");
+    const size_t F = p.xF, P = p.P, nG = p.nGhost;
+    const size_t flagW = 2 * (size_t)R, redW = 2 * (size_t)R * 2 * kRedMax, fixedW = flagW + redW + 8;
+    const size_t words = fixedW + 2 * 2 * F * nG + 2 * 2 * P * nG;
+    bool ok = hipExtMallocWithFlags(&d->ipcBase, words * 8, hipDeviceMallocUncached) == hipSuccess &&
+              hipMemset(d->ipcBase, 0, words * 8) == hipSuccess;
+    hipIpcMemHandle_t h{};
+    ok = ok && hipIpcGetMemHandle(&h, d->ipcBase) == hipSuccess;
+    (void)hipGetLastError();
+    // record per rank: 64 handle bytes, ok, nGhost, then per sender rank the
+    // start of its ghosts here + 1 (0: none) and their count
+    const int RL = 66 + 2 * R;
+    std::vector<double> rec((size_t)R * RL, 0.0);
+    double* mine = rec.data() + (size_t)me * RL;
+    const unsigned char* hb = (const unsigned char*)&h;
+    static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle size");
+    for (size_t i = 0; i < sizeof h; i++) mine[i] = hb[i];
+    mine[64] = ok ? 1.0 : 0.0;
+    mine[65] = (double)nG;
+    for (size_t k = 0; k < part.nbr.size(); k++) {
+        mine[66 + 2 * part.nbr[k]] = part.recvOff[k] + 1.0;
+        mine[67 + 2 * part.nbr[k]] = part.recvOff[k + 1] - part.recvOff[k];
+    }
+    if (int r = bootReduce(d, rec.data(), (long)rec.size(), 0)) return r;
+    for (int r = 0; r < R; r++) ok = ok && rec[(size_t)r * RL + 64] == 1.0;
+    // map the peers' regions
+    d->ipcPeer.assign(R, nullptr);
+    std::vector<unsigned long long*> base(R, nullptr);
+    base[me] = (unsigned long long*)d->ipcBase;
+    for (int r = 0; r < R && ok; r++) {
+        if (r == me) continue;
+        hipIpcMemHandle_t hr{};
+        unsigned char* b = (unsigned char*)&hr;
+        for (size_t i = 0; i < sizeof hr; i++) b[i] = (unsigned char)rec[(size_t)r * RL + i];
+        void* ptr = nullptr;
+        if (hipIpcOpenMemHandle(&ptr, hr, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !ptr) {
+            (void)hipGetLastError();
+            ok = false;
+            break;
+        }
+        d->ipcPeer[r] = ptr;
+        base[r] = (unsigned long long*)ptr;
+    }
+    // each send entry's receiver slot; every receiver expects exactly what is sent
+    std::vector<int> sendNbr(std::max<size_t>(part.sendLink.size(), 1), 0), sendGi(sendNbr.size(), 0);
+    std::vector<XPeer> xp(std::max<size_t>(part.nbr.size(), 1));
+    for (size_t k = 0; k < part.nbr.size() && ok; k++) {
+        const int r = part.nbr[k];
+        const double* rr = rec.data() + (size_t)r * RL;
+        const int ns = part.sendOff[k + 1] - part.sendOff[k];
+        if (ns > 0 && (rr[66 + 2 * me] < 1.0 || (int)rr[67 + 2 * me] != ns)) { ok = false; break; }
+        const int start = ns > 0 ? (int)rr[66 + 2 * me] - 1 : 0;
+        const size_t ngr = (size_t)rr[65];
+        xp[k].nGhost = (int)ngr;
+        xp[k].ghost = base[r] + fixedW;
+        xp[k].qual = base[r] + fixedW + 2 * 2 * F * ngr;
+        for (int e = part.sendOff[k]; e < part.sendOff[k + 1]; e++) {
+            sendNbr[e] = (int)k;
+            sendGi[e] = start + (e - part.sendOff[k]);
+        }
+    }
+    std::vector<int> ghostFrom(std::max<size_t>(nG, 1), -1);
+    for (size_t k = 0; k < part.nbr.size(); k++)
+        for (int g = part.recvOff[k]; g < part.recvOff[k + 1]; g++) ghostFrom[g] = part.nbr[k];
+    {
+        double a = ok ? 1.0 : 0.0;                 // every rank mapped every peer
+        if (int r = bootReduce(d, &a, 1, 1)) return r;
+        ok = a == 1.0;
+    }
+    if (!ok) return 1;
+    // device tables
+    std::vector<unsigned long long*> pf(R), pr(R), pa(R);
+    for (int r = 0; r < R; r++) {
+        pf[r] = base[r];
+        pr[r] = base[r] + flagW;
+        pa[r] = base[r] + flagW + redW;
+    }
+    auto up = [&](const void* src, size_t bytes) -> void* {
+        void* q = nullptr;
+        if (hipMalloc(&q, std::max<size_t>(bytes, 8)) != hipSuccess) return nullptr;
+        d->allocs.push_back(q);
+        if (!src) return hipMemset(q, 0, std::max<size_t>(bytes, 8)) == hipSuccess ? q : nullptr;
+        if (bytes && hipMemcpy(q, src, bytes, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+        return q;
+    };
+    p.xpeer = (const XPeer*)up(xp.data(), xp.size() * sizeof(XPeer));
+    p.sendNbr = (const int*)up(sendNbr.data(), sendNbr.size() * sizeof(int));
+    p.sendGi = (const int*)up(sendGi.data(), sendGi.size() * sizeof(int));
+    p.ghostFrom = (const int*)up(ghostFrom.data(), ghostFrom.size() * sizeof(int));
+    p.peerFlag = (unsigned long long* const*)up(pf.data(), R * sizeof(void*));
+    p.peerRed = (unsigned long long* const*)up(pr.data(), R * sizeof(void*));
+    p.peerAbort = (unsigned long long* const*)up(pa.data(), R * sizeof(void*));
+    XCtl x0{};
+    p.xctl = (XCtl*)up(&x0, sizeof x0);
+    if (!p.xpeer || !p.sendNbr || !p.sendGi || !p.ghostFrom || !p.peerFlag || !p.peerRed || !p.peerAbort || !p.xctl)
+        return xfail(d, "IPC transport: device tables");
+    unsigned long long* own = base[me];
+    p.flagRx = own;
+    p.redRx = own + flagW;
+    p.abortW = own + flagW + redW;
+    p.ghostRx = own + fixedW;
+    p.qualRx = own + fixedW + 2 * 2 * F * nG;
+    p.xRank = me;
+    p.xRanks = R;
+    p.ipc = 1;
+    // handshake: flag exchange number 1, every rank's flag set, 10 s at most
+    int* dOk = (int*)up(nullptr, sizeof(int));
+    if (!dOk) return xfail(d, "IPC transport: device tables");
+    const long long tmo = p.xTimeout;
+    p.xTimeout = std::min<long long>(tmo, (long long)(10.0 * d->wallKHz * 1000.0));
+    hipLaunchKernelGGL(k_ipc_flag<true>, dim3(1), dim3(64), 0, d->stream, p, 0, dOk);
+    p.xTimeout = tmo;
+    int hv = 0;
+    ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(d->stream) == hipSuccess &&
+         hipMemcpy(&hv, dOk, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess && hv == 1 &&
+         d->xerrHost[0] == 0;
+    {
+        double a = ok ? 1.0 : 0.0;
+        if (int r = bootReduce(d, &a, 1, 1)) return r;
+        ok = a == 1.0;
+    }
+    if (!ok) {
+        p.ipc = 0;
+        return 1;
     }
     return 0;
 }
@@ -5099,16 +5679,12 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     p.minRouteStep = prj.opt.minRouteStep;
     p.routeStep = prj.opt.routeStep;
     p.varStep = (prj.opt.courantFactor != 0.0 && prj.opt.routeStep >= 0.001) ? 1 : 0;
-    // SKIP_STEADY_STATE (routing.c:236-244, 383-395): single GPU (the inflow
-    // test and the flow error would need exchanges between the ranks)
+    // SKIP_STEADY_STATE (routing.c:236-244, 383-395); with several ranks the
+    // inflow test and the step's flow totals are reduced over the ranks once
+    // per step each (launchStep), so every rank makes the same decision
     p.skipSteady = prj.opt.skipSteadyState ? 1 : 0;
     p.sysFlowTol = prj.opt.sysFlowTol;
     p.latFlowTol = prj.opt.latFlowTol;
-    if (p.skipSteady && partIn && partIn->active()) {
-        err_ = 200;
-        errMsg_ = "ERROR 200: SKIP_STEADY_STATE is not supported with several GPUs";
-        return err_;
-    }
 
     hipError_t e;
     auto upD = [&](const std::vector<double>& v, size_t n) -> double* {
@@ -5724,8 +6300,12 @@ int Router::init(Project& prj, int device, const Partition* partIn)
     p.nSend = (int)part.sendLink.size();
     p.nGhost = (int)part.lghost.size();
     {
-        bool seep = false;                          // evaporation / seepage values travel too
-        for (int j = 0; j < nL; j++) seep = seep || (lflags[j] & LF_SEEP);
+        // evaporation / seepage values travel too when any link of the whole
+        // network has them (the same count on every rank: what one rank sends
+        // another receives)
+        bool seep = false;
+        for (int g = 0; g < gL && !seep; g++)
+            seep = net.seepRate[g] > 0.0 || (prj.evapCanBePositive() && isOpen(net.xsect[g].type));
         p.xF = seep ? 6 : 4;
         const int w = std::max(p.xF, P);
         int* ip;
@@ -5734,17 +6314,73 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         UPD(p.xsend, zs, zs.size());
         UPD(p.xrecv, zg, zg.size());
         d->gridX = std::max(1, std::min((std::max(p.nSend, p.nGhost) + kBlock - 1) / kBlock, maxBlocks));
+        p.ipc = 0;
+        p.xRank = part.rank;
+        p.xRanks = part.nranks;
+        p.stallStep = -1;
+        HIPCHECK(hipHostMalloc((void**)&d->xerrHost, 4 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHECK(hipHostMalloc((void**)&d->hostAbortH, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+        memset(d->xerrHost, 0, 4 * sizeof(int));
+        *d->hostAbortH = 0;
+        {
+            void* dp = nullptr;
+            HIPCHECK(hipHostGetDevicePointer(&dp, d->xerrHost, 0));
+            p.xerr = (int*)dp;
+            HIPCHECK(hipHostGetDevicePointer(&dp, d->hostAbortH, 0));
+            p.hostAbort = (const int*)dp;
+        }
+        if (const char* ts = getenv("SWMM5_XCHG_TIMEOUT"))
+            if (atof(ts) > 0.0) d->xTimeoutSec = atof(ts);
+        p.xTimeout = (long long)(d->xTimeoutSec * d->wallKHz * 1000.0);
+        if (const char* st = getenv("SWMM5_XCHG_STALL")) {     // test hook "rank:step"
+            int r = -1;
+            long long s = -1;
+            if (sscanf(st, "%d:%lld", &r, &s) == 2 && r == part.rank) p.stallStep = s;
+        }
+        d->transportName = "single";
         if (part.active()) {
-            if (part.transport == XCHG_RCCL) {
-                if (part.ncclId.size() != sizeof(ncclUniqueId)) { fail("RCCL unique id missing"); return err_; }
+            auto initRccl = [&]() -> bool {
+                // single-node bootstrap over the loopback interface unless the
+                // caller chose one (an unset interface lets RCCL probe the
+                // host's interfaces at communicator creation)
+                setenv("NCCL_SOCKET_IFNAME", "lo", 0);
+                if (part.ncclId.size() != sizeof(ncclUniqueId)) { fail("RCCL unique id missing"); return false; }
                 ncclUniqueId id;
                 memcpy(&id, part.ncclId.data(), sizeof id);
                 ncclResult_t r = ncclCommInitRank(&d->comm, part.nranks, id, part.rank);
-                if (r != ncclSuccess) { fail(std::string("ncclCommInitRank: ") + ncclGetErrorString(r)); return err_; }
-            } else {
+                if (r != ncclSuccess) { fail(std::string("ncclCommInitRank: ") + ncclGetErrorString(r)); return false; }
+                return true;
+            };
+            if (part.transport == XCHG_RCCL) {
+                if (!initRccl()) return err_;
+                d->transportName = "rccl";
+            } else if (part.transport == XCHG_IPC) {
+                if (!part.xchg && !initRccl()) return err_;      // bootstrap over RCCL
+                const int r = setupIpc(d);
+                if (r == 500) { fail(d->xerrMsg); return err_; }
+                if (r == 0) {
+                    d->transportName = "ipc";
+                } else {                                          // not usable here: fall back
+                    memset(d->xerrHost, 0, 4 * sizeof(int));
+                    *d->hostAbortH = 0;
+                    if (part.ncclId.size() == sizeof(ncclUniqueId)) {
+                        if (!d->comm && !initRccl()) return err_;
+                        d->part.transport = XCHG_RCCL;
+                        d->transportName = "rccl (IPC transport unavailable: fell back)";
+                    } else if (part.xchg) {
+                        d->part.transport = XCHG_HOST;
+                        d->transportName = "host (IPC transport unavailable: fell back)";
+                    } else {
+                        fail("IPC transport unavailable and no fallback transport");
+                        return err_;
+                    }
+                }
+            }
+            if (d->part.transport == XCHG_HOST) {
                 if (!part.xchg) { fail("host exchange callback missing"); return err_; }
                 size_t nx = (size_t)w * std::max(p.nSend, p.nGhost) + 8;
                 HIPCHECK(hipHostMalloc((void**)&d->hostX, nx * sizeof(double), hipHostMallocDefault));
+                if (d->transportName == "single") d->transportName = "host";
             }
         }
     }
@@ -5905,7 +6541,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
             hipLaunchKernelGGL(k_outfall_qcs, dim3((26 * p.nOutLinks + kBlock - 1) / kBlock), dim3(kBlock), 0,
                                d->stream, p, q);
             HIPCHECK(hipGetLastError());
-            HIPCHECK(hipStreamSynchronize(d->stream));
+            WAITCHECK(waitDone(d_, nullptr));
         }
         p.ofQcs = q;
     }
@@ -6143,7 +6779,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         HIPCHECK(hipGraphInstantiate(&d->graphCompact, g, nullptr, nullptr, 0));
         (void)hipGraphDestroy(g);
     }
-    HIPCHECK(hipStreamSynchronize(d->stream));
+    WAITCHECK(waitDone(d_, nullptr));
     ok_ = true;
     return 0;
 #undef UPD
@@ -6226,7 +6862,7 @@ static void probeCollect(Router::Impl* d)
 static void flushTiming(Router::Impl* d)
 {
     if (!d->tUsed) return;
-    (void)hipStreamSynchronize(d->stream);
+    (void)waitDone(d, nullptr);
     const Params& p = d->p;
     for (int s = 0; s < d->tUsed; s++) {
         Router::Impl::TimingSlot& t = d->tslots[s];
@@ -6326,6 +6962,10 @@ static int chooseGraph(Router::Impl* d)
         d->itersSeen = n;
     }
     const bool fresh = d->itersSeen < 0;
+    // several ranks: the same graph on every rank at every step, whatever each
+    // rank's own live lists (the choice must not depend on the timing of a
+    // non-blocking event query); the list graph unless it is turned off
+    if (d->part.active()) return d->listOk ? GM_LIST : GM_UNROLLED;
     if (d->sparseOk && d->sparseMode == 1) return GM_SPARSE;
     if (d->listOk && d->sparseMode == 3) return GM_LIST;
     if (d->fusedGrid > 0 && d->sparseMode == 4) return GM_FUSED;
@@ -6363,11 +7003,15 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
         fail("k_tail grid barrier timed out (workgroups not co-resident); the step it ran is incomplete");
         return err_;
     }
+    {   // XCHG_IPC: a wait of an earlier step gave up (the record is host-mapped)
+        std::string m;
+        if (ipcFailed(d, &m)) { fail(m); return err_; }
+    }
     if (latFlow) {
         // pinned ring slot: wait until the DMA that last read this slot is done
         int s = d->ringNext;
         d->ringNext = (d->ringNext + 1) % Impl::kRing;
-        HIPCHECK(hipEventSynchronize(d->ringEv[s]));
+        WAITCHECK(waitDone(d_, d->ringEv[s]));
         double* slot = d->hostPinned + (size_t)s * d->slotDoubles;
         size_t nN = p.nN, nq = (size_t)p.P * nN;
         const Partition& part = d->part;
@@ -6458,7 +7102,7 @@ int Router::launchedDt(double* dt)
     // the step just launched is L-1; its dt was written by step L-2's
     // k_finalize into slot (L-1) % kRing (slot 0 holds the initial step)
     long long L = d->launched;
-    if (L >= 2) HIPCHECK(hipEventSynchronize(d->clockEv[(L - 2) % Impl::kRing]));
+    if (L >= 2) WAITCHECK(waitDone(d_, d->clockEv[(L - 2) % Impl::kRing]));
     if (tailFailed(d)) {
         fail("k_tail grid barrier timed out (workgroups not co-resident); the step it ran is incomplete");
         return err_;
@@ -6472,7 +7116,7 @@ int Router::readClock(double* t, double* lastDt, double* nextDt)
     auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
     Impl* d = d_;
     HIPCHECK(hipMemcpyAsync(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost, d->stream));
-    HIPCHECK(hipStreamSynchronize(d->stream));
+    WAITCHECK(waitDone(d_, nullptr));
     if (t) *t = d->hostCtl->newRoutingTime;
     if (nextDt) *nextDt = d->hostCtl->dt;
     if (lastDt) *lastDt = d->lastDtHost;
@@ -6482,7 +7126,7 @@ int Router::readClock(double* t, double* lastDt, double* nextDt)
 int Router::sync()
 {
     auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
-    HIPCHECK(hipStreamSynchronize(d_->stream));
+    WAITCHECK(waitDone(d_, nullptr));
     return 0;
 }
 
@@ -6554,7 +7198,7 @@ int Router::download(Project& prj)
     if (P) {
         HIPCHECK(hipMemcpyAsync(&d->hostCtl->qualPar, &d->ctl->qualPar, sizeof(int), hipMemcpyDeviceToHost,
                                 d->stream));
-        HIPCHECK(hipStreamSynchronize(d->stream));
+        WAITCHECK(waitDone(d_, nullptr));
         qp = d->hostCtl->qualPar;
     }
     if (P && !multi) {
@@ -6594,7 +7238,7 @@ int Router::download(Project& prj)
     HIPCHECK(hipMemcpyAsync(ls.data(), p.lstate, nL * sizeof(int), hipMemcpyDeviceToHost, d->stream));
     HIPCHECK(hipMemcpyAsync(cv.data(), p.conv, nN * sizeof(int), hipMemcpyDeviceToHost, d->stream));
     HIPCHECK(hipMemcpyAsync(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost, d->stream));
-    HIPCHECK(hipStreamSynchronize(d->stream));
+    WAITCHECK(waitDone(d_, nullptr));
     size_t gL = multi ? prj.net.nLinks() : nL, gN = multi ? prj.net.nNodes() : nN;
     st.flowClass.resize(gL); st.fullState.resize(gL); st.normalFlow.resize(gL); st.capacityLimited.resize(gL);
     st.converged.resize(gN);
@@ -6654,7 +7298,7 @@ int Router::downloadStats(Project& prj)
         for (size_t j = 0; j < nL; j++) out[multi ? part.llink[j] : j] = itmp[j];
         return e;
     };
-    HIPCHECK(hipStreamSynchronize(d->stream));
+    WAITCHECK(waitDone(d_, nullptr));
     HIPCHECK(node(R.avgDepth, S.avgDepth));
     HIPCHECK(node(R.maxDepth, S.maxDepth));
     HIPCHECK(node(R.maxDepthDate, S.maxDepthDate));
@@ -6778,7 +7422,7 @@ int Router::upload(Project& prj)
     HIPCHECK(upL(p.q1, st.q1));
     HIPCHECK(upL(p.a1, st.a1));
     HIPCHECK(upL(p.setting, st.setting));
-    HIPCHECK(hipStreamSynchronize(d->stream));
+    WAITCHECK(waitDone(d_, nullptr));
     return 0;
 }
 
@@ -6788,7 +7432,10 @@ static void pullCtl(Router::Impl* d, int& err, std::string& msg)
 {
     hipError_t e = hipMemcpyAsync(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost,
                                   d->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
+    if (e == hipSuccess && waitDone(d, nullptr) && !err) {
+        err = 500;
+        msg = "ERROR 500: GPU router: " + d->xerrMsg;
+    }
     if (e != hipSuccess && !err) {
         err = 500;
         msg = std::string("ERROR 500: GPU router: ") + hipGetErrorString(e);
@@ -6877,7 +7524,7 @@ int Router::timeKernel(int which, int reps, double* avgUs)
     hipEvent_t a, b;
     HIPCHECK(hipEventCreate(&a));
     HIPCHECK(hipEventCreate(&b));
-    HIPCHECK(hipStreamSynchronize(d->stream));
+    WAITCHECK(waitDone(d_, nullptr));
     HIPCHECK(hipEventRecord(a, d->stream));
     // the probe instantiations (distinct kernel names, same code)
     LinkKernelFn lk = nullptr;
@@ -6940,7 +7587,7 @@ int Router::peek(int field, int g, double* v)
         }
     }
     HIPCHECK(hipMemcpyAsync(v, src + i, sizeof(double), hipMemcpyDeviceToHost, d->stream));
-    HIPCHECK(hipStreamSynchronize(d->stream));
+    WAITCHECK(waitDone(d_, nullptr));
     return 0;
 }
 
@@ -6951,7 +7598,7 @@ int Router::setOutfallStage(int g, double stage)
     Params& p = d->p;
     int i = localIndex(d->part.gnode, d->part.active(), g);
     if (i < 0 || i >= p.nN) return 0;                   // not on this rank
-    HIPCHECK(hipStreamSynchronize(d->stream));
+    WAITCHECK(waitDone(d_, nullptr));
     int f = 0;
     HIPCHECK(hipMemcpy(&f, p.nflags + i, sizeof(int), hipMemcpyDeviceToHost));
     f = (int)(((uint32_t)f & ~(0x7u << NF_OTYPE_SHIFT)) | ((uint32_t)O_FIXED << NF_OTYPE_SHIFT));
@@ -6974,7 +7621,7 @@ int Router::repickStep(double cap, double durBefore, double durAfter)
     auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
     Impl* d = d_;
     const Params& p = d->p;
-    HIPCHECK(hipStreamSynchronize(d->stream));
+    WAITCHECK(waitDone(d_, nullptr));
     HIPCHECK(hipMemcpy(d->hostCtl, d->ctl, sizeof(StepCtl), hipMemcpyDeviceToHost));
     StepCtl* h = d->hostCtl;
     const double oldCap = h->routeStep;
@@ -7034,7 +7681,7 @@ int Router::setClimate(double rate, double hydcon, double recovery)
     }
     const int sl = d->evapNext;
     d->evapNext = (d->evapNext + 1) % Impl::kRing;
-    HIPCHECK(hipEventSynchronize(d->evapEv[sl]));           // the copy that last read this slot
+    WAITCHECK(waitDone(d_, d->evapEv[sl]));           // the copy that last read this slot
     double* slot = d->evapPinned + 3 * sl;
     for (int q = 0; q < 3; q++) slot[q] = v[q];
     static_assert(offsetof(StepCtl, hydconFactor) == offsetof(StepCtl, evapRate) + sizeof(double) &&
@@ -7050,7 +7697,7 @@ int Router::setRouteStep(double step, double dtNext)
 {
     auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
     Impl* d = d_;
-    HIPCHECK(hipStreamSynchronize(d->stream));
+    WAITCHECK(waitDone(d_, nullptr));
     StepCtl* c = d->p.ctl;
     int off = 1;
     HIPCHECK(hipMemcpy(&c->routeStep, &step, sizeof(double), hipMemcpyHostToDevice));
@@ -7144,7 +7791,7 @@ int Router::avgTake(double uL, double uV, double uQ, const float** avgNode, cons
     HIPCHECK(hipMemcpyAsync(d->resLHost, d->resL, lb * sizeof(float), hipMemcpyDeviceToHost, d->stream));
     HIPCHECK(hipMemcpyAsync(d->depthHost, p.nNewDepth, (size_t)p.nN * sizeof(double), hipMemcpyDeviceToHost,
                             d->stream));
-    HIPCHECK(hipStreamSynchronize(d->stream));
+    WAITCHECK(waitDone(d_, nullptr));
     *avgNode = d->avgONHost;
     *avgLink = d->avgOLHost;
     *curNode = d->resNHost;
@@ -7164,23 +7811,27 @@ int Router::packResults(double f, double uL, double uV, double uQ, const float**
     if (launchPack(d, f, uL, uV, uQ, &m)) { fail(m); return err_; }
     HIPCHECK(hipMemcpyAsync(d->resNHost, d->resN, nb * sizeof(float), hipMemcpyDeviceToHost, d->stream));
     HIPCHECK(hipMemcpyAsync(d->resLHost, d->resL, lb * sizeof(float), hipMemcpyDeviceToHost, d->stream));
-    HIPCHECK(hipStreamSynchronize(d->stream));
+    WAITCHECK(waitDone(d_, nullptr));
     *nodeVals = d->resNHost;
     *linkVals = d->resLHost;
     return 0;
 }
 
 const Partition& Router::partition() const { return d_->part; }
+std::string Router::transport() const { return d_->transportName; }
 
 int Router::allreduceHost(double* buf, int n, int op)
 {
     auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
     Impl* d = d_;
     if (!d->part.active() || n <= 0) return 0;
-    if (d->part.transport == XCHG_HOST) {
+    // the host callback when one is set (host transport; IPC bootstrapped over
+    // it), else the RCCL communicator
+    if (d->part.xchg) {
         if (d->part.xchg(buf, n, op, d->part.xuser)) { fail("host exchange failed"); return err_; }
         return 0;
     }
+    if (!d->comm) { fail("no communicator (aborted after an earlier failure)"); return err_; }
     double* tmp = nullptr;
     HIPCHECK(hipMalloc(&tmp, n * sizeof(double)));
     hipError_t e = hipMemcpyAsync(tmp, buf, n * sizeof(double), hipMemcpyHostToDevice, d->stream);
@@ -7189,7 +7840,11 @@ int Router::allreduceHost(double* buf, int n, int op)
         if (r != ncclSuccess) { (void)hipFree(tmp); fail(std::string("ncclAllReduce: ") + ncclGetErrorString(r)); return err_; }
         e = hipMemcpyAsync(buf, tmp, n * sizeof(double), hipMemcpyDeviceToHost, d->stream);
     }
-    if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
+    if (e == hipSuccess && waitDone(d, nullptr)) {
+        (void)hipFree(tmp);
+        fail(d->xerrMsg);
+        return err_;
+    }
     (void)hipFree(tmp);
     if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
     return 0;

@@ -31,13 +31,18 @@ namespace swx {
 // of n doubles across the ranks (op 0 = sum, 1 = min).  Returns 0 on success.
 typedef int (*ExchangeFn)(double* buf, long n, int op, void* user);
 
-enum { XCHG_RCCL = 0, XCHG_HOST = 1 };
+// Transports of the per-iteration exchange: RCCL (ncclSend / ncclRecv and
+// ncclAllReduce captured in the step graph), HOST (the callback below; tests:
+// several ranks on one GPU), IPC (device-initiated stores into the peers'
+// memory, mapped with hipIpcOpenMemHandle; no collective library inside a
+// step; bootstrapped over the host callback when one is set, else over RCCL).
+enum { XCHG_RCCL = 0, XCHG_HOST = 1, XCHG_IPC = 2 };
 
 struct Partition {
     int rank = 0, nranks = 1;
     int transport = XCHG_RCCL;
-    std::vector<unsigned char> ncclId;     // 128-byte ncclUniqueId (RCCL transport)
-    ExchangeFn xchg = nullptr;
+    std::vector<unsigned char> ncclId;     // 128-byte ncclUniqueId (RCCL transport / bootstrap)
+    ExchangeFn xchg = nullptr;             // host callback (HOST transport; IPC bootstrap)
     void* xuser = nullptr;
 
     // ---- derived by buildPartition (identical on every rank) -------------

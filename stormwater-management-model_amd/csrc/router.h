@@ -107,6 +107,9 @@ public:
     // updates, k_link ms, k_node ms; returns the number of values available
     int iterationStats(double* out, int n);
     std::string deviceName() const { return devName_; }
+    // the multi-GPU transport in use ("single", "rccl", "host", "ipc", or a
+    // fallback note)
+    std::string transport() const;
     bool ok() const { return ok_; }
     int lastError() const { return err_; }
     std::string lastErrorMsg() const { return errMsg_; }

@@ -108,6 +108,8 @@ def load_library(path: str | None = None):
         "swmmx_ncclUniqueId": (c_int, [ctypes.c_void_p, c_int]),
         "swmmx_setPartition": (c_int, [c_int, c_int, ctypes.c_void_p, c_int]),
         "swmmx_setExchange": (c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+        "swmmx_setTransport": (c_int, [c_int]),
+        "swmmx_getTransport": (c_int, [ctypes.c_char_p, c_int]),
         "swmmx_getOwner": (c_int, [c_int, P(c_int), c_int]),
         "swmmx_getPartition": (ctypes.c_long, [c_char_p, P(c_int), ctypes.c_long]),
         "swmmx_xsect": (c_int, [c_int, P(c_dbl), c_dbl, c_int, P(c_dbl), P(c_dbl), c_int, c_int]),
@@ -369,6 +371,19 @@ class SWMM:
                 return 1
         self._xchg = CB(tramp)
         return self.L.swmmx_setExchange(ctypes.cast(self._xchg, ctypes.c_void_p), None)
+
+    TRANSPORTS = {"rccl": 0, "host": 1, "ipc": 2}
+
+    def set_transport(self, kind: str):
+        """Transport of the per-iteration exchange (swmmx_setTransport): "rccl",
+        "host" (the set_exchange callback) or "ipc" (device stores into the
+        peers' memory; bootstrapped over the callback when one is set)."""
+        return self.L.swmmx_setTransport(self.TRANSPORTS[kind])
+
+    def transport(self) -> str:
+        buf = ctypes.create_string_buffer(256)
+        self.L.swmmx_getTransport(buf, 256)
+        return buf.value.decode()
 
     def partition_array(self, name: str):
         """This rank's part of the partition (swmmx_getPartition)."""

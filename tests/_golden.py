@@ -20,7 +20,7 @@ CASES = ["grid12", "grid12_var_qual", "grid10_surcharge", "example", "example_va
          "example_stride_fixed", "example_dummy", "example_dummy_var", "example_evap_monthly",
          "example_evap_series", "example_avg", "example_exfil", "example_exfil_var",
          "example_evap_file", "example_evap_temp", "example_evap_td3200", "example_evap_dly",
-         "example_steady", "example_steady_var"]
+         "example_steady", "example_steady_var", "example_steady_pump"]
 # cases using objects outside the C restatement's scope (oracle/dw_oracle.c
 # covers junctions, outfalls and conduits): pinned by the GPU tests against the
 # reference's own fixtures only
@@ -37,7 +37,7 @@ BEYOND_ORACLE = {"example_storage", "example_storage_var", "example_storage_qual
                  "example_stride", "example_stride_fixed",
                  # SKIP_STEADY_STATE: routing_execute's steady-state skip (routing.c:383-395)
                  # is not in the restatement's step
-                 "example_steady", "example_steady_var"}
+                 "example_steady", "example_steady_var", "example_steady_pump"}
 # cases whose input writes a file next to itself ([FILES] SAVE ...): they run
 # from a private copy so the fixtures directory is never written to
 SAVES = {"example_hotsave": "example_hotsave.hsf"}

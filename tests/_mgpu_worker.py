@@ -31,7 +31,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     s = swmm5.SWMM()
-    if transport == "host":
+    if transport in ("host", "ipc"):
         import torch
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -42,6 +42,8 @@ def main():
 
         s.set_partition(rank, world)
         s.set_exchange(xchg)
+        if transport == "ipc":          # device stores into the peers' memory; gloo bootstraps it
+            s.set_transport("ipc")
     else:
         assert world == 1
         s.set_partition(0, 1, s.nccl_unique_id())
@@ -56,7 +58,7 @@ def main():
         msg = s.getError()
         s.close()
         np.savez(out, codes=np.array(codes), msg=np.frombuffer(str(msg).encode(), dtype=np.uint8))
-        if transport == "host":
+        if transport in ("host", "ipc"):
             import torch.distributed as dist
             dist.destroy_process_group()
         sys.exit(0 if any(codes) else 3)
@@ -71,6 +73,7 @@ def main():
         "link_owner": s.owners(swmm5.LINK),
         "counters": np.array([c["steps"], c["iterations"], c["nonconverged"]]),
         "graphs": np.array([c["steps_unrolled"], c["steps_list"]]),
+        "transport": np.frombuffer(s.transport().encode(), dtype=np.uint8),
     }
     for f in ("newDepth", "newVolume", "inflow", "outflow", "overflow"):
         res["node." + f] = s.get_array("node." + f)
@@ -86,7 +89,7 @@ def main():
     res["flow_error"] = np.array([ferr])
     s.close()
     np.savez(out, **res)
-    if transport == "host":
+    if transport in ("host", "ipc"):
         import torch.distributed as dist
         dist.barrier()
         dist.destroy_process_group()

@@ -151,6 +151,12 @@ CASES = {
                                                       options={"SKIP_STEADY_STATE": "YES",
                                                                "SYS_FLOW_TOL": "1",
                                                                "LAT_FLOW_TOL": "2"}), 2),
+    # SKIP_STEADY_STATE with pumps (C17 switches on above 2.0 ft and off
+    # below 0.5 ft of its inlet depth: a step whose pump settings change is
+    # never steady, routing.c:224, 388-391), storage units and pollutants
+    "example_steady_pump": (netgen.write_example, dict(end_time="08:00:00", route_step=10.0,
+                                                       regulators=True, storage=True, pollutants=True,
+                                                       options={"SKIP_STEADY_STATE": "YES"}), 2),
     "example_dummy": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, dummy=True,
                                                  pollutants=True), 1),
     "example_dummy_var": (netgen.write_example, dict(end_time="02:00:00", route_step=10.0, variable_step=0.75,

@@ -18,7 +18,11 @@ GPU:
     step; 3 pollutants; pumps and regulators; the list graph on every step,
     with strips, interleaved blocks, pollutants and regulators);
   * results and hot-start files byte-identical to one GPU's; a write error on
-    rank 0 stops every rank; SKIP_STEADY_STATE refused with several ranks;
+    rank 0 stops every rank; SKIP_STEADY_STATE with two ranks bitwise equal
+    to one GPU (its .out byte-identical);
+  * the IPC transport (device stores into the peers' memory, captured step
+    graphs): the same bitwise cases with 2 and 3 ranks on the one GPU, and a
+    rank that stops answering makes every rank fail within the deadline;
   * 1 rank through the RCCL path (captured ncclSend/ncclRecv + flag
     all-reduce): bitwise equal to the single-GPU engine;
   * the 4M-conduit configs[4] network split in two strips, bitwise.
@@ -338,7 +342,12 @@ def _assert_bitwise(parts, one):
         assert abs(part["flow_error"][0] - one["flow_error"][0]) < 1e-3
 
 
+def _transport_of(part):
+    return bytes(part["transport"]).decode()
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["host", "ipc"])
 @pytest.mark.parametrize("kw,steps,surcharged,world", [
     (dict(route_step=1.0), 120, False, 2),
     # the benchmark's regime: surcharged, non-converging, iterations >= 2 with
@@ -349,20 +358,50 @@ def _assert_bitwise(parts, one):
     (dict(route_step=5.0, variable_step=0.75, diameter=1.0, q=0.5), 250, True, 3),
     # water quality (qualrout): ghost links' concentrations move once per step
     (dict(route_step=5.0, variable_step=0.75, diameter=1.0, q=0.5, pollutants=3), 250, True, 2)])
-def test_ranks_match_one_gpu_bitwise(kw, steps, surcharged, world, tmp_path):
+def test_ranks_match_one_gpu_bitwise(kw, steps, surcharged, world, transport, tmp_path):
     """Every held node is summed over all its links in the reference's order
     on every rank (ghost links exchanged between neighbours), so the
-    partitioned run is bitwise equal to one GPU."""
+    partitioned run is bitwise equal to one GPU.  host: gloo through the
+    host, eager launches; ipc: the captured step graphs with the ghost
+    values, convergence flags and Courant limits stored by each rank's
+    kernels straight into its peers' memory (the ranks share this box's
+    GPU: IPC within one device)."""
     inp = _grid(tmp_path, 30, 30, **kw)
     one = _run_workers(inp, steps, tmp_path, 1, "host", "one")[0]
     if surcharged:
         st, its, nonconv = one["counters"]
         assert nonconv > 10 and its / st > 2.5, one["counters"]
         assert (one["node.newDepth"][:-1] > kw["diameter"]).sum() > 100
-    parts = _run_workers(inp, steps, tmp_path, world, "host", "part")
+    parts = _run_workers(inp, steps, tmp_path, world, transport, "part")
+    for part in parts:
+        assert _transport_of(part) == transport, _transport_of(part)
     _assert_bitwise(parts, one)
     if kw.get("pollutants"):
         assert (one["node.qual2"] > 1.0).mean() > 0.5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_ipc_stalled_rank_fails_every_rank(world, tmp_path):
+    """Failure detection on the exchange path (swmm5.c:420's sticky error
+    contract): the last rank stops posting its ghost values and flags at step
+    20 (test hook SWMM5_XCHG_STALL); the others' bounded waits (3 s,
+    SWMM5_XCHG_TIMEOUT) give up, tell every rank to stop, and every rank's
+    swmm_step returns error 500 -- no rank hangs."""
+    import time
+    inp = _grid(tmp_path, 30, 30, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.5)
+    t0 = time.time()
+    parts = _run_workers(inp, 400, tmp_path, world, "ipc", "stall",
+                         extra_env={"WORKER_OUT0": str(tmp_path / "stall0.out"),
+                                    "SWMM5_XCHG_STALL": "%d:20" % (world - 1), "SWMM5_XCHG_TIMEOUT": "3"},
+                         timeout=240)
+    elapsed = time.time() - t0
+    for p in parts:
+        codes = [int(c) for c in p["codes"]]
+        msg = bytes(p["msg"]).decode()
+        assert codes[0] == 0 and codes[1] == 500, (codes, msg)
+        assert "exchange" in msg, msg
+    assert elapsed < 150, elapsed
 
 
 def _grid_with_regulators(tmp_path, n=20):
@@ -397,8 +436,10 @@ def _grid_with_regulators(tmp_path, n=20):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,block,pollutants", [(2, 0, 0), (3, 0, 0), (2, 90, 0), (3, 60, 0), (2, 0, 2)])
-def test_ranks_list_graph_bitwise(world, block, pollutants, tmp_path):
+@pytest.mark.parametrize("world,block,pollutants,transport", [
+    (2, 0, 0, "host"), (3, 0, 0, "host"), (2, 90, 0, "host"), (3, 60, 0, "host"), (2, 0, 2, "host"),
+    (2, 0, 0, "ipc"), (3, 60, 0, "ipc"), (2, 0, 2, "ipc")])
+def test_ranks_list_graph_bitwise(world, block, pollutants, transport, tmp_path):
     """The list graph (iterations k >= 2 as unconverged-list walks and
     live-list node passes, each followed by the neighbour exchange and the
     flag all-reduce) on several ranks: every step runs it and the run is
@@ -413,9 +454,10 @@ def test_ranks_list_graph_bitwise(world, block, pollutants, tmp_path):
     one = _run_workers(inp, 250, tmp_path, 1, "host", "one", extra_env=env)[0]
     st, its, nonconv = one["counters"]
     assert nonconv > 10 and its / st > 2.5, one["counters"]
-    parts = _run_workers(inp, 250, tmp_path, world, "host", "part", extra_env=env)
+    parts = _run_workers(inp, 250, tmp_path, world, transport, "part", extra_env=env)
     for part in parts:
         assert part["graphs"][1] == part["counters"][0], (part["graphs"], part["counters"])
+        assert _transport_of(part) == transport
     _assert_bitwise(parts, one)
 
 
@@ -488,17 +530,26 @@ def test_rank0_write_error_stops_every_rank(n, tmp_path):
 
 
 @pytest.mark.gpu
-def test_steady_state_skipping_rejected_with_ranks(tmp_path):
-    """SKIP_STEADY_STATE runs on one GPU only (its flow-error and inflow tests
-    would need a collective every step): with two ranks swmm_start returns
-    ERROR 200 on both, and neither goes on into a collective."""
+@pytest.mark.parametrize("case,transport", [("example_steady", "host"), ("example_steady_var", "host"),
+                                            ("example_steady_pump", "host"), ("example_steady", "ipc"),
+                                            ("example_steady_pump", "ipc")])
+def test_steady_state_skipping_ranks_bitwise(case, transport, tmp_path):
+    """SKIP_STEADY_STATE with two ranks (routing.c:236-244, 383-395): each
+    step's inflow test (and pump switching, routing.c:224) and the previous
+    step's system flow totals are reduced over the ranks, so every rank skips
+    the same steps.  The owned state is bitwise the one-GPU run's and the
+    binary results file rank 0 writes is byte-identical to the one-GPU file
+    (the reference fixtures' networks: a hydrograph that settles; with pumps,
+    storage units and pollutants)."""
+    import shutil
     import _golden
-    inp = _golden.inp("example_steady")
-    parts = _run_workers(inp, 10, tmp_path, 2, "host", "steady",
-                         extra_env={"WORKER_OUT0": str(tmp_path / "steady0.out")}, timeout=300)
-    for p in parts:
-        assert int(p["codes"][0]) == 200, p["codes"]
-        assert "SKIP_STEADY_STATE" in bytes(p["msg"]).decode(), bytes(p["msg"]).decode()
+    inp = str(tmp_path / (case + ".inp"))
+    shutil.copy(_golden.inp(case), inp)
+    one = _run_workers(inp, 100000, tmp_path, 1, "host", "one", save=True)[0]
+    parts = _run_workers(inp, 100000, tmp_path, 2, transport, "two", save=True)
+    assert all((p["link_owner"] == r).any() for r, p in enumerate(parts))
+    _assert_bitwise(parts, one)
+    assert open(str(tmp_path / "two_r0.out"), "rb").read() == open(str(tmp_path / "one_r0.out"), "rb").read()
 
 
 @pytest.mark.gpu
@@ -539,5 +590,7 @@ def test_two_ranks_match_one_gpu_4m(tmp_path):
     assert one["link.newFlow"].size == 3995965
     assert nonconv > 0 and its / st > 3.0, one["counters"]
     assert (one["node.newDepth"][:-1] > cfg["diameter"]).sum() > 1000
-    parts = _run_workers(inp, steps, tmp_path, 2, "host", "two")
-    _assert_bitwise(parts, one)
+    for transport in ("host", "ipc"):
+        parts = _run_workers(inp, steps, tmp_path, 2, transport, "two_" + transport)
+        assert all(_transport_of(p) == transport for p in parts)
+        _assert_bitwise(parts, one)
