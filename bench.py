@@ -178,6 +178,45 @@ def cpu_baseline(dump, steps, q, route_step, variable, threads=1):
     return o.nL * iters / dt, iters / steps, dt
 
 
+def ref_baseline(threads, seconds=10.0):
+    """The reference solver itself (oracle/_ref/ref_timing: EPA SWMM 5.2.4
+    compiled from its own sources, checker infrastructure) on configs[1]'s
+    100k grid (224 x 224, fixed 1 s step), on 1 thread and on `threads`
+    (its THREADS option): `seconds` of its step loop each, timed inside the
+    harness from swmm_start to the last step (parse excluded).  None when the
+    harness was not built (no /root/reference where the oracle was built)."""
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_timing")
+    if not os.path.exists(exe):
+        return None
+    import netgen
+    d = os.path.join("/tmp", "swmm_bench")
+    os.makedirs(d, exist_ok=True)
+    legs = {}
+    for nt in sorted({1, threads}):
+        inp = os.path.join(d, "ref100k_t%d.inp" % nt)
+        netgen.write_grid(inp, 224, 224, route_step=1.0, variable_step=0.0, diameter=1.5, q=0.02,
+                          end_time="23:00:00", report_all=False, threads=nt)
+        out = subprocess.run([exe, inp, os.path.join(d, "ref%d.rpt" % nt), os.path.join(d, "ref%d.out" % nt),
+                              str(seconds), "1000000"], capture_output=True, text=True, timeout=300)
+        r = json.loads(out.stdout.strip().splitlines()[-1])
+        if r["error"] or r["iterations_per_step"] <= 0:
+            return None
+        r["value"] = r["links"] * r["iterations_per_step"] * r["steps"] / r["step_s"]
+        legs[nt] = r
+    one, many = legs[1], legs[threads]
+    return {"value": round(many["value"], 1), "unit": "link-updates/s", "cores": threads, "kind": "reference",
+            "single_thread": {"value": round(one["value"], 1), "cores": 1, "steps": one["steps"],
+                              "seconds": round(one["step_s"], 2)},
+            "parse_s": round(many["open_s"], 2),
+            "iterations_per_step": many["iterations_per_step"],
+            "sample": "EPA SWMM 5.2.4 itself (oracle/_ref/libswmm5_ref.so from /root/reference's sources, -O3 "
+                      "OpenMP) on configs[1]'s 224 x 224 grid (99,905 conduits, fixed 1 s step): %d and %d "
+                      "steps from swmm_start in %.1f s on %d threads and %.1f s on 1 thread (THREADS option; "
+                      "swmm_open's parse, %.2f s, excluded); Picard iterations from its report"
+                      % (many["steps"], one["steps"], many["step_s"], threads, one["step_s"], many["open_s"])}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -471,6 +510,15 @@ def main():
         dist.all_gather_object(allw, mine_w)
         roof["per_rank_sparse_work"] = {"conduits_updated_k>=2": [w[0] for w in allw],
                                         "nodes_updated_k>=2": [w[1] for w in allw]}
+    if world > 1 and kt.get("ghost_exchange", (0, 0))[0]:
+        # the per-iteration exchanges on the routing stream (timing-mode
+        # steps): their cost per Picard iteration on this rank
+        roof["other_kernels"]["ghost_exchange"] = {
+            "avg_us": round(avg_us("ghost_exchange"), 2), "launches": int(kt["ghost_exchange"][0]),
+            "note": "per Picard iteration: pack .. unpack of the strip neighbours' ghost-link values (%s)" % transport}
+        roof["other_kernels"]["flag_exchange"] = {
+            "avg_us": round(avg_us("flag_exchange"), 2), "launches": int(kt["flag_exchange"][0]),
+            "note": "per Picard iteration: the convergence flag reduced over every rank (%s)" % transport}
     if cfg["pollutants"]:
         roof["other_kernels"]["k_qual_node+k_qual_link"] = {
             "avg_launch_us": round(avg_us("quality"), 2), "achieved_GBs": round(gbs("quality"), 1)}
@@ -485,7 +533,12 @@ def main():
             rate, ipc_n, secs = cpu_baseline(dump, args.cpu_steps, cfg["q"], cfg["route_step"],
                                              cfg["variable_step"] > 0, nt)
         os.remove(dump)
+        try:
+            ref = ref_baseline(nt)
+        except Exception as exc:        # noqa: BLE001 -- a baseline, never the measurement
+            ref = {"error": repr(exc)}
         cpu = {"value": round(rate, 1), "unit": "link-updates/s", "cores": nt, "kind": "port",
+               "reference": ref,
                "cpu_model": cpu_model(),
                "single_thread": {"value": round(rate1, 1), "cores": 1, "seconds": round(secs1, 2)},
                "sample": "%d routing steps (%.1f s on %d threads, %.2f iterations/step) of the same "

@@ -60,7 +60,9 @@ int    DLLEXPORT swmmx_getCounters(long long *out, int n);
  *      1 node update of iteration 0, 2 step end (k_step_end .. k_finalize),
  *      3 quality, 4 link momentum, executed iterations >= 1 (bypassed
  *      conduits skipped), 5 node update of iteration 1, 6 node updates of the
- *      executed iterations >= 2.
+ *      executed iterations >= 2, 7 k_sparse + k_unfreeze, 8 ghost-link
+ *      exchange of an iteration (several ranks: pack .. unpack on the routing
+ *      stream), 9 convergence-flag exchange of an iteration (several ranks).
  * Returns the number of classes written. */
 int    DLLEXPORT swmmx_setTiming(int mode);
 int    DLLEXPORT swmmx_getKernelTimes(double *out, int n);

@@ -441,6 +441,16 @@ struct Params {
     const int* hostAbort;         // host-mapped: the host gave up waiting
     long long xTimeout;           // wall-clock ticks a wait may take
     long long stallStep;          // test hook (SWMM5_XCHG_STALL): from this step on this rank posts nothing
+    // shared nodes that freeze (multi-GPU): the unpack of iteration k >= 2
+    // marks a held end of a ghost link whose received values changed
+    // (bitwise) as stale (dirty), exactly as the walk marks the ends of the
+    // conduits it updates, and wakes it if frozen (xwlist / xwcount[k], the
+    // list graph's third item source); with every change seen, a node touched
+    // by ghost links may reuse its sums, relax on its cached depth and freeze
+    // like any other junction.  0: such nodes never do (SWMM5_SHARED_FREEZE=0)
+    int xwake;
+    int* xwlist;                  // [nN] frozen held nodes a changed ghost value woke at iteration k
+    int* xwcount;                 // [maxTrials]
 };
 // this step is skipped as steady (isInSteadyState, routing.c:383-395): read by
 // the launches of Picard iterations 0 and 1 (the later ones see iteration 1's
@@ -1378,7 +1388,10 @@ void k_link(Params p, int k)
     double dt = p.ctl->dt;
     int work = 0;
     if (kFirst && blockIdx.x == 0)
-        for (int t = threadIdx.x; t < p.maxTrials; t += kBlock) { p.ucount[t] = 0; p.vcount[t] = 0; p.wcount[t] = 0; }
+        for (int t = threadIdx.x; t < p.maxTrials; t += kBlock) {
+            p.ucount[t] = 0; p.vcount[t] = 0; p.wcount[t] = 0;
+            if (p.xwcount) p.xwcount[t] = 0;
+        }
     if (kFirst && blockIdx.x == 0 && threadIdx.x == 0) p.ctl->tailBar = 0;
     if (kFirst || k < 2) {
         stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
@@ -1690,8 +1703,8 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
     int c = (fabs(yLast - yNew) > p.headTol) ? 0 : 1;  // dynwave.c:615-621
     SWX_NST(conv, c);
     if (p.convW) convWord(p, i, k, c);
-    if (k >= 1 && k + 1 < p.maxTrials && p.freeze && plain && c && !(nf & (NF_SHARED | NF_DEFER | NF_REPLICA)) &&
-        freezable(p, yNew, yRaw, yMax, yCrown)) {
+    if (k >= 1 && k + 1 < p.maxTrials && p.freeze && plain && c && !(nf & NF_DEFER) &&
+        (p.xwake || !(nf & (NF_SHARED | NF_REPLICA))) && freezable(p, yNew, yRaw, yMax, yCrown)) {
         SWX_NST(frz, (unsigned char)(k + 1));
         return c | 2;                                  // bit 1: frozen by this update
     }
@@ -1949,7 +1962,7 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
                     alive = false;
                     done = true;
                 }
-            } else if (type != OUTFALL && !(nf & (NF_SHARED | NF_DEFER)) && cache == 2) {
+            } else if (type != OUTFALL && !(nf & NF_DEFER) && (p.xwake || !(nf & NF_SHARED)) && cache == 2) {
                 // plain clean junction: the relaxation step of setNodeDepth
                 // (dynwave.c:700-715) on the cached unrelaxed depth
                 double yLast2 = SWX_NIN(y, nNewDepth), yCrown = SWX_NIN(yCrown, yCrown), yRaw = SWX_NIN(yRaw, yRaw),
@@ -2007,8 +2020,8 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
             lat = SWX_NIN(lat, newLat);
         }
         double inflow, outflow, surf, sumdqdh;
-        const bool reuse = !kFirst && k >= 2 && !(nf & (NF_CANPOND | NF_SHARED | NF_DEFER)) &&
-                           type != STORAGE && !(pre.cache & 1);
+        const bool reuse = !kFirst && k >= 2 && !(nf & (NF_CANPOND | NF_DEFER)) &&
+                           (p.xwake || !(nf & NF_SHARED)) && type != STORAGE && !(pre.cache & 1);
         if (reuse) {
             inflow = SWX_NIN(inflow, inflow);
             outflow = SWX_NIN(outflow, outflow);
@@ -2640,6 +2653,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
                                                                                                          int k)
 {
     const int vc = p.vcount[k - 1], uc = p.ucount[k - 1];   // load with the flag below
+    const int xc = p.xwcount ? p.xwcount[k] : 0;             // C: frozen nodes a changed ghost value woke
     if (p.unconv[k - 1] == 0) return;
     probeMark(p, k, PR_N_IN);
     probeMark(p, k, PR_N_LAST_IN);
@@ -2657,7 +2671,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
     }
     const int b = (int)blockIdx.x - (proOnly ? 1 : 0);
     const int nt = ((int)gridDim.x - (proOnly ? 1 : 0)) * kBlock;
-    const int items = vc + 4 * uc;
+    const int items = vc + 4 * uc + xc;
     // a workgroup with no first-round item has none (uniform)
     if (b * kBlock >= items) return;
     __shared__ LdsList<true> ldsU;
@@ -2688,6 +2702,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
     for (int t = b * kBlock + (int)threadIdx.x; t < items; t += nt) {
         if (t < vc) {
             update(vprev[t], vrprev[t]);                 // A (its entry carries the row bounds)
+        } else if (t >= vc + 4 * uc) {                   // C: woken by a ghost value (claimed at the unpack)
+            const int n = p.xwlist[t - vc - 4 * uc];
+            bool listMe = false, alive = false;
+            int2 row = make_int2(0, 0);
+            nodeItem<false, kGeneral>(p, k, n, dt, loadNodePre(p, n, k), listMe, row, anyUnconv, gathered, live,
+                                      fast, alive);
+            sinkAppend(su, listMe, n, row);
+            sinkAppend(sv, alive, n, row);
         } else {                                         // B: a frozen neighbour of a listed node
             const int s = t - vc;
             const int2 rb = rprev[s >> 2];
@@ -3497,6 +3519,31 @@ __global__ __launch_bounds__(kBlock) void k_outfall_qcs(Params p, double* out)
 // order); k_xunpack: the received values into this rank's ghost slots.  The
 // node update then sums every held node over all its links in global link
 // order, exactly as on one GPU.  An iteration after convergence moves nothing.
+// a received ghost value replaces the slot's previous one: when any of its
+// bits changed at iteration k >= 2, the ghost link's held ends are stale
+// (their sums must be gathered again: dirty, as the walk marks the ends of the
+// conduits it updates), and a frozen end is woken -- claimed with k_node_list's
+// stamp (so its frozen-neighbour pass does not take it twice) and listed for
+// that launch (the list graphs; the unrolled k_node scans every node and
+// wakes a frozen one by its dirty mark)
+__device__ __forceinline__ bool ghostChanged(double oldV, double newV)
+{
+    return __double_as_longlong(oldV) != __double_as_longlong(newV);
+}
+__device__ void ghostWake(const Params& p, int l, int k)
+{
+    const int2 nn = p.lnodes[l];
+    const unsigned stamp = (unsigned)p.ctl->totalSteps * (unsigned)(p.maxTrials + 1) + (unsigned)k;
+    for (int s = 0; s < 2; s++) {
+        const int n = s ? nn.y : nn.x;
+        if (n < 0) continue;
+        p.dirty[n] = 1;
+        const int fz = p.frz[n];
+        if (p.buildVlist && fz != 0 && fz <= k && atomicExch(&p.nstamp[n], stamp) != stamp)
+            p.xwlist[atomicAdd(&p.xwcount[k], 1)] = n;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_xpack(Params p, int k)
 {
     if (k >= 2 && p.unconv[k - 1] == 0) return;
@@ -3519,6 +3566,12 @@ __global__ __launch_bounds__(kBlock) void k_xunpack(Params p, int k)
     for (int g = blockIdx.x * kBlock + threadIdx.x; g < p.nGhost; g += gridDim.x * kBlock) {
         const int l = p.nL + g;
         const double* v = p.xrecv + (size_t)p.xF * g;
+        if (p.xwake && k >= 2) {
+            bool ch = ghostChanged(p.lNewFlow[l], v[0]) || ghostChanged(p.sa1[l], v[1]) ||
+                      ghostChanged(p.sa2[l], v[2]) || ghostChanged(p.dqdh[l], v[3]);
+            if (p.xF > 4) ch = ch || ghostChanged(p.evapLoss[l], v[4]) || ghostChanged(p.seepLoss[l], v[5]);
+            if (ch) ghostWake(p, l, k);
+        }
         p.lNewFlow[l] = v[0];
         p.sa1[l] = v[1];
         p.sa2[l] = v[2];
@@ -3652,6 +3705,7 @@ __global__ __launch_bounds__(kBlock) void k_ipc_unpack(Params p, int k)
     double* lq = kQual ? p.lQual[p.ctl->qualPar] : nullptr;
     for (int g = blockIdx.x * kBlock + threadIdx.x; g < p.nGhost; g += gridDim.x * kBlock) {
         const int l = p.nL + g;
+        bool ch = false;
         for (int f = 0; f < F; f++) {
             unsigned lo = 0, hi = 0;
             if (!llWait(p, b + (size_t)(2 * f) * nG + g, seq, &lo, t0) ||
@@ -3660,6 +3714,11 @@ __global__ __launch_bounds__(kBlock) void k_ipc_unpack(Params p, int k)
                 return;
             }
             const double v = llDouble(lo, hi);
+            if (!kQual && p.xwake && k >= 2) {
+                const double o = f == 0 ? p.lNewFlow[l] : f == 1 ? p.sa1[l] : f == 2 ? p.sa2[l] : f == 3 ? p.dqdh[l]
+                               : f == 4 ? p.evapLoss[l] : p.seepLoss[l];
+                ch = ch || ghostChanged(o, v);
+            }
             if (kQual) lq[(size_t)f * p.nLs + l] = v;
             else if (f == 0) p.lNewFlow[l] = v;
             else if (f == 1) p.sa1[l] = v;
@@ -3668,6 +3727,7 @@ __global__ __launch_bounds__(kBlock) void k_ipc_unpack(Params p, int k)
             else if (f == 4) p.evapLoss[l] = v;
             else p.seepLoss[l] = v;
         }
+        if (ch) ghostWake(p, l, k);
     }
 }
 // One wave: iteration k's flag from every rank, ORed into unconv[k] (the
@@ -4845,6 +4905,7 @@ struct Router::Impl {
     bool constantInflow = true;
     struct TimingSlot {               // one timed step's events + readback
         std::vector<hipEvent_t> ev, evHot;
+        std::vector<hipEvent_t> evX;  // several ranks: per iteration [4k, 4k+1] ghost exchange, [4k+2, 4k+3] flag
         unsigned long long* pinned = nullptr;   // [0] iterations run, [1..] conduits updated, nodes gathered
         int mode = 0;                 // graph the step mirrored (0 unrolled, 2 sparse: k >= 2 in k_sparse)
     };
@@ -4858,11 +4919,14 @@ struct Router::Impl {
     int tUsed = 0;
     hipEvent_t* curEv = nullptr;     // event set of the step being launched
     hipEvent_t* curHot = nullptr;
+    hipEvent_t* curX = nullptr;      // evX of the step being launched (null: not timed)
     // kernel classes: 0 k_link<first>, 1 k_node<first>, 2 step end (k_step_end +
     // k_finalize), 3 quality, 4 k_link iterations >= 1, 5 k_node iteration 1,
     // 6 k_node iterations >= 2, 7 k_sparse + k_unfreeze (iterations >= 2 of a
     // sparse-graph step)
-    static constexpr int kClasses = 8;
+    // 8 ghost-link exchange (pack .. unpack, every iteration), 9 convergence
+    // flag exchange (several ranks only)
+    static constexpr int kClasses = 10;
     long long itersTimed1 = 0;        // timed iterations k >= 1 that ran (either graph)
     double kms[kClasses] = {};
     long long kcnt[kClasses] = {};
@@ -4905,6 +4969,7 @@ Router::~Router()
         for (auto& t : d_->tslots) {
             for (auto e : t.ev) (void)hipEventDestroy(e);
             for (auto e : t.evHot) (void)hipEventDestroy(e);
+            for (auto e : t.evX) (void)hipEventDestroy(e);
             if (t.pinned) (void)hipHostFree(t.pinned);
         }
         for (void* a : d_->allocs) (void)hipFree(a);
@@ -5148,7 +5213,15 @@ static int neighbourExchange(Router::Impl* d, int f)
 
 // Iteration k's "some node did not converge" flag, max over the ranks (in
 // place in the per-iteration flags), so every rank runs the same iterations.
+static int flagExchangeImpl(Router::Impl* d, int k);
 static int flagExchange(Router::Impl* d, int k)
+{
+    if (d->curX) (void)hipEventRecord(d->curX[4 * k + 2], d->stream);
+    const int r = flagExchangeImpl(d, k);
+    if (d->curX) (void)hipEventRecord(d->curX[4 * k + 3], d->stream);
+    return r;
+}
+static int flagExchangeImpl(Router::Impl* d, int k)
 {
     int* flag = d->p.unconv + k;
     if (d->part.transport == XCHG_IPC) {
@@ -5173,7 +5246,16 @@ static int flagExchange(Router::Impl* d, int k)
 // pack, transfer, unpack on the RCCL / host transports; on XCHG_IPC the owners
 // store them straight into this rank's ghost area and k_ipc_unpack waits for
 // them.  qualExchange: the ghost links' concentrations, once per step.
+static int ghostExchangeImpl(Router::Impl* d, int k);
 static int ghostExchange(Router::Impl* d, int k)
+{
+    // timing mode: the exchange's span on the routing stream
+    if (d->curX) (void)hipEventRecord(d->curX[4 * k], d->stream);
+    const int r = ghostExchangeImpl(d, k);
+    if (d->curX) (void)hipEventRecord(d->curX[4 * k + 1], d->stream);
+    return r;
+}
+static int ghostExchangeImpl(Router::Impl* d, int k)
 {
     const Params& p = d->p;
     if (d->part.transport == XCHG_IPC) {
@@ -6318,6 +6400,17 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         p.xRank = part.rank;
         p.xRanks = part.nranks;
         p.stallStep = -1;
+        p.xwake = 0;
+        p.xwlist = nullptr;
+        p.xwcount = nullptr;
+        if (part.active()) {                        // shared nodes freeze unless SWMM5_SHARED_FREEZE=0
+            const char* sf = getenv("SWMM5_SHARED_FREEZE");
+            p.xwake = (sf && atoi(sf) == 0) ? 0 : 1;
+            p.xwlist = devAlloc<int>(d, (size_t)std::max(nN, 1), &e);
+            if (e == hipSuccess) p.xwcount = devAlloc<int>(d, (size_t)std::max(p.maxTrials, 1), &e);
+            if (e == hipSuccess) e = hipMemset(p.xwcount, 0, (size_t)std::max(p.maxTrials, 1) * sizeof(int));
+            if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
+        }
         HIPCHECK(hipHostMalloc((void**)&d->xerrHost, 4 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
         HIPCHECK(hipHostMalloc((void**)&d->hostAbortH, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
         memset(d->xerrHost, 0, 4 * sizeof(int));
@@ -6915,6 +7008,13 @@ static void flushTiming(Router::Impl* d)
             }
             const int cn = (k == 0) ? 1 : (k == 1 ? 5 : 6);
             d->kms[cn] += ms2; d->kcnt[cn]++;
+            if (!t.evX.empty()) {                  // several ranks: the two exchanges of iteration k
+                float mx = 0, mf = 0;
+                (void)hipEventElapsedTime(&mx, t.evX[4 * k], t.evX[4 * k + 1]);
+                (void)hipEventElapsedTime(&mf, t.evX[4 * k + 2], t.evX[4 * k + 3]);
+                d->kms[8] += mx; d->kcnt[8]++;
+                d->kms[9] += mf; d->kcnt[9]++;
+            }
             if (k == 0) d->kbytesSum[1] += d->kbytes[1];
             else if (k == 1) d->kbytesSum[5] += d->nodeIter1;
             else {
@@ -7050,6 +7150,8 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
             const int M = std::max(p.maxTrials, 1);
             t.ev.resize(4 * M + 6);
             t.evHot.resize(M);
+            if (d->part.active()) t.evX.resize(4 * (size_t)M);
+            for (auto& ev : t.evX) HIPCHECK(hipEventCreate(&ev));
             for (auto& ev : t.ev) HIPCHECK(hipEventCreate(&ev));
             for (auto& ev : t.evHot) HIPCHECK(hipEventCreate(&ev));
             HIPCHECK(hipHostMalloc((void**)&t.pinned, (1 + 4 * (size_t)M) * sizeof(unsigned long long),
@@ -7058,6 +7160,7 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
         Impl::TimingSlot& t = d->tslots[d->tUsed++];
         d->curEv = t.ev.data();
         d->curHot = t.evHot.data();
+        d->curX = t.evX.empty() ? nullptr : t.evX.data();
         // the sparse tail when the graphs would run it (k_tail steps are
         // timed as the unrolled sequence)
         t.mode = d->useGraph ? chooseGraph(d) : GM_UNROLLED;
@@ -7503,6 +7606,7 @@ void Router::setTiming(bool on)
         d_->p.probeBlocks = 0;
     }
     d_->timing = on;
+    if (!on) d_->curX = nullptr;
     d_->p.countWork = on ? 1 : 0;                  // eager launches only; the graph keeps 0
     for (int k = 0; k < Impl::kClasses; k++) { d_->kms[k] = 0; d_->kcnt[k] = 0; d_->kbytesSum[k] = 0; }
     d_->workSum = 0;

@@ -56,7 +56,7 @@ class EngineMissing(RuntimeError):
 
 # kernel classes of swmmx_getKernelTimes / swmmx_getKernelBytes
 KERNEL_CLASSES = ["link_momentum_first", "node_update_first", "step_end", "quality", "link_momentum_iter",
-                  "node_update_iter1", "node_update_iter2plus", "sparse_tail"]
+                  "node_update_iter1", "node_update_iter2plus", "sparse_tail", "ghost_exchange", "flag_exchange"]
 
 
 def load_library(path: str | None = None):
