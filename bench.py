@@ -568,8 +568,7 @@ def main():
                        "surcharged_pct": round(surcharged, 2),
                        # step graphs the timed steps launched (Router::step's per-step choice)
                        "step_graphs": {g: c1["steps_" + g] - c0["steps_" + g]
-                                       for g in ("unrolled", "tail", "sparse", "list", "fused", "compact")},
-                       "compact_grown_nodes": c1["compact_grown"] - c0["compact_grown"],
+                                       for g in ("unrolled", "tail", "sparse", "list")},
                        "sim_time_at_end_s": round(t_days * 86400.0, 1),
                        "parallelism": ("link-partitioned x%d (row strips); per Picard iteration "
                                        "%s of the strip neighbours' ghost-link values and an "

@@ -43,10 +43,8 @@ int    DLLEXPORT swmmx_runSteps(int n, double *elapsedTime);
  * iterations >= 2, [10] timed iterations >= 1, [11] [12] [13] [14] steps
  * launched with the unrolled, k_tail, k_sparse and list step graphs, [15] 1
  * when the outfall depths of iterations >= 2 are found in the next link
- * launch (deferred outfall prologue), [16] steps launched with the fused
- * step graph (one k_fused launch per iteration >= 2), [17] steps launched
- * with the compact step graph (iterations >= 2 over compact copies of the
- * live sub-network), [18] nodes its walks added to the compact sets (growth).
+ * launch (deferred outfall prologue), [16] [17] [18] retired (the fused and
+ * compact step graphs of rounds 4-5, removed; always 0).
  * Synchronises with the device. */
 int    DLLEXPORT swmmx_getCounters(long long *out, int n);
 

@@ -292,16 +292,6 @@ struct Params {
     // step s is claimed by the one thread that exchanges its stamp to
     // s (MaxTrials + 1) + k first
     unsigned* nstamp;
-    // the fused graph (GM_FUSED) only, else null: convW[i] = (S << 2) |
-    // (c_k << 1) | c_{k-1}, written by node i's update at iteration k of
-    // stamp S (convWord), so that k_fused's conduit filter can read the k-1
-    // flag whether or not the node's iteration-k update has run (convBefore);
-    // outfalls hold kConvOutfall (never converged); lstamp[l] = the stamp of
-    // the iteration whose flow conduit l's producer has published; gNode:
-    // k_fused's claimed nodes
-    unsigned* convW;
-    unsigned* lstamp;
-    int* gNode;
     int* wcount;                  // [maxTrials] wake-list length of iteration k (list graph)
     // non-conduit links (k_nc), in link order
     int nNC, nDef;
@@ -377,7 +367,6 @@ struct Params {
     // iterations 2 <= k < MaxTrials - 1: outfall depths deferred from k_node(k)
     // to the next walk (k_walk, deferredOutfalls); host-checked (Router init)
     int deferPro;
-    int pollSleep;                // k_fused: s_sleep(1) rounds between polls of a stamp (SWMM5_POLL_SLEEP)
     // measurement only (SWMM5_STEPEND_SKIP, PMC attribution of k_step_end's
     // bytes; results are wrong with any bit set): 1 link statistics, 2 link
     // flow-class times, 4 link maxima, 8 node volume totals, 16 node
@@ -397,25 +386,6 @@ struct Params {
     const double* ofQcs;          // [nOutLinks][26] their critical flows at the enumeration's
                                   // depths i yFull / 25 (static geometry: k_outfall_qcs at init)
     StepCtl* ctl;
-    // ---- the compact graph (GM_COMPACT, k_cgather / k_cwalk / k_cnode) ----
-    // In the Params those kernels hand to conduitFlow / nodeItem (compactView)
-    // the node and link arrays point at the compact copies (CView), and wt at
-    // the global arrays, which every store there updates as well
-    // (write-through: the global arrays stay the canonical state at all times)
-    struct WThrough {
-        double *lNewFlow, *lNewDepth, *lNewVolume, *a1, *q1, *dqdh, *froude, *sa1, *sa2, *evapLoss, *seepLoss;
-        int* lstate;
-        double *nNewDepth, *yRaw, *oldSurfArea, *inflow, *outflow, *nSurf, *nDqdh, *nNewVolume, *overflow;
-        int* conv;
-        unsigned char* frz;
-    } wt;
-    // k_node(1) of a compact step: the live nodes' membership (cmStamp[g] =
-    // iterStamp(1), cmCid[g] = their vlist position = compact id); the outfall
-    // prologue then also writes an outfall's compact depth (cOutDepth[cmCid[o]])
-    unsigned* cmStamp;
-    int* cmCid;
-    double* cOutDepth;
-    int* cCnt;                    // CView::cnt: k_unfreeze zeroes the next gather's counters ([1], [3])
     // SKIP_STEADY_STATE: a step in steady state routes no flow (routing.c:
     // 236-244; StepCtl::steadyOk / steadyChanged, stepIsSteady)
     int skipSteady;
@@ -640,30 +610,6 @@ __device__ double conduitLossRate(const Params& p, int j, const Geom& x, double 
 // advances by the relaxation of setNodeDepth's plain branch (dynwave.c:
 // 700-715, omega = 0.5, yNew = yOld + dV / surfArea = yRaw unchanged), the
 // same operations the live update would have made
-// k_fused's convergence words (Params::convW).  The stamp of iteration k of
-// the current step: unique over the run (s (MaxTrials + 1) + k)
-__device__ __forceinline__ unsigned iterStamp(const Params& p, int k)
-{
-    return (unsigned)p.ctl->totalSteps * (unsigned)(p.maxTrials + 1) + (unsigned)k;
-}
-constexpr unsigned kConvOutfall = 0xFFFFFFFCu;      // stamp field above every real stamp, flags 0
-// node i's update at iteration k: c_k, and c_{k-1} from its own word (a word
-// older than k-1: frozen since, so converged)
-__device__ __forceinline__ void convWord(const Params& p, int i, int k, int c)
-{
-    const unsigned s = iterStamp(p, k), w = p.convW[i];
-    const unsigned prev = ((w >> 2) == s - 1) ? ((w >> 1) & 1u) : 1u;
-    p.convW[i] = (s << 2) | ((unsigned)c << 1) | prev;
-}
-// node i converged after iteration k-1 (s = iterStamp(k)), read while its
-// iteration-k update may or may not have run
-__device__ __forceinline__ bool convBefore(unsigned w, unsigned s)
-{
-    const unsigned it = w >> 2;
-    if (it == s) return (w & 1u) != 0;
-    if (it == s - 1) return (w & 2u) != 0;
-    return it < s;                                   // frozen since (converged) / an outfall
-}
 __device__ __forceinline__ double frozenDepthV(double y, double yr, int fz, int m)
 {
     if (fz)
@@ -736,62 +682,17 @@ __device__ __forceinline__ int flowClassOf(const Params& p, int j, const Geom& x
     return fc;
 }
 
-// a store of conduit j's (node i's) state; kWT (the compact graph): p's arrays
-// are the compact copies and the same value also goes to the global array
-// p.wt.<arr> at the global index jg (ig)
-#define SWX_LST(arr, v)                                  \
-    do {                                                 \
-        const auto v_ = (v);                             \
-        p.arr[j] = v_;                                   \
-        if (kWT) p.wt.arr[jg] = v_;                      \
-    } while (0)
-#define SWX_NST(arr, v)                                  \
-    do {                                                 \
-        const auto v_ = (v);                             \
-        p.arr[i] = v_;                                   \
-        if (kWT) p.wt.arr[ig] = v_;                      \
-    } while (0)
 
-// A conduit's inputs of an iteration k >= 1, loaded ahead of the
-// bypass decision (the compact walk: they travel with the slot's own words in
-// one round instead of a dependent round after the filter)
-struct LinkIn {
-    Geom x;
-    double oldFlow, qLast, setting, inv1, inv2, aOld, modLength, len0, roughFactor, beta;
-    int lstate;
-};
-template <bool kFast>
-__device__ __forceinline__ LinkIn loadLinkIn(const Params& p, int j, uint32_t f, const double* ct)
-{
-    LinkIn r;
-    r.x = loadGeom<kFast>(p, j, f, ct);
-    r.oldFlow = p.lOldFlow[j];
-    r.qLast = p.q1[j];
-    r.setting = p.setting[j];
-    r.inv1 = p.inv1[j];
-    r.inv2 = p.inv2[j];
-    r.aOld = p.a2[j];
-    r.modLength = p.modLength[j];
-    r.len0 = p.length[j];
-    r.roughFactor = p.roughFactor[j];
-    r.beta = p.beta[j];
-    r.lstate = p.lstate[j];
-    return r;
-}
-
-// dwflow.c:57-293 -- one conduit, one Picard iteration.  pre: its inputs,
-// already loaded (loadLinkIn; iterations k >= 1 only)
-template <bool kFirst, bool kCold, bool kFast = false, bool kWT = false>
+// dwflow.c:57-293 -- one conduit, one Picard iteration
+template <bool kFirst, bool kCold, bool kFast = false>
 __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, int2 nn, int steps,
-                                            double dt, const double* ct, double yn1, double yn2, int jg = 0,
-                                            const LinkIn* pre = nullptr)
+                                            double dt, const double* ct, double yn1, double yn2)
 {
-    static_assert(!(kWT && kFirst), "write-through only in iterations k >= 2");
     const double omega = 0.5;
     (void)nn;                     // end-node depths arrive as yn1 / yn2
     const double off1 = kCold ? p.off1[j] : 0.0;     // hot links: both offsets are 0
     const double off2 = kCold ? p.off2[j] : 0.0;
-    Geom x = pre ? pre->x : loadGeom<kFast>(p, j, f, ct);
+    Geom x = loadGeom<kFast>(p, j, f, ct);
     double barrels = (double)((f >> LF_BARREL_SHIFT) & 0xFF);
 
     // iteration 0: link_setOldHydState (link.c:564-583), a2 <- a1 (dynwave.c:292)
@@ -806,14 +707,14 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         double a1v = p.a1[j];
         p.a2[j] = a1v;
     } else {
-        oldFlow = pre ? pre->oldFlow : p.lOldFlow[j];
+        oldFlow = p.lOldFlow[j];
     }
-    bool isClosed = ((pre ? pre->setting : p.setting[j]) == 0);
+    bool isClosed = (p.setting[j] == 0);
     double qOld = (barrels == 1.0) ? oldFlow : oldFlow / barrels;   // x / 1 == x
-    double qLast = pre ? pre->qLast : p.q1[j];
+    double qLast = p.q1[j];
     double evapRate = 0.0, seepRate = 0.0;
 
-    double inv1 = pre ? pre->inv1 : p.inv1[j], inv2 = pre ? pre->inv2 : p.inv2[j];
+    double inv1 = p.inv1[j], inv2 = p.inv2[j];
     double z1 = inv1 + off1;
     double z2 = inv2 + off2;
     double h1 = yn1 + inv1;
@@ -828,9 +729,9 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         y1 = gmin(y1, x.yFull);
         y2 = gmin(y2, x.yFull);
     }
-    double aOld = kFirst ? p.a1[j] : (pre ? pre->aOld : p.a2[j]);
+    double aOld = kFirst ? p.a1[j] : p.a2[j];
     aOld = gmax(aOld, 0.0001);
-    double length = pre ? pre->modLength : p.modLength[j];
+    double length = p.modLength[j];
 
     // ---- findSurfArea (dwflow.c:417-550) ----
     int fc;
@@ -921,8 +822,8 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
             wMidF = wMid;
         }
     }
-    SWX_LST(sa1, sa1);
-    SWX_LST(sa2, sa2);
+    p.sa1[j] = sa1;
+    p.sa2[j] = sa2;
 
     double a1, r1, a2, aMid, rMid;
     double yMid = 0.5 * (y1 + y2);
@@ -950,28 +851,28 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         rMid = hydRadAt<kCold>(x, yMid, ct);
     }
     bool isFull = (y1 >= x.yFull && y2 >= x.yFull);
-    double len0 = pre ? pre->len0 : p.length[j];
+    double len0 = p.length[j];
 
     if (fc == F_DRY || fc == F_UP_DRY || fc == F_DN_DRY || isClosed || aMid <= 0.0001) {
         double a1n = 0.5 * (a1 + a2);
-        SWX_LST(a1, a1n);
-        SWX_LST(q1, 0.0);
-        SWX_LST(dqdh, 32.2 * dt * aMid / length * barrels);
-        SWX_LST(froude, 0.0);
-        SWX_LST(lNewDepth, gmin(yMid, x.yFull));
-        SWX_LST(lNewVolume, a1n * len0 * barrels);
-        SWX_LST(lNewFlow, 0.0);
+        p.a1[j] = a1n;
+        p.q1[j] = 0.0;
+        p.dqdh[j] = 32.2 * dt * aMid / length * barrels;
+        p.froude[j] = 0.0;
+        p.lNewDepth[j] = gmin(yMid, x.yFull);
+        p.lNewVolume[j] = a1n * len0 * barrels;
+        p.lNewFlow[j] = 0.0;
         if (f & LF_SEEP) {            // always 0 without LF_SEEP: not rewritten
-            if constexpr (kFast && !kWT) {
+            if constexpr (kFast) {
                 p.rare->evapLoss[j] = 0.0;
                 p.rare->seepLoss[j] = 0.0;
             } else {
-                SWX_LST(evapLoss, 0.0);
-                SWX_LST(seepLoss, 0.0);
+                p.evapLoss[j] = 0.0;
+                p.seepLoss[j] = 0.0;
             }
         }
-        int old = pre ? pre->lstate : p.lstate[j];
-        SWX_LST(lstate, (old & ~0xF) | fc);   // fullState / normalFlow / inletControl untouched (dwflow.c:165-180)
+        int old = p.lstate[j];
+        p.lstate[j] = (old & ~0xF) | fc;   // fullState / normalFlow / inletControl untouched (dwflow.c:165-180)
         return;
     }
 
@@ -980,7 +881,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     double froude;
     if constexpr (kFast) froude = circFroude(p, x, v, yMid, ndM, cM, aMid, wMidF, ct);
     else froude = linkFroude<kCold>(x, v, yMid, ct);
-    SWX_LST(froude, froude);
+    p.froude[j] = froude;
     if (fc == F_SUBCRIT && froude > 1.0) fc = F_SUPCRIT;
 
     double sigma;
@@ -1006,7 +907,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     // culverts, offsets) amplify a last-bit difference into a chaotic value
     // -- with the short form example_shapes' final stored volume moved 1.1 %,
     // where all three reference builds agree
-    else dq1 = dt * (pre ? pre->roughFactor : p.roughFactor[j]) / (kFast ? swxPowFriction(rWtd) : pow(rWtd, 1.33333)) *
+    else dq1 = dt * p.roughFactor[j] / (kFast ? swxPowFriction(rWtd) : pow(rWtd, 1.33333)) *
                fabs(v);
     // the three quotients by the conduit's length and the two by the
     // momentum denominator share a reciprocal pair each (divdd.h
@@ -1023,7 +924,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     if (f & LF_LOSSES) {                                        // dwflow.c:554-571
         double losses = 0.0, qa = fabs(qLast);
         const double *cIn = p.cIn, *cOut = p.cOut, *cAvg = p.cAvg;
-        if constexpr (kFast && !kWT) {
+        if constexpr (kFast) {
             cIn = p.rare->cIn;
             cOut = p.rare->cOut;
             cAvg = p.rare->cAvg;
@@ -1074,7 +975,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
                 }
             }
             if (check) {
-                double qNorm = (pre ? pre->beta : p.beta[j]) * a1 * (kFast ? swxPowTwoThirds(r1) : pow(r1, 2. / 3.));
+                double qNorm = p.beta[j] * a1 * (kFast ? swxPowTwoThirds(r1) : pow(r1, 2. / 3.));
                 if (qNorm < q) {
                     normalFlow = 1;
                     q = qNorm;
@@ -1088,7 +989,7 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
         if (q * qLast < 0.0) q = 0.001 * gsgn(q);
     }
     if (f & LF_QLIMIT) {
-        double ql = (kFast && !kWT) ? p.rare->qLimit[j] : p.qLimit[j];
+        double ql = kFast ? p.rare->qLimit[j] : p.qLimit[j];
         if (fabs(q) > ql) q = gsgn(q) * ql;
     }
     // link_setFlapGate (link.c:643-670)
@@ -1107,27 +1008,27 @@ __device__ __forceinline__ void conduitFlow(const Params& p, int j, uint32_t f, 
     if (q > 0.0001 && yn1 <= 0.0001) q = 0.0001;
     if (q < -0.0001 && yn2 <= 0.0001) q = -0.0001;
 
-    SWX_LST(dqdh, dqdhV);
-    SWX_LST(a1, aMid);
-    SWX_LST(q1, q);
-    SWX_LST(lNewDepth, gmin(yMid, x.yFull));
+    p.dqdh[j] = dqdhV;
+    p.a1[j] = aMid;
+    p.q1[j] = q;
+    p.lNewDepth[j] = gmin(yMid, x.yFull);
     double aAvg = (a1 + a2) / 2.0;
     int fs = 0;
     if (a1 >= x.aFull) fs = (a2 >= x.aFull) ? FS_ALL_FULL : FS_UP_FULL;
     else if (a2 >= x.aFull) fs = FS_DN_FULL;
-    SWX_LST(lNewVolume, aAvg * len0 * barrels);
-    SWX_LST(lNewFlow, q * barrels);
+    p.lNewVolume[j] = aAvg * len0 * barrels;
+    p.lNewFlow[j] = q * barrels;
     if (f & LF_SEEP) {
-        if constexpr (kFast && !kWT) {
+        if constexpr (kFast) {
             p.rare->evapLoss[j] = evapRate;
             p.rare->seepLoss[j] = seepRate;
         } else {
-            SWX_LST(evapLoss, evapRate);
-            SWX_LST(seepLoss, seepRate);
+            p.evapLoss[j] = evapRate;
+            p.seepLoss[j] = seepRate;
         }
     }
-    int old = pre ? pre->lstate : p.lstate[j];
-    SWX_LST(lstate, (old & (1 << 9)) | fc | (fs << 4) | (normalFlow << 8) | (inletCtl << 10));
+    int old = p.lstate[j];
+    p.lstate[j] = (old & (1 << 9)) | fc | (fs << 4) | (normalFlow << 8) | (inletCtl << 10);
 }
 
 // ===========================================================================
@@ -1216,10 +1117,7 @@ __device__ __forceinline__ void probeMark(const Params& p, int k, int slot, unsi
 // wave.  (Per-chunk segments without atomics were measured slower on the
 // surcharged 1M grid: its unconverged nodes are clustered, so the adds are
 // few, and the walk over segments could not pack them as tightly.)
-// mStamp / mCid (the compact graph's live list after iteration 1): i's
-// membership stamp and its list position, its compact id
-__device__ __forceinline__ void waveAppend(bool me, int i, int2 row, int* count, int* list, int2* rows,
-                                           unsigned* mStamp = nullptr, int* mCid = nullptr, unsigned mVal = 0)
+__device__ __forceinline__ void waveAppend(bool me, int i, int2 row, int* count, int* list, int2* rows)
 {
     unsigned long long m = __ballot(me);
     if (m) {
@@ -1230,10 +1128,6 @@ __device__ __forceinline__ void waveAppend(bool me, int i, int2 row, int* count,
             const int e = base + __popcll(m & ((1ull << lane) - 1ull));
             list[e] = i;
             if (rows) rows[e] = row;
-            if (mStamp) {
-                mStamp[i] = mVal;
-                mCid[i] = e;
-            }
         }
     }
 }
@@ -1247,7 +1141,7 @@ __device__ __forceinline__ void waveAppend(bool me, int i, int2 row, int* count,
 // kernels' long pole.  Entries past the buffer go straight to the global
 // list.  Without the buffer (lds == nullptr) every append is waveAppend (the
 // count may itself live in LDS: k_sparse).
-// (kCap: the buffer's entries; k_fused's workgroups append about a hundred)
+// (kCap: the buffer's entries)
 constexpr int kLdsListCap = 512;
 template <bool kRows, int kCap = kLdsListCap>
 struct LdsList {
@@ -1261,14 +1155,11 @@ struct ListSink {
     int* list;
     int2* rows;
     LdsList<kRows, kCap>* lds;
-    unsigned* mStamp;             // (waveAppend) null but for the compact graph's live list
-    int* mCid;
-    unsigned mVal;
 };
 template <bool kRows>
 __device__ __forceinline__ ListSink<kRows> directSink(int* count, int* list, int2* rows = nullptr)
 {
-    return ListSink<kRows>{count, list, rows, nullptr, nullptr, nullptr, 0u};
+    return ListSink<kRows>{count, list, rows, nullptr};
 }
 // workgroup-collective: before the first append (a barrier follows before use)
 template <bool kRows, int kCap>
@@ -1280,7 +1171,7 @@ template <bool kRows, int kCap>
 __device__ __forceinline__ void sinkAppend(const ListSink<kRows, kCap>& s, bool me, int i, int2 row)
 {
     if (!s.lds) {
-        waveAppend(me, i, row, s.count, s.list, kRows ? s.rows : (int2*)nullptr, s.mStamp, s.mCid, s.mVal);
+        waveAppend(me, i, row, s.count, s.list, kRows ? s.rows : (int2*)nullptr);
         return;
     }
     const unsigned long long m = __ballot(me);
@@ -1295,7 +1186,7 @@ __device__ __forceinline__ void sinkAppend(const ListSink<kRows, kCap>& s, bool 
         s.lds->idx[e] = i;
         if (kRows) s.lds->row[e] = row;
     }
-    waveAppend(me && !fits, i, row, s.count, s.list, kRows ? s.rows : (int2*)nullptr, s.mStamp, s.mCid, s.mVal);
+    waveAppend(me && !fits, i, row, s.count, s.list, kRows ? s.rows : (int2*)nullptr);
 }
 // workgroup-collective, after the last append; gbase: an LDS int
 template <bool kRows, int kCap>
@@ -1311,10 +1202,6 @@ __device__ __forceinline__ void sinkFlush(const ListSink<kRows, kCap>& s, int* g
         const int i = s.lds->idx[e];
         s.list[b + e] = i;
         if (kRows) s.rows[b + e] = s.lds->row[e];
-        if (s.mStamp) {
-            s.mStamp[i] = s.mVal;
-            s.mCid[i] = b + e;
-        }
     }
 }
 
@@ -1593,54 +1480,22 @@ __device__ __forceinline__ bool freezable(const Params& p, double yNew, double y
     return true;
 }
 
-// A node's inputs of an iteration k >= 2, loaded in one round ahead of its
-// update (the compact node pass: no load waits for the flag words)
-struct NodeIn {
-    double y, yRaw, yCrown, yMaxNP, yOld, lat, inflow, outflow, surf, dqdh;
-    double fullDepth, pondedArea, oldNetInflow, surDepth, oldSurfArea, fullVolume, oldVolume;
-};
-__device__ __forceinline__ NodeIn loadNodeIn(const Params& p, int i)
-{
-    NodeIn r;
-    r.y = p.nNewDepth[i];
-    r.yRaw = p.yRaw[i];
-    r.yCrown = p.yCrown[i];
-    r.yMaxNP = p.yMaxNP[i];
-    r.yOld = p.nOldDepth[i];
-    r.lat = p.newLat[i];
-    r.inflow = p.inflow[i];
-    r.outflow = p.outflow[i];
-    r.surf = p.nSurf[i];
-    r.dqdh = p.nDqdh[i];
-    r.fullDepth = p.fullDepth[i];
-    r.pondedArea = p.pondedArea[i];
-    r.oldNetInflow = p.oldNetInflow[i];
-    r.surDepth = p.surDepth[i];
-    r.oldSurfArea = p.oldSurfArea[i];
-    r.fullVolume = p.fullVolume[i];
-    r.oldVolume = p.nOldVolume[i];
-    return r;
-}
-// node i's value of field F: preloaded (nin) or from its array
-#define SWX_NIN(F, arr) (nin ? nin->F : p.arr[i])
-
 // setNodeDepth (dynwave.c:636-762) for node i given its summed inflow,
 // outflow, surface area and dq/dh; returns 1 when converged (dynwave.c:615-621)
-template <bool kStorage = true, bool kWT = false>
+template <bool kStorage = true>
 __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_t nf, double dt,
                                           double yLast, double yOld, double inflow, double outflow,
-                                          double surf, double sumdqdh, int ig = 0, const NodeIn* nin = nullptr)
+                                          double surf, double sumdqdh)
 {
-    static_assert(!(kWT && kStorage), "the compact graph has no storage units");
     const double omega = 0.5;
     bool canPond = (nf & NF_CANPOND) != 0;
-    double fullDepth = SWX_NIN(fullDepth, fullDepth);
+    double fullDepth = p.fullDepth[i];
     bool isPonded = (canPond && yLast > fullDepth);
-    double yCrown = SWX_NIN(yCrown, yCrown);
+    double yCrown = p.yCrown[i];
     double overflow = 0.0;
     double surfArea = gmax(surf, p.minSurfArea);
     double dQ = inflow - outflow;
-    double dV = 0.5 * (SWX_NIN(oldNetInflow, oldNetInflow) + dQ) * dt;
+    double dV = 0.5 * (p.oldNetInflow[i] + dQ) * dt;
     const bool isStorage = kStorage && (int)(nf & NF_TYPE) == STORAGE;
     bool isSurcharged = false;
     if (p.surchargeMethod == SUR_EXTRAN) {
@@ -1654,7 +1509,7 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
         dy = dV / surfArea;
         yNew = yOld + dy;
         yRaw = yNew;
-        if (!isPonded) SWX_NST(oldSurfArea, surfArea);
+        if (!isPonded) p.oldSurfArea[i] = surfArea;
         if (k > 0) yNew = (1.0 - omega) * yLast + omega * yNew;
         if (isPonded && yNew < fullDepth) yNew = fullDepth - 0.0001;
     } else {
@@ -1662,7 +1517,7 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
         double denom = sumdqdh;
         if (yLast < 1.25 * yCrown) {
             double fr = (yLast - yCrown) / yCrown;
-            denom += (SWX_NIN(oldSurfArea, oldSurfArea) / dt - sumdqdh) * exp(-15.0 * fr);
+            denom += (p.oldSurfArea[i] / dt - sumdqdh) * exp(-15.0 * fr);
         }
         if (denom == 0.0) dy = 0.0;
         else dy = corr * dQ / denom;
@@ -1672,13 +1527,13 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
     }
     if (yNew < 0) yNew = 0.0;
     double yMax = fullDepth;
-    if (!canPond) yMax += SWX_NIN(surDepth, surDepth);
-    double fullVolume = SWX_NIN(fullVolume, fullVolume);
+    if (!canPond) yMax += p.surDepth[i];
+    double fullVolume = p.fullVolume[i];
     const bool flooded = yNew > yMax;
     const bool plain = !isSurcharged && !canPond && !flooded && fullVolume == 0.0 && !isStorage;
     if (k >= 1) {                                      // fast-path cache for the next iteration
-        if (plain) SWX_NST(yRaw, yRaw);
-        p.dirty[i] = plain ? 2 : 0;                    // (iterations >= 2 read it only from the compact copy)
+        if (plain) p.yRaw[i] = yRaw;
+        p.dirty[i] = plain ? 2 : 0;
     }
     if (flooded) {                                     // getFloodedDepth dynwave.c:766-795
         double newVolume;
@@ -1687,25 +1542,24 @@ __device__ __forceinline__ int nodeUpdate(const Params& p, int i, int k, uint32_
             newVolume = fullVolume;
             yNew = yMax;
         } else {
-            double oldVolume = SWX_NIN(oldVolume, nOldVolume);
+            double oldVolume = p.nOldVolume[i];
             newVolume = gmax((oldVolume + dV), fullVolume);
             overflow = (newVolume - gmax(oldVolume, fullVolume)) / dt;
         }
         if (overflow < 0.0001) overflow = 0.0;
-        SWX_NST(nNewVolume, newVolume);
+        p.nNewVolume[i] = newVolume;
     } else if (kStorage && isStorage) {
         p.nNewVolume[i] = devStorageVolume(p, i, yNew);
     } else {
-        SWX_NST(nNewVolume, (fullDepth > 0.0) ? fullVolume * (yNew / fullDepth) : 0.0);
+        p.nNewVolume[i] = (fullDepth > 0.0) ? fullVolume * (yNew / fullDepth) : 0.0;
     }
-    SWX_NST(overflow, overflow);
-    SWX_NST(nNewDepth, yNew);     // Xnode.dYdT = |yNew - yOld| / dt: formed at the step end
+    p.overflow[i] = overflow;
+    p.nNewDepth[i] = yNew;     // Xnode.dYdT = |yNew - yOld| / dt: formed at the step end
     int c = (fabs(yLast - yNew) > p.headTol) ? 0 : 1;  // dynwave.c:615-621
-    SWX_NST(conv, c);
-    if (p.convW) convWord(p, i, k, c);
+    p.conv[i] = c;
     if (k >= 1 && k + 1 < p.maxTrials && p.freeze && plain && c && !(nf & NF_DEFER) &&
         (p.xwake || !(nf & (NF_SHARED | NF_REPLICA))) && freezable(p, yNew, yRaw, yMax, yCrown)) {
-        SWX_NST(frz, (unsigned char)(k + 1));
+        p.frz[i] = (unsigned char)(k + 1);
         return c | 2;                                  // bit 1: frozen by this update
     }
     return c;
@@ -1753,14 +1607,7 @@ struct BlockSync {
 // kGroups: 32-lane critical-depth groups on waves 1.. (6 = waves 1-3 of a
 // 256-thread block); Sync: the barrier between the team's waves (the whole
 // block, or k_sparse's prologue team only)
-// kCoherentQ (k_fused): the outfall conduits' flows were published by
-// other workgroups in this launch: read them at agent scope (past this XCD's
-// L2), not from a cached line
-__device__ __forceinline__ double loadFlowAgent(const Params& p, int j)
-{
-    return __hip_atomic_load(&p.lNewFlow[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <bool kFirst, bool kGeneral, int kGroups = 6, class Sync = BlockSync, bool kCoherentQ = false>
+template <bool kFirst, bool kGeneral, int kGroups = 6, class Sync = BlockSync>
 __device__ __forceinline__ void outfallPrologue(const Params& p, const double* ct, OutfallLds* sh, bool stage,
                                                 int kProbeK = 0, Sync sync = Sync())
 {
@@ -1782,12 +1629,9 @@ __device__ __forceinline__ void outfallPrologue(const Params& p, const double* c
         double prev = 0.0;
         uint32_t nfo = 0;
         OutfallOps ops{0.0, 0.0, 0.0};
-        // a compact step's iterations k >= 2: the outfall's compact copy too
-        const bool mirror = p.cOutDepth && kProbeK >= 2;
-        int oc = 0;
         if (j >= 0) {
             x = loadGeomEager(p, j, f);
-            q = kCoherentQ ? loadFlowAgent(p, j) : p.lNewFlow[j];
+            q = p.lNewFlow[j];
             if (w == 0) {                              // the outlet node's operands
                 qMax = p.qMax[j];
                 beta = p.beta[j];
@@ -1795,7 +1639,6 @@ __device__ __forceinline__ void outfallPrologue(const Params& p, const double* c
                 prev = p.nNewDepth[o];
                 nfo = p.nflags[o];
                 ops = loadOutfallOps(p, o, j, f);
-                if (mirror) oc = p.cmCid[o];
             }
         }
         const bool cond = (j >= 0) && !(f & LF_NC);
@@ -1819,7 +1662,7 @@ __device__ __forceinline__ void outfallPrologue(const Params& p, const double* c
                     cc = !(ff & LF_NC);
                     if (cc) {
                         xx = loadGeomEager(p, jj, ff);
-                        qq = fabs((kCoherentQ ? loadFlowAgent(p, jj) : p.lNewFlow[jj]) /
+                        qq = fabs(p.lNewFlow[jj] /
                                   (double)((ff >> LF_BARREL_SHIFT) & 0xFF));
                     }
                 }
@@ -1847,7 +1690,6 @@ __device__ __forceinline__ void outfallPrologue(const Params& p, const double* c
             if (p.nNC) p.nPrevDepth[o] = prev;
             const double yo = outfallCombine(p, o, nfo, ops, yn, sh->yc[lane]);
             p.nNewDepth[o] = yo;
-            if (mirror) p.cOutDepth[oc] = yo;
         }
         sync();
     }
@@ -1899,19 +1741,9 @@ __device__ __forceinline__ NodePre loadNodePre(const Params& p, int i, int k)
 }
 
 // alive: not frozen after this iteration (k_sparse's live list)
-// k_fused: rows of at most kFusedMaxDeg entries (its phase-1 lanes take two
-// entries each)
-constexpr int kFusedMaxDeg = 6;
-
 // rowIn: the node's CSR row bounds when its list entry carries them (x < 0:
-// load them).  kCoh (k_fused): the link values were published in this launch
-// by other workgroups -- read at agent scope, past this XCD's L2
-__device__ __forceinline__ double ldAgent(const double* a)
-{
-    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// where a node's gather reads its row and its links' values: the Params' own
-// arrays, or (the compact graph) the compact copies or the global arrays
+// load them)
+// where a node's gather reads its row and its links' values
 struct GatherSrc {
     const int* csr;
     const double *q, *sa1, *sa2, *dqdh, *evap, *seep;
@@ -1921,19 +1753,13 @@ __device__ __forceinline__ GatherSrc gatherSrcOf(const Params& p)
 {
     return GatherSrc{p.csr, p.lNewFlow, p.sa1, p.sa2, p.dqdh, p.evapLoss, p.seepLoss, p.lflags};
 }
-// kWT (the compact graph): p's node arrays are the compact copies, i the
-// compact index, ig the global one (write-through stores, SWX_NST); gsp: the
-// gather's source (rowIn then holds its row bounds)
-template <bool kFirst, bool kGeneral, bool kCoh = false, bool kWT = false>
+template <bool kFirst, bool kGeneral>
 __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double dt, NodePre pre, bool& listMe,
                                          int2& row, bool& anyUnconv, int& gathered, int& live, int& fast,
-                                         bool& alive, int2 rowIn = make_int2(-1, -1),
-                                         const GatherSrc* gsp = nullptr, int ig = 0, const NodeIn* nin = nullptr,
-                                         const int* entPre = nullptr)
+                                         bool& alive, int2 rowIn = make_int2(-1, -1))
 {
     constexpr bool kStorage = kGeneral;
-    static_assert(!(kWT && (kFirst || kGeneral || kCoh)), "the compact graph: iterations >= 2, no storage units");
-    const GatherSrc gs = gsp ? *gsp : gatherSrcOf(p);
+    const GatherSrc gs = gatherSrcOf(p);
         const uint32_t nf = pre.nf;
         int type = (int)(nf & NF_TYPE);
         // an outfall's depth is written by the prologue above: not read here
@@ -1951,13 +1777,13 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
                 // read); once one is updated it is live again from its
                 // depth at the last iteration
                 if (cache & 1) {
-                    yLast = nin ? frozenDepthV(nin->y, nin->yRaw, fz, k - 1) : frozenDepth(p, i, fz, k - 1);
+                    yLast = frozenDepth(p, i, fz, k - 1);
                     haveYLast = true;
-                    SWX_NST(frz, (unsigned char)0);
+                    p.frz[i] = (unsigned char)0;
                 } else {
                     if (k == p.maxTrials - 1) {            // the last possible iteration
-                        SWX_NST(nNewDepth, nin ? frozenDepthV(nin->y, nin->yRaw, fz, k) : frozenDepth(p, i, fz, k));
-                        SWX_NST(frz, (unsigned char)0);
+                        p.nNewDepth[i] = frozenDepth(p, i, fz, k);
+                        p.frz[i] = (unsigned char)0;
                     }
                     alive = false;
                     done = true;
@@ -1965,8 +1791,8 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
             } else if (type != OUTFALL && !(nf & NF_DEFER) && (p.xwake || !(nf & NF_SHARED)) && cache == 2) {
                 // plain clean junction: the relaxation step of setNodeDepth
                 // (dynwave.c:700-715) on the cached unrelaxed depth
-                double yLast2 = SWX_NIN(y, nNewDepth), yCrown = SWX_NIN(yCrown, yCrown), yRaw = SWX_NIN(yRaw, yRaw),
-                       yMax = SWX_NIN(yMaxNP, yMaxNP);
+                double yLast2 = p.nNewDepth[i], yCrown = p.yCrown[i], yRaw = p.yRaw[i],
+                       yMax = p.yMaxNP[i];
                 row = (rowIn.x >= 0) ? rowIn : make_int2(p.rowptr[i], p.rowptr[i + 1]);
                 bool sur = p.surchargeMethod == SUR_EXTRAN && yCrown > 0.0 && yLast2 > yCrown;
                 if (!sur) {
@@ -1974,13 +1800,12 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
                     double yNew = (1.0 - omega) * yLast2 + omega * yRaw;
                     if (yNew < 0) yNew = 0.0;
                     if (!(yNew > yMax)) {
-                        SWX_NST(nNewDepth, yNew);
+                        p.nNewDepth[i] = yNew;
                         int c = (fabs(yLast2 - yNew) > p.headTol) ? 0 : 1;
-                        SWX_NST(conv, c);
-                        if (p.convW) convWord(p, i, k, c);
+                        p.conv[i] = c;
                         if (!c) { anyUnconv = true; listMe = true; }
                         else if (p.freeze && k + 1 < p.maxTrials && freezable(p, yNew, yRaw, yMax, yCrown)) {
-                            SWX_NST(frz, (unsigned char)(k + 1));
+                            p.frz[i] = (unsigned char)(k + 1);
                             alive = false;
                         }
                         done = true;
@@ -1996,7 +1821,7 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
         // reuse test): one dependent round trip fewer before the gather
         const int e0 = (rowIn.x >= 0) ? rowIn.x : p.rowptr[i], e1 = (rowIn.x >= 0) ? rowIn.y : p.rowptr[i + 1];
         row = make_int2(e0, e1);
-        if (!haveYLast) yLast = (type == OUTFALL) ? 0.0 : SWX_NIN(y, nNewDepth);
+        if (!haveYLast) yLast = (type == OUTFALL) ? 0.0 : p.nNewDepth[i];
         double yOld, lat;
         if (kFirst) {
             // routing.c:328-332, node.c:293-304, 325-341 -- step-begin rotation
@@ -2016,23 +1841,23 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
                 p.nExfilVol[i] = xv;
             }
         } else {
-            yOld = SWX_NIN(yOld, nOldDepth);
-            lat = SWX_NIN(lat, newLat);
+            yOld = p.nOldDepth[i];
+            lat = p.newLat[i];
         }
         double inflow, outflow, surf, sumdqdh;
         const bool reuse = !kFirst && k >= 2 && !(nf & (NF_CANPOND | NF_DEFER)) &&
                            (p.xwake || !(nf & NF_SHARED)) && type != STORAGE && !(pre.cache & 1);
         if (reuse) {
-            inflow = SWX_NIN(inflow, inflow);
-            outflow = SWX_NIN(outflow, outflow);
-            surf = SWX_NIN(surf, nSurf);
-            sumdqdh = SWX_NIN(dqdh, nDqdh);
+            inflow = p.inflow[i];
+            outflow = p.outflow[i];
+            surf = p.nSurf[i];
+            sumdqdh = p.nDqdh[i];
         } else {
             // initNodeStates (dynwave.c:297-331)
             bool canPond = (nf & NF_CANPOND) != 0;
-            double fullDepth = SWX_NIN(fullDepth, fullDepth);
+            double fullDepth = p.fullDepth[i];
             surf = 0.0;
-            if (canPond && yLast > fullDepth) surf = SWX_NIN(pondedArea, pondedArea);
+            if (canPond && yLast > fullDepth) surf = p.pondedArea[i];
             inflow = 0.0;
             outflow = 0.0;                        // node losses are 0 for non-storage nodes
             if (kStorage && type == STORAGE) {
@@ -2075,32 +1900,31 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
                 uint32_t lfv[kGather];
 #pragma unroll
                 for (int t = 0; t < kGather; t++)
-                    ent[t] = (eb + t < e1) ? (entPre ? entPre[eb - e0 + t] : gs.csr[eb + t]) : 0;
+                    ent[t] = (eb + t < e1) ? gs.csr[eb + t] : 0;
 #pragma unroll
                 for (int t = 0; t < kGather; t++) {
                     if (eb + t < e1) {
                         const int l = ent[t] & 0x7FFFFFFF;
-                        qv[t] = kCoh ? ldAgent(&gs.q[l]) : gs.q[l];
+                        qv[t] = gs.q[l];
                         lfv[t] = gs.lf[l];
                         const double* sp = (ent[t] < 0) ? &gs.sa2[l] : &gs.sa1[l];
-                        sav[t] = kCoh ? ldAgent(sp) : *sp;
-                        dqv[t] = kCoh ? ldAgent(&gs.dqdh[l]) : gs.dqdh[l];
+                        sav[t] = *sp;
+                        dqv[t] = gs.dqdh[l];
                     }
                 }
 #pragma unroll
                 for (int t = 0; t < kGather; t++) {
                     if (eb + t >= e1) break;
                     const int l = ent[t] & 0x7FFFFFFF;
-                    const double lossSum = (lfv[t] & LF_SEEP) ? (kCoh ? ldAgent(&gs.evap[l]) + ldAgent(&gs.seep[l])
-                                                                      : gs.evap[l] + gs.seep[l])
+                    const double lossSum = (lfv[t] & LF_SEEP) ? (gs.evap[l] + gs.seep[l])
                                                               : 0.0;
                     addEntry(ent[t], qv[t], lfv[t], sav[t], dqv[t], lossSum);
                 }
             }
-            SWX_NST(inflow, inflow);
-            SWX_NST(outflow, outflow);
+            p.inflow[i] = inflow;
+            p.outflow[i] = outflow;
             // (the gather-reuse sums are read by the iterations k >= 2 of this
-            // step only: in the compact graph from the compact copy)
+            // step only)
             p.nSurf[i] = surf;
             p.nDqdh[i] = sumdqdh;
             if (!kFirst && k >= 2) p.dirty[i] = 0;
@@ -2112,8 +1936,7 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
             // conduit sums written above; k_nc adds the non-conduit links
             // and updates the depth
         } else {
-            const int r = nodeUpdate<kStorage, kWT>(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh, ig,
-                                                    nin);
+            const int r = nodeUpdate<kStorage>(p, i, k, nf, dt, yLast, yOld, inflow, outflow, surf, sumdqdh);
             if (!(r & 1)) {
                 anyUnconv = true;
                 listMe = true;
@@ -2136,9 +1959,7 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
     __shared__ int sBase;
     const ListSink<true> su{&p.ucount[k], p.ulist + (size_t)(k & 1) * p.nN, p.ulistRow + (size_t)(k & 1) * p.nN,
                             &ldsU};
-    // (a compact step: the live nodes' membership stamps and compact ids too)
-    const ListSink<true> sv{&p.vcount[1], p.vlist + p.nN, p.vlistRow + p.nN, &ldsV,
-                            p.cmStamp, p.cmCid, iterStamp(p, 1)};
+    const ListSink<true> sv{&p.vcount[1], p.vlist + p.nN, p.vlistRow + p.nN, &ldsV};
     const bool listV = !kFirst && k == 1 && p.buildVlist;
     if (!kFirst) {
         sinkInit(su);
@@ -2739,748 +2560,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral
     probeMark(p, k, PR_N_OUT);
 }
 
-// ---------------------------------------------------------------------------
-// The compact graph (GM_COMPACT): Picard iterations k >= 2 over contiguous
-// copies of the live sub-network, each kernel two dependent memory rounds.
-//
-// After iteration 1 almost every junction of a large network is frozen
-// (converged, plain, relaxing toward its cached depth).  The list graph's
-// iterations k >= 2 chase list -> CSR row -> conduit -> end nodes through a
-// dozen scattered SoA arrays: about five dependent memory rounds per launch,
-// each touching one line per array per node.  Here, once per step, the live
-// nodes L1 of iteration 1 (vlist(1)) and the frozen neighbours of its
-// unconverged nodes (the "ring": the junctions iteration 2 wakes) are copied
-// into dense compact node arrays (k_cgather1), and every conduit incident to
-// one of them into dense compact conduit arrays, each node's row as compact
-// conduit ids (k_cgather2).  Every iteration k >= 2 is then
-//   k_cwalk(k)  one thread per compact conduit: its words and every input of
-//               its momentum update in one round (loadLinkIn), both ends'
-//               state in the second; the conduit is updated unless both
-//               ends converged in iteration k-1 (findBypassedLinks,
-//               dynwave.c:335-345; an outfall never converges) by the same
-//               conduitFlow code (dwflow_findConduitFlow);
-//   k_cnode(k)  one thread per compact node: its state and row in one round
-//               (loadNodeIn), its conduits' values in the second, then
-//               findNodeDepths / setNodeDepth (dynwave.c:593-762, the same
-//               nodeItem code); block 0 the outfall depths
-//               (link_setOutfallDepth, link.c:728-766) as k_node does.
-// No lists are built in iterations k >= 2.
-//
-// Write-through: every store to a compact copy also goes to the global array
-// (SWX_LST / SWX_NST), so the global arrays hold the canonical state at every
-// kernel boundary and a reader may take either; the step end, quality and
-// k_unfreeze read the global arrays as in every other graph.  (A node's
-// `dirty` word is read in iterations k >= 2 only, and there only from the
-// compact copy: it is not written through.)
-//
-// Growth.  A node outside the compact set is frozen: the set holds every node
-// not frozen after iteration 1, and every node that wakes joins.  When an
-// updated conduit has such an end, the walk claims it (CAS of its membership
-// stamp cmStamp to iterStamp(k)) and appends it; k_cnode(k) copies the fresh
-// node, appends its conduits not yet in the set (CAS of lStamp) and updates it
-// with the gather over its global row.  An end outside the set at gather time
-// is named by ~global id and read from the global arrays (canonical:
-// write-through).  Every node k_node(k) would update is therefore in the
-// compact set, every conduit k_link(k) would update is in it, each update is
-// the same code on the same operands, and the results are bitwise those of
-// every other graph.
-//
-// Conduit ids.  A conduit is copied by its lower-numbered end in the set (or
-// its only end in it); k_cgather2 numbers them densely (a workgroup prefix
-// sum, one atomic per workgroup).  A row entry whose conduit the other end
-// copied holds its global id (kUnresolved) until k_cnode resolves it (lCid).
-// Single GPU, no pumps / regulators, no cold conduits, no storage units,
-// freezing on, rows of at most kCompactMaxDeg entries (host-checked:
-// Router::init, compactOk).
-constexpr int kCompactMaxDeg = 8;
-constexpr int kUnresolved = 1 << 30;      // row entry: global conduit id, compact id not yet looked up
-struct CView {
-    int seep;                    // some conduit has LF_SEEP (its depth, volume and losses are copied)
-    int* cnt;                    // [0] compact nodes, [1] compact conduits, [2] nodes grown (run total),
-                                 // [3] ring nodes ([1], [3] zeroed by k_unfreeze: Params::cCnt)
-    unsigned* lStamp;            // per global link: iterStamp of the iteration it joined
-    int* lCid;                   // per global link: its compact id (with lStamp)
-    int *node, *link;            // compact -> global
-    int* deg;                    // per compact node: its row length; -1 gathers over its global row; -2 fresh
-    int* csr;                    // [kCompactMaxDeg per node] compact conduit id (or kUnresolved | global
-                                 // id) | (1 << 31: the node is its node2)
-    int2* ends;                  // per compact conduit: its end nodes, compact id (>= 0) or ~global id
-    // node copies, by compact id
-    uint32_t* nflags;
-    unsigned char *dirty, *frz;
-    int* conv;
-    double *nNewDepth, *yRaw, *yCrown, *yMaxNP, *nOldDepth, *newLat, *inflow, *outflow, *nSurf, *nDqdh;
-    double *fullDepth, *pondedArea, *oldNetInflow, *surDepth, *oldSurfArea, *fullVolume, *nOldVolume;
-    double *nNewVolume, *overflow;                // written only
-    // conduit copies, by compact id; optional groups are null when no conduit needs them
-    uint32_t* lflags;
-    int* lstate;
-    double *lNewFlow, *lOldFlow, *q1, *setting, *inv1, *inv2, *a2, *modLength, *length, *roughFactor, *beta;
-    double *sa1, *sa2, *dqdh;
-    double *a1, *froude, *lNewDepth, *lNewVolume, *evapLoss, *seepLoss;   // written (copied with LF_SEEP)
-    double *cIn, *cOut, *cAvg;                    // LF_LOSSES
-    double* qLimit;                               // LF_QLIMIT
-    double *seepRate, *lOldDepth;                 // LF_SEEP
-    double *yFull, *wMax, *ywMax, *aFull, *rFull, *sFull, *sMax, *yBot, *aBot, *sBot, *rBot;   // not kFast
-};
-
-// the Params conduitFlow / nodeItem see in the compact kernels: node and
-// conduit arrays on the compact copies, write-through to the global ones
-__device__ __forceinline__ Params compactView(const Params& p, const CView& v)
-{
-    Params q = p;
-    q.wt = Params::WThrough{p.lNewFlow, p.lNewDepth, p.lNewVolume, p.a1, p.q1, p.dqdh, p.froude, p.sa1, p.sa2,
-                            p.evapLoss, p.seepLoss, p.lstate, p.nNewDepth, p.yRaw, p.oldSurfArea, p.inflow,
-                            p.outflow, p.nSurf, p.nDqdh, p.nNewVolume, p.overflow, p.conv, p.frz};
-    q.lflags = v.lflags; q.lstate = v.lstate;
-    q.lNewFlow = v.lNewFlow; q.lOldFlow = v.lOldFlow; q.q1 = v.q1; q.setting = v.setting;
-    q.inv1 = v.inv1; q.inv2 = v.inv2; q.a1 = v.a1; q.a2 = v.a2;
-    q.modLength = v.modLength; q.length = v.length; q.roughFactor = v.roughFactor; q.beta = v.beta;
-    q.sa1 = v.sa1; q.sa2 = v.sa2; q.dqdh = v.dqdh; q.froude = v.froude;
-    q.lNewDepth = v.lNewDepth; q.lNewVolume = v.lNewVolume; q.lOldDepth = v.lOldDepth;
-    q.evapLoss = v.evapLoss; q.seepLoss = v.seepLoss; q.seepRate = v.seepRate;
-    q.cIn = v.cIn; q.cOut = v.cOut; q.cAvg = v.cAvg; q.qLimit = v.qLimit;
-    q.yFull = v.yFull; q.wMax = v.wMax; q.ywMax = v.ywMax; q.aFull = v.aFull; q.rFull = v.rFull;
-    q.sFull = v.sFull; q.sMax = v.sMax; q.yBot = v.yBot; q.aBot = v.aBot; q.sBot = v.sBot; q.rBot = v.rBot;
-    q.lTabOff = nullptr;                          // basic shapes only
-    q.nflags = v.nflags; q.dirty = v.dirty; q.frz = v.frz; q.conv = v.conv;
-    q.nNewDepth = v.nNewDepth; q.yRaw = v.yRaw; q.yCrown = v.yCrown; q.yMaxNP = v.yMaxNP;
-    q.nOldDepth = v.nOldDepth; q.newLat = v.newLat; q.inflow = v.inflow; q.outflow = v.outflow;
-    q.nSurf = v.nSurf; q.nDqdh = v.nDqdh; q.fullDepth = v.fullDepth; q.pondedArea = v.pondedArea;
-    q.oldNetInflow = v.oldNetInflow; q.surDepth = v.surDepth; q.oldSurfArea = v.oldSurfArea;
-    q.fullVolume = v.fullVolume; q.nOldVolume = v.nOldVolume; q.nNewVolume = v.nNewVolume;
-    q.overflow = v.overflow;
-    q.csr = v.csr;
-    q.rowptr = nullptr;                           // rows come with each item
-    q.convW = nullptr;
-    return q;
-}
-
-// node g's state into compact node c
-__device__ __forceinline__ void copyNode(const Params& p, const CView& v, int g, int c)
-{
-    const uint32_t nf = p.nflags[g];
-    const unsigned char dy = p.dirty[g], fz = p.frz[g];
-    const int cn = p.conv[g];
-    const double a0 = p.nNewDepth[g], a1 = p.yRaw[g], a2 = p.yCrown[g], a3 = p.yMaxNP[g], a4 = p.nOldDepth[g];
-    const double a5 = p.newLat[g], a6 = p.inflow[g], a7 = p.outflow[g], a8 = p.nSurf[g], a9 = p.nDqdh[g];
-    const double b0 = p.fullDepth[g], b1 = p.pondedArea[g], b2 = p.oldNetInflow[g], b3 = p.surDepth[g];
-    const double b4 = p.oldSurfArea[g], b5 = p.fullVolume[g], b6 = p.nOldVolume[g];
-    v.nflags[c] = nf; v.dirty[c] = dy; v.frz[c] = fz; v.conv[c] = cn;
-    v.nNewDepth[c] = a0; v.yRaw[c] = a1; v.yCrown[c] = a2; v.yMaxNP[c] = a3; v.nOldDepth[c] = a4;
-    v.newLat[c] = a5; v.inflow[c] = a6; v.outflow[c] = a7; v.nSurf[c] = a8; v.nDqdh[c] = a9;
-    v.fullDepth[c] = b0; v.pondedArea[c] = b1; v.oldNetInflow[c] = b2; v.surDepth[c] = b3;
-    v.oldSurfArea[c] = b4; v.fullVolume[c] = b5; v.nOldVolume[c] = b6;
-}
-// conduit l's state into compact conduit m
-__device__ __forceinline__ void copyLink(const Params& p, const CView& v, int l, int m)
-{
-    const uint32_t f = p.lflags[l];
-    const int st = p.lstate[l];
-    const double a0 = p.lNewFlow[l], a1 = p.lOldFlow[l], a2 = p.q1[l], a3 = p.setting[l], a4 = p.inv1[l];
-    const double a5 = p.inv2[l], a6 = p.a2[l], a7 = p.modLength[l], a8 = p.length[l], a9 = p.roughFactor[l];
-    const double b0 = p.beta[l], b1 = p.sa1[l], b2 = p.sa2[l], b3 = p.dqdh[l];
-    v.lflags[m] = f; v.lstate[m] = st;
-    v.lNewFlow[m] = a0; v.lOldFlow[m] = a1; v.q1[m] = a2; v.setting[m] = a3; v.inv1[m] = a4;
-    v.inv2[m] = a5; v.a2[m] = a6; v.modLength[m] = a7; v.length[m] = a8; v.roughFactor[m] = a9;
-    v.beta[m] = b0; v.sa1[m] = b1; v.sa2[m] = b2; v.dqdh[m] = b3;
-    if (v.cIn) { v.cIn[m] = p.cIn[l]; v.cOut[m] = p.cOut[l]; v.cAvg[m] = p.cAvg[l]; }
-    if (v.qLimit) v.qLimit[m] = p.qLimit[l];
-    if (v.seep) {
-        v.seepRate[m] = p.seepRate[l]; v.lOldDepth[m] = p.lOldDepth[l];
-        v.lNewDepth[m] = p.lNewDepth[l]; v.lNewVolume[m] = p.lNewVolume[l];
-        v.evapLoss[m] = p.evapLoss[l]; v.seepLoss[m] = p.seepLoss[l];
-    }
-    if (v.yFull) {
-        v.yFull[m] = p.yFull[l]; v.wMax[m] = p.wMax[l]; v.ywMax[m] = p.ywMax[l]; v.aFull[m] = p.aFull[l];
-        v.rFull[m] = p.rFull[l]; v.sFull[m] = p.sFull[l]; v.sMax[m] = p.sMax[l]; v.yBot[m] = p.yBot[l];
-        v.aBot[m] = p.aBot[l]; v.sBot[m] = p.sBot[l]; v.rBot[m] = p.rBot[l];
-    }
-}
-
-// After k_node(1) of a compact step.  Threads [0, vc): the live nodes L1
-// (vlist(1); k_node(1) stamped them with their list position = compact id)
-// copied into the compact node arrays.  Threads [vc, vc + 4 uc): four per
-// unconverged node of iteration 1 (ulist(1)) over its row: a frozen neighbour
-// is claimed (CAS of its stamp) and appended after L1 (the ring; one atomic
-// per wave on cnt[3]).
-__global__ __launch_bounds__(kBlock) void k_cgather1(Params p, CView v)
-{
-    const int vc = p.vcount[1], uc = p.ucount[1];
-    if (p.unconv[1] == 0) return;                 // converged at iteration 1: no iteration k >= 2 runs
-    const unsigned s1 = iterStamp(p, 1);
-    const int* vl = p.vlist + p.nN;
-    const int* ul = p.ulist + p.nN;
-    const int2* ur = p.ulistRow + p.nN;
-    const int items = vc + 4 * uc;
-    for (int t0 = blockIdx.x * kBlock; t0 < items; t0 += gridDim.x * kBlock) {   // (uniform per wave)
-        const int t = t0 + (int)threadIdx.x;
-        if (t < vc) {
-            const int g = vl[t];
-            copyNode(p, v, g, t);
-            v.node[t] = g;
-        }
-        const int s = t - vc;
-        int2 rb = make_int2(0, 0);
-        if (s >= 0 && t < items) rb = ur[s >> 2];
-        (void)ul;
-        for (int e0 = rb.x + (s & 3); __any(s >= 0 && t < items && e0 < rb.y); e0 += 4) {
-            const bool in = s >= 0 && t < items && e0 < rb.y;
-            int o = -1;
-            bool mine = false;
-            if (in) {
-                o = p.csrOther[e0];
-                const unsigned st = p.cmStamp[o];
-                mine = st != s1 && atomicCAS(&p.cmStamp[o], st, s1) == st;
-            }
-            const unsigned long long m = __ballot(mine);
-            if (m) {
-                const int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1;
-                int base = 0;
-                if (lane == leader) base = atomicAdd(&v.cnt[3], __popcll(m));
-                base = __shfl(base, leader, 64);
-                if (mine) {
-                    const int c = vc + base + __popcll(m & ((1ull << lane) - 1ull));
-                    p.cmCid[o] = c;
-                    v.node[c] = o;
-                    copyNode(p, v, o, c);
-                }
-            }
-        }
-    }
-}
-
-// One thread per compact node of k_cgather1: the conduits of its row that it
-// copies (see "Conduit ids"), numbered densely, and its row as compact ids.
-__global__ __launch_bounds__(kBlock) void k_cgather2(Params p, CView v)
-{
-    const int vc = p.vcount[1], ring = v.cnt[3];
-    if (p.unconv[1] == 0) return;
-    const int nm = vc + ring;
-    if (blockIdx.x == 0 && threadIdx.x == 0) v.cnt[0] = nm;
-    const unsigned s1 = iterStamp(p, 1);
-    __shared__ int wsum[kBlock / 64];
-    __shared__ int sBase;
-    for (int c0 = blockIdx.x * kBlock; c0 < nm; c0 += gridDim.x * kBlock) {      // uniform per workgroup
-        const int c = c0 + (int)threadIdx.x;
-        const bool in = c < nm;
-        int g = 0, e0 = 0, deg = 0;
-        if (in) {
-            g = v.node[c];
-            e0 = p.rowptr[g];
-            deg = p.rowptr[g + 1] - e0;
-        }
-        int ent[kCompactMaxDeg], o[kCompactMaxDeg];
-        unsigned ost[kCompactMaxDeg];
-        int oc[kCompactMaxDeg];
-#pragma unroll
-        for (int r = 0; r < kCompactMaxDeg; r++) {
-            ent[r] = (r < deg) ? p.csr[e0 + r] : 0;
-            o[r] = (r < deg) ? p.csrOther[e0 + r] : -1;
-        }
-#pragma unroll
-        for (int r = 0; r < kCompactMaxDeg; r++) {
-            ost[r] = (o[r] >= 0) ? p.cmStamp[o[r]] : 0u;
-            oc[r] = (o[r] >= 0) ? p.cmCid[o[r]] : 0;
-        }
-        unsigned own = 0;
-#pragma unroll
-        for (int r = 0; r < kCompactMaxDeg; r++)
-            if (o[r] >= 0 && (ost[r] != s1 || g < o[r])) own |= 1u << r;
-        // workgroup exclusive prefix sum of the owned counts -> dense ids
-        const int mineN = __popc(own);
-        int incl = mineN;
-        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-        for (int off = 1; off < 64; off <<= 1) {
-            const int y = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += y;
-        }
-        if (lane == 63) wsum[w] = incl;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int tot = 0;
-            for (int q = 0; q < kBlock / 64; q++) tot += wsum[q];
-            sBase = tot ? atomicAdd(&v.cnt[1], tot) : 0;
-        }
-        __syncthreads();
-        int before = sBase;
-        for (int q = 0; q < w; q++) before += wsum[q];
-        int id = before + incl - mineN;
-        __syncthreads();                          // (wsum / sBase reused by the next round)
-#pragma unroll
-        for (int r = 0; r < kCompactMaxDeg; r++) {
-            if (r >= deg) break;
-            const int l = ent[r] & 0x7FFFFFFF, n2 = ent[r] & (int)0x80000000;
-            if ((own >> r) & 1u) {
-                const int oe = (ost[r] == s1) ? oc[r] : ~o[r];
-                copyLink(p, v, l, id);
-                v.link[id] = l;
-                v.ends[id] = n2 ? make_int2(oe, c) : make_int2(c, oe);
-                v.lStamp[l] = s1;
-                v.lCid[l] = id;
-                v.csr[kCompactMaxDeg * c + r] = id | n2;
-                id++;
-            } else {
-                v.csr[kCompactMaxDeg * c + r] = kUnresolved | l | n2;
-            }
-        }
-        if (in) v.deg[c] = deg;
-    }
-}
-
-// an end of a conduit updated in iteration k: its sums are stale (dirty); an
-// end outside the compact set (frozen) is woken: claimed and appended
-__device__ __forceinline__ void cWake(const Params& p, const CView& v, int e, unsigned st, unsigned s1, unsigned sK)
-{
-    if (e >= 0) {
-        v.dirty[e] = 1;
-        return;
-    }
-    const int g = ~e;
-    if (st >= s1) {
-        if (st < sK) v.dirty[p.cmCid[g]] = 1;     // joined in an earlier launch
-        return;                                    // (sK: claimed in this launch, its claimer marks it)
-    }
-    if (atomicCAS(&p.cmStamp[g], st, sK) != st) return;   // claimed by another thread of this launch
-    const int c = atomicAdd(&v.cnt[0], 1);
-    v.node[c] = g;
-    v.deg[c] = -2;                                 // fresh: k_cnode(k) copies and updates it
-    p.cmCid[g] = c;
-    atomicAdd(&v.cnt[2], 1);
-}
-
-template <bool kFast>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kLinkWavesDefault))) void k_cwalk(Params p,
-                                                                                                       CView v,
-                                                                                                       int k)
-{
-    const int n = v.cnt[1];                       // loads with the flag below
-    if (p.unconv[k - 1] == 0) return;             // converged: dynwave.c:249-251
-    if (blockIdx.x * kBlock >= n) return;         // a workgroup with no first-round conduit has none (uniform)
-    probeMark(p, k, PR_L_IN);
-    const int tid = blockIdx.x * kBlock + threadIdx.x, nthr = gridDim.x * kBlock;
-    __shared__ double ct[kFast ? kCtFast : 5 * SWX_CIRC_N];
-    stageTables(ct, p.gTables, kFast ? p.nGeom : 0);
-    probeMark(p, k, PR_L_STAGED);
-    const Params pc = compactView(p, v);
-    const double dt = p.ctl->dt;
-    const unsigned s1 = iterStamp(p, 1), sK = iterStamp(p, k);
-    int work = 0;
-    for (int m = tid; m < n; m += nthr) {
-        // round 1: the conduit's words and every input of its update
-        const int l = v.link[m];
-        const uint32_t f = v.lflags[m];
-        const int2 en = v.ends[m];
-        const LinkIn in = loadLinkIn<kFast>(pc, m, f, ct);
-        // round 2: both ends' state (compact copy, or the global arrays for an
-        // end outside the set: one load each through a selected base)
-        const bool r1 = en.x >= 0, r2 = en.y >= 0;
-        const int i1 = r1 ? en.x : ~en.x, i2 = r2 ? en.y : ~en.y;
-        const double d1 = (r1 ? v.nNewDepth : p.nNewDepth)[i1], d2 = (r2 ? v.nNewDepth : p.nNewDepth)[i2];
-        const double y1r = (r1 ? v.yRaw : p.yRaw)[i1], y2r = (r2 ? v.yRaw : p.yRaw)[i2];
-        const int f1 = (r1 ? v.frz : p.frz)[i1], f2 = (r2 ? v.frz : p.frz)[i2];
-        const int c1 = (r1 ? v.conv : p.conv)[i1], c2 = (r2 ? v.conv : p.conv)[i2];
-        const unsigned st1 = r1 ? 0u : p.cmStamp[i1], st2 = r2 ? 0u : p.cmStamp[i2];
-        const bool listed1 = (f & LF_N1_OUTFALL) || !c1, listed2 = (f & LF_N2_OUTFALL) || !c2;
-        if (!listed1 && !listed2) continue;       // both ends converged: bypassed
-        const double y1 = frozenDepthV(d1, y1r, f1, k - 1);
-        const double y2 = frozenDepthV(d2, y2r, f2, k - 1);
-        conduitFlow<false, false, kFast, true>(pc, m, f, make_int2(0, 0), k, dt, ct, y1, y2, l, &in);
-        cWake(p, v, en.x, st1, s1, sK);
-        cWake(p, v, en.y, st2, s1, sK);
-        work++;
-    }
-    probeMark(p, k, PR_L_WORK);
-    probeMark(p, k, PR_L_OUT);
-    if (p.countWork) {                            // measurement only
-        for (int off = 32; off > 0; off >>= 1) work += __shfl_down(work, off, 64);
-        if ((threadIdx.x & 63) == 0 && work) atomicAdd(&p.work[k], (unsigned long long)work);
-    }
-}
-
-// a fresh node (woken by the walk of this iteration): its copy, then its
-// conduits not yet in the set (each appended by one of its fresh ends);
-// returns its flag words for the update
-__device__ __forceinline__ NodePre cFresh(const Params& p, const CView& v, int g, int c, unsigned s1, unsigned sK)
-{
-    copyNode(p, v, g, c);
-    v.dirty[c] = 1;                               // an incident conduit was updated
-    v.deg[c] = -1;                                // gathers over its global row from now on
-    const int e0 = p.rowptr[g], e1 = p.rowptr[g + 1];
-    for (int e = e0; e < e1; e++) {
-        const int ent = p.csr[e], l = ent & 0x7FFFFFFF;
-        const unsigned ls = v.lStamp[l];
-        if (ls >= s1) continue;                   // in the set already (or appended in this launch)
-        if (atomicCAS(&v.lStamp[l], ls, sK) != ls) continue;
-        const int m = atomicAdd(&v.cnt[1], 1);
-        copyLink(p, v, l, m);
-        v.link[m] = l;
-        v.lCid[l] = m;
-        const int oe = ~p.csrOther[e];
-        v.ends[m] = (ent < 0) ? make_int2(oe, c) : make_int2(c, oe);
-    }
-    return NodePre{p.nflags[g], 1, p.frz[g]};
-}
-
-#ifndef SWX_CNODE_WAVES
-#define SWX_CNODE_WAVES 3
-#endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SWX_CNODE_WAVES))) void k_cnode(Params p, CView v,
-                                                                                                      int k)
-{
-    const int n = v.cnt[0];                       // loads with the flag below
-    if (p.unconv[k - 1] == 0) return;
-    probeMark(p, k, PR_N_IN);
-    probeMark(p, k, PR_N_LAST_IN);
-    // block 0: the outfall depths of this iteration (as k_node), also into
-    // their compact copies (Params::cOutDepth)
-    const bool proOnly = p.nOutLinks > 0 && p.nOutLinks <= 64 && gridDim.x > 1;
-    if (blockIdx.x * 64 < p.nOutLinks) {
-        __shared__ OutfallLds sh;
-        outfallPrologue<false, false>(p, p.gTables, &sh, false, k);
-        if (blockIdx.x == 0) probeMark(p, k, PR_N_PRO);
-        if (proOnly) {
-            probeMark(p, k, PR_N_OUT);
-            probeMark(p, k, PR_N_B0);
-            return;
-        }
-    }
-    const int b = (int)blockIdx.x - (proOnly ? 1 : 0);
-    const int nt = ((int)gridDim.x - (proOnly ? 1 : 0)) * kBlock;
-    if (b * kBlock >= n) return;                  // uniform
-    const Params pc = compactView(p, v);
-    const GatherSrc gc{v.csr, v.lNewFlow, v.sa1, v.sa2, v.dqdh, v.evapLoss, v.seepLoss, v.lflags};
-    const GatherSrc gg = gatherSrcOf(p);
-    const double dt = p.ctl->dt;
-    const unsigned s1 = iterStamp(p, 1), sK = iterStamp(p, k);
-    bool anyUnconv = false;
-    int gathered = 0, live = 0, fast = 0;
-    for (int c = b * kBlock + (int)threadIdx.x; c < n; c += nt) {
-        // round 1: the node's words, state and row
-        int deg = v.deg[c];
-        const int g = v.node[c];
-        NodePre pre{v.nflags[c], v.dirty[c], v.frz[c]};
-        const NodeIn nin = loadNodeIn(pc, c);
-        int ent[kCompactMaxDeg];
-        {
-            const int4 a = *reinterpret_cast<const int4*>(v.csr + (size_t)kCompactMaxDeg * c);
-            ent[0] = a.x; ent[1] = a.y; ent[2] = a.z; ent[3] = a.w;
-            if (deg > 4) {
-                const int4 q = *reinterpret_cast<const int4*>(v.csr + (size_t)kCompactMaxDeg * c + 4);
-                ent[4] = q.x; ent[5] = q.y; ent[6] = q.z; ent[7] = q.w;
-            } else {
-                ent[4] = ent[5] = ent[6] = ent[7] = 0;
-            }
-        }
-        bool listMe = false, alive = true;
-        int2 row = make_int2(0, 0);
-        if (deg >= 0) {
-            // row entries whose conduit the other end copied: their compact ids
-#pragma unroll
-            for (int r = 0; r < kCompactMaxDeg; r++)
-                if (r < deg && (ent[r] & kUnresolved)) {
-                    const int n2 = ent[r] & (int)0x80000000;
-                    ent[r] = v.lCid[ent[r] & (kUnresolved - 1)] | n2;
-                    v.csr[(size_t)kCompactMaxDeg * c + r] = ent[r];
-                }
-            // round 2 (in nodeItem's gather): the conduits' compact values
-            nodeItem<false, false, false, true>(pc, k, c, dt, pre, listMe, row, anyUnconv, gathered, live, fast,
-                                                alive, make_int2(0, deg), &gc, g, &nin, ent);
-        } else {
-            // grown: the gather over its global row (a fresh node copied first)
-            if (deg == -2) pre = cFresh(p, v, g, c, s1, sK);
-            nodeItem<false, false, false, true>(pc, k, c, dt, pre, listMe, row, anyUnconv, gathered, live, fast,
-                                                alive, make_int2(p.rowptr[g], p.rowptr[g + 1]), &gg, g);
-        }
-    }
-    nodePassEnd(p, k, anyUnconv, gathered, live, fast, true);
-    probeMark(p, k, PR_N_OUT);
-}
-
-// ---------------------------------------------------------------------------
-// k_fused: Picard iteration k >= 2 in ONE launch (the fused graph, GM_FUSED).
-// The list graph's two launches per iteration (walk, then node update) are
-// latency chains of ~13 and ~19 us on the surcharged 1M grid; here every node
-// k_node(k) would update -- (A) the live list of k-1 and (B) the frozen
-// neighbours of its unconverged list (see k_node_list) -- is a group of four
-// lanes, one per CSR entry of its row, and each updated conduit (an end
-// unconverged after k-1: findBypassedLinks, dynwave.c:335-345) is computed
-// once, by its lower-numbered end's lane (both ends of an updated conduit are
-// in A or B), which publishes it; the other end's lane waits for it.  Then
-// the group's first lane runs the node update (nodeItem) on the row's values
-// collected in LDS, in CSR order -- the reference's operations in its order,
-// so the results are bitwise those of the unrolled graph.
-//
-// Ordering without grid barriers:
-//  * a node's state (depth, frz, yRaw) is read only by the producers of its
-//    updated conduits, and its update waits for all of them, so no producer
-//    can read a value of iteration k; the conduit filter reads the k-1
-//    convergence flags through convW, whose words keep c_{k-1} beside c_k;
-//  * only the producer reads a conduit's last flow (q1) and writes its state;
-//  * a producer publishes the five values the other end gathers (flow,
-//    surface areas, dq/dh, losses) with agent-scope stores (through the XCD's
-//    L2 to memory), drains them (s_waitcnt vmcnt(0)), then stores the
-//    conduit's stamp; the consumer polls the stamp and reads the values at
-//    agent scope.  No agent-scope release fence: that writes back the whole
-//    L2, which is what made k_tail's grid barriers slow;
-//  * deadlock freedom: the grid is resident (host-checked occupancy) and every
-//    thread produces all its conduits (phase 1) before it waits for any
-//    (phase 2).  The polls are bounded; a timeout sets StepCtl::tailErr and
-//    fails the step (as k_tail does).
-// Block 0 runs the outfall prologue once the outfall conduits are published.
-// Single GPU, no pumps / regulators / cold conduits, freezing on, rows of at
-// most kFusedMaxDeg entries (host-checked); the frozen junctions' final
-// depths come from k_unfreeze.
-__device__ __forceinline__ bool pollStamp(const Params& p, const unsigned* addr, unsigned want)
-{
-    for (unsigned spins = 0; __hip_atomic_load(addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want;) {
-        // (every poll is a load past the L2: spaced out, they leave the
-        // memory pipeline to the producers)
-        for (int z = 0; z < p.pollSleep; z++) __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 22)) {                   // ~seconds: never expected
-            __hip_atomic_store(&p.ctl->tailErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return false;
-        }
-        if ((spins & 4095) == 0 &&
-            __hip_atomic_load(&p.ctl->tailErr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-            return false;
-    }
-    return true;
-}
-template <bool kFast, bool kGeneral>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGeneral ? 2 : 4))) void k_fused(Params p,
-                                                                                                      int k)
-{
-    const int vc = p.vcount[k - 1], uc = p.ucount[k - 1];   // load with the flag below
-    if (p.unconv[k - 1] == 0) return;                      // converged: dynwave.c:249-251
-    const unsigned stamp = iterStamp(p, k);
-    const int pc = (k - 1) & 1, c = k & 1;
-    probeMark(p, k, PR_L_IN);
-    // c_{k-1} of node i: a plain load suffices, its word holds c_{k-1}
-    // before and after the node's iteration-k update
-    auto convPrev = [&](int i) { return convBefore(p.convW[i], stamp); };
-    __shared__ double ct[kFast ? kCtFast : 5 * SWX_CIRC_N];
-    if (blockIdx.x == 0) {
-        // the outfall depths of iteration k (link_setOutfallDepth, dynwave.c:605),
-        // from the outfall conduits' flows once their producers published them;
-        // the root finders' tables from LDS (staged by the prologue): their
-        // lookups are dependent loads, and the memory system is busy here
-        __shared__ OutfallLds sh;
-        for (int t = threadIdx.x; t < p.nOutLinks; t += kBlock) (void)pollStamp(p, &p.lstamp[outLinkAt(p, t)], stamp);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);       // (as in phase 2 below)
-        __syncthreads();
-        probeMark(p, k, PR_N_PRO);
-        if (p.nOutLinks > 0) outfallPrologue<false, kGeneral, 6, BlockSync, true>(p, ct, &sh, true, k);
-        probeMark(p, k, PR_N_B0);
-        return;
-    }
-    constexpr int kCap = 128;
-    __shared__ LdsList<true, kCap> ldsU;
-    __shared__ LdsList<true, kCap> ldsV;
-    __shared__ int sBase, sClaimed;
-    const ListSink<true, kCap> su{&p.ucount[k], p.ulist + (size_t)c * p.nN, p.ulistRow + (size_t)c * p.nN, &ldsU};
-    const ListSink<true, kCap> sv{&p.vcount[k], p.vlist + (size_t)c * p.nN, p.vlistRow + (size_t)c * p.nN, &ldsV};
-    sinkInit(su);
-    sinkInit(sv);
-    if (threadIdx.x == 0) sClaimed = 0;
-    const int W = (int)gridDim.x - 1, b = (int)blockIdx.x - 1;
-    // this workgroup's share: live-list entries [aLo, aHi) and candidate
-    // slots [cLo, cHi) (four per unconverged node of k-1: its CSR entries)
-    const int aLo = (int)((long long)vc * b / W), aHi = (int)((long long)vc * (b + 1) / W);
-    const int cLo = (int)(4LL * uc * b / W), cHi = (int)(4LL * uc * (b + 1) / W);
-    const int* vprev = p.vlist + (size_t)pc * p.nN;
-    const int2* vrprev = p.vlistRow + (size_t)pc * p.nN;
-    const int2* rprev = p.ulistRow + (size_t)pc * p.nN;
-    stageTables(ct, p.gTables, kFast ? p.nGeom : 0);   // (its barrier publishes the counts' zeroes)
-    probeMark(p, k, PR_L_STAGED);
-    // B: the frozen neighbours of the unconverged nodes of k-1 (see
-    // k_node_list), claimed one thread per candidate slot and compacted into
-    // this workgroup's part of gNode
-    for (int t = cLo + (int)threadIdx.x; t - (int)threadIdx.x < cHi; t += kBlock) {
-        int cand = -1;
-        if (t < cHi) {
-            const int2 rb = rprev[t >> 2];
-            const int e = rb.x + (t & 3);
-            if (e < rb.y) {
-                const int o = p.csrOther[e];
-                if (o >= 0) {
-                    const int fz = p.frz[o];
-                    if (fz != 0 && fz <= k && atomicExch(&p.nstamp[o], stamp) != stamp) cand = o;
-                }
-            }
-        }
-        const unsigned long long m = __ballot(cand >= 0);
-        if (m) {
-            const int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1;
-            int base = 0;
-            if (lane == leader) base = atomicAdd(&sClaimed, __popcll(m));
-            base = __shfl(base, leader, 64);
-            if (cand >= 0) p.gNode[cLo + base + __popcll(m & ((1ull << lane) - 1ull))] = cand;
-        }
-    }
-    __syncthreads();
-    const int aN = aHi - aLo, nItems = aN + sClaimed;
-    const double dt = p.ctl->dt;
-    const int lane4 = threadIdx.x & 3, g0 = (int)threadIdx.x >> 2;
-    // one group item: the node, its row, and this lane's (at most two, rows
-    // of at most kFusedMaxDeg = 6) CSR entries with their update flags --
-    // loaded once for the first round (kept in registers for phase 2)
-    struct GroupItem {
-        int n;
-        int2 row;
-        int ent[2], o[2];
-        unsigned upd;            // bit j: entry j's conduit is updated at k
-    };
-    static_assert(kFusedMaxDeg <= 8, "two entries per lane");
-    auto loadItem = [&](int t) {
-        GroupItem g;
-        if (t < aN) {
-            g.n = vprev[aLo + t];                        // A: live after k-1 (row with the entry)
-            g.row = vrprev[aLo + t];
-        } else {
-            g.n = p.gNode[cLo + t - aN];                 // B (claimed above)
-            g.row = make_int2(p.rowptr[g.n], p.rowptr[g.n + 1]);
-        }
-        const bool cn = convPrev(g.n);
-        g.upd = 0;
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int e = g.row.x + lane4 + 4 * j;
-            g.ent[j] = 0;
-            g.o[j] = -1;
-            if (e < g.row.y) {
-                g.ent[j] = p.csr[e];
-                g.o[j] = p.csrOther[e];
-                if (!(cn && convPrev(g.o[j]))) g.upd |= 1u << j;
-            }
-        }
-        return g;
-    };
-    GroupItem first;
-    if (g0 < nItems) first = loadItem(g0);
-    probeMark(p, k, PR_L_SCAN);
-    int work = 0;                                        // conduits produced (measurement)
-    // ---- phase 1: produce this workgroup's nodes' conduits -----------------
-    for (int t = g0; t < nItems; t += kBlock / 4) {
-        const GroupItem g = (t == g0) ? first : loadItem(t);
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int o = g.o[j], n = g.n;
-            if (!((g.upd >> j) & 1u) || !(n < o)) continue;   // bypassed, or the other end produces it
-            const int ent = g.ent[j];
-            const int l = ent & 0x7FFFFFFF;
-            const int2 nn = (ent < 0) ? make_int2(o, n) : make_int2(n, o);
-            const uint32_t f = p.lflags[l];
-            const int f1 = p.frz[nn.x], f2 = p.frz[nn.y];
-            const double y1 = frozenDepthV(p.nNewDepth[nn.x], p.yRaw[nn.x], f1, k - 1);
-            const double y2 = frozenDepthV(p.nNewDepth[nn.y], p.yRaw[nn.y], f2, k - 1);
-            conduitFlow<false, false, kFast>(p, l, f, nn, k, dt, ct, y1, y2);
-            // publish what the other end's gather reads: through the L2
-            // (agent scope), drained, then the stamp
-            const double qv = p.lNewFlow[l], s1 = p.sa1[l], s2 = p.sa2[l], dqv = p.dqdh[l];
-            __hip_atomic_store(&p.lNewFlow[l], qv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&p.sa1[l], s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&p.sa2[l], s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&p.dqdh[l], dqv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (f & LF_SEEP) {
-                const double ev = p.evapLoss[l], se = p.seepLoss[l];
-                __hip_atomic_store(&p.evapLoss[l], ev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&p.seepLoss[l], se, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(&p.lstamp[l], stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            work++;
-        }
-    }
-    probeMark(p, k, PR_L_WORK);
-    probeMark(p, k, PR_N_IN);
-    probeMark(p, k, PR_N_LAST_IN);
-    // ---- phase 2: one thread per node: wait for its updated conduits, update
-    // (the values are read at agent scope: the producers' stores went
-    // through to memory before their stamps)
-    __syncthreads();
-    bool anyUnconv = false;
-    int gathered = 0, live = 0, fast = 0;
-    for (int t0 = 0; t0 < nItems; t0 += kBlock) {
-        const int t = t0 + (int)threadIdx.x;
-        bool listMe = false, alive = false, me = t < nItems;
-        int n = 0;
-        int2 rowOut = make_int2(0, 0);
-        if (me) {
-            int2 row;
-            if (t < aN) {
-                n = vprev[aLo + t];
-                row = vrprev[aLo + t];
-            } else {
-                n = p.gNode[cLo + t - aN];
-                row = make_int2(p.rowptr[n], p.rowptr[n + 1]);
-            }
-            const bool cn = convPrev(n);
-            int lk[kFusedMaxDeg];
-            unsigned need = 0;
-#pragma unroll
-            for (int j = 0; j < kFusedMaxDeg; j++) {
-                lk[j] = 0;
-                if (row.x + j < row.y) {
-                    const int e = row.x + j;
-                    lk[j] = p.csr[e] & 0x7FFFFFFF;
-                    if (!(cn && convPrev(p.csrOther[e]))) need |= 1u << j;
-                }
-            }
-            // every stamp load in flight at once, then only the missing ones
-            unsigned ready = 0;
-            for (unsigned spins = 0; ready != need;) {
-#pragma unroll
-                for (int j = 0; j < kFusedMaxDeg; j++)
-                    if (((need & ~ready) >> j) & 1u)
-                        if (__hip_atomic_load(&p.lstamp[lk[j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == stamp)
-                            ready |= 1u << j;
-                if (ready == need) break;
-                for (int z = 0; z < p.pollSleep; z++) __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1u << 21)) {                  // ~seconds: never expected
-                    __hip_atomic_store(&p.ctl->tailErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                if ((spins & 1023) == 0 &&
-                    __hip_atomic_load(&p.ctl->tailErr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                    break;
-            }
-            // (ordering: the producers' stores went through the L2 and were
-            // drained before their stamps, and the values are read at agent
-            // scope below; this compiler barrier keeps those reads after the
-            // stamps were seen.  The graph relies on gfx9's in-order
-            // write-through of agent-scope stores, not on a release/acquire
-            // pair, whose L2 writeback measured too slow: it stays opt-in,
-            // DESIGN §4)
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            NodePre pre = loadNodePre(p, n, k);
-            if (need) pre.cache = 1;                     // an incident conduit was updated (the walk's mark)
-            nodeItem<false, kGeneral, true>(p, k, n, dt, pre, listMe, rowOut, anyUnconv, gathered, live, fast, alive,
-                                            row);
-        }
-        sinkAppend(su, me && listMe, n, rowOut);
-        sinkAppend(sv, me && alive, n, rowOut);
-    }
-    sinkFlush(su, &sBase);
-    sinkFlush(sv, &sBase);
-    nodePassEnd(p, k, anyUnconv, gathered, live, fast, true);
-    probeMark(p, k, PR_N_OUT);
-    probeMark(p, k, PR_L_OUT);
-    if (p.countWork) {                                   // measurement only
-        for (int off = 32; off > 0; off >>= 1) work += __shfl_down(work, off, 64);
-        if ((threadIdx.x & 63) == 0 && work) atomicAdd(&p.work[k], (unsigned long long)work);
-    }
-}
-
 // After k_sparse: the frozen junctions take their depth at the step's last
 // iteration (what finalizeFrozen and the last k_node(k) do in the unrolled
 // graph), from the iteration count the convergence flags give
 __global__ __launch_bounds__(kBlock) void k_unfreeze(Params p)
 {
-    if (p.cCnt && blockIdx.x == 0 && threadIdx.x == 0) {     // a compact step: the next one's gather counters
-        p.cCnt[1] = 0;
-        p.cCnt[3] = 0;
-    }
     if (!p.freeze) return;
     bool converged;
     const int m = stepIterations(p, &converged) - 1;
@@ -4864,26 +3948,9 @@ struct Router::Impl {
     bool listOk = false;
     double sparseMax = 6000.0;
     double liveAvg = 0.0;            // moving average of the live-list length after iteration 1
-    long long modeSteps[6] = {0, 0, 0, 0, 0, 0};   // steps launched per graph (unrolled, k_tail, sparse, list, fused, compact)
+    long long modeSteps[4] = {0, 0, 0, 0};   // steps launched per graph (unrolled, k_tail, sparse, list)
     hipGraphExec_t graphList = nullptr;   // iterations k >= 2 as list-driven k_walk / k_node_list pairs
-    // iterations k >= 2 as one k_fused launch each (fusedGrid > 0 only:
-    // built for SWMM5_SPARSE = 4 (then always used) or SWMM5_FUSED = 1 / 2
-    // (2: in the list graph's place in the auto choice))
-    hipGraphExec_t graphFused = nullptr;
-    int fusedGrid = 0;
-    bool fusedAuto = false;
-    unsigned* convW = nullptr;       // Params::convW while a fused step is launched
     double listMax = 200000.0;       // auto: the list graph while the live lists average at most this
-    // iterations k >= 2 over the compact copies of the live sub-network
-    // (k_cgather1/2, then k_cwalk / k_cnode per iteration): compactOk when the
-    // network qualifies and it was asked for (SWMM5_SPARSE = 5: always;
-    // SWMM5_COMPACT = 1: in the auto choice, in the list graph's place)
-    hipGraphExec_t graphCompact = nullptr;
-    bool compactOk = false, compactAuto = true;
-    CView cv{};
-    unsigned* cmStamp = nullptr;
-    int* cmCid = nullptr;
-    int gridCWalk = 1, gridCNode = 1, gridCGather = 1, gridCGather2 = 1;
     bool useGraph = true;
     bool timing = false;
     int gridL = 1, gridN = 1, gridEnd = 1, gridC = 1;
@@ -4964,8 +4031,6 @@ Router::~Router()
         if (d_->graphTail) (void)hipGraphExecDestroy(d_->graphTail);
         if (d_->graphSparse) (void)hipGraphExecDestroy(d_->graphSparse);
         if (d_->graphList) (void)hipGraphExecDestroy(d_->graphList);
-        if (d_->graphFused) (void)hipGraphExecDestroy(d_->graphFused);
-        if (d_->graphCompact) (void)hipGraphExecDestroy(d_->graphCompact);
         for (auto& t : d_->tslots) {
             for (auto e : t.ev) (void)hipEventDestroy(e);
             for (auto e : t.evHot) (void)hipEventDestroy(e);
@@ -5364,54 +4429,29 @@ static TailFn sparseKernel(bool fast, bool general)
 // k_link / k_node pair (later ones exit at once after convergence); GM_TAIL:
 // iterations k >= 2 in one k_tail launch (d->tailGrid > 0 only); GM_SPARSE:
 // iterations k >= 2 in k_sparse (one workgroup), then k_unfreeze
-// (d->sparseOk only)
-// GM_FUSED: iterations k >= 2 as one k_fused launch each, then k_unfreeze
-// (d->fusedGrid > 0 only)
-// GM_COMPACT: k_cgather, then iterations k >= 2 as k_cwalk / k_cnode pairs
-// over the compact copies, then k_unfreeze (d->compactOk only)
-enum { GM_UNROLLED = 0, GM_TAIL = 1, GM_SPARSE = 2, GM_LIST = 3, GM_FUSED = 4, GM_COMPACT = 5 };
-typedef void (*FusedFn)(Params, int);
-static FusedFn fusedKernel(bool fast, bool general)
-{
-    if (fast) return general ? k_fused<true, true> : k_fused<true, false>;
-    return general ? k_fused<false, true> : k_fused<false, false>;
-}
+// (d->sparseOk only); GM_LIST: iterations k >= 2 as list-driven k_walk /
+// k_node_list pairs, then k_unfreeze (d->listOk only).  (The round-4 fused
+// and round-5 compact graphs were measured slower than the list graph and
+// removed in round 6: DESIGN section 4.)
+enum { GM_UNROLLED = 0, GM_TAIL = 1, GM_SPARSE = 2, GM_LIST = 3 };
 static int launchStepImpl(Router::Impl* d, int mode);
 static int launchStep(Router::Impl* d, int mode = GM_UNROLLED)
 {
-    // the fused graph's launches write the convergence words and run the
-    // outfall prologue in k_fused (never deferred); the others do neither
     // (each captured graph keeps its own copy of the arguments)
     Params& p = d->p;
-    const int defer = p.deferPro;
-    p.convW = (mode == GM_FUSED) ? d->convW : nullptr;
-    if (mode == GM_FUSED || mode == GM_COMPACT) p.deferPro = 0;
-    // the compact graph: k_node(1) stamps the live nodes' membership, and the
-    // outfall prologue of iterations k >= 2 writes the compact copies too
-    const bool compact = mode == GM_COMPACT;
-    p.cmStamp = compact ? d->cmStamp : nullptr;
-    p.cmCid = compact ? d->cmCid : nullptr;
-    p.cOutDepth = compact ? d->cv.nNewDepth : nullptr;
-    p.cCnt = compact ? d->cv.cnt : nullptr;
-    // the list and fused graphs with a separate quality launch: k_qual_node
-    // gives the frozen junctions their final depth (each node's own thread,
-    // before its quality reads the depth), one full-grid k_unfreeze less
-    p.qualUnfreeze = ((mode == GM_LIST || mode == GM_FUSED) && p.P > 0 && !d->fuseQual && p.freeze) ? 1 : 0;
+    // the list graph with a separate quality launch: k_qual_node gives the
+    // frozen junctions their final depth (each node's own thread, before its
+    // quality reads the depth), one full-grid k_unfreeze less
+    p.qualUnfreeze = (mode == GM_LIST && p.P > 0 && !d->fuseQual && p.freeze) ? 1 : 0;
     const int r = launchStepImpl(d, mode);
     p.qualUnfreeze = 0;
-    p.convW = nullptr;
-    p.cmStamp = nullptr;
-    p.cmCid = nullptr;
-    p.cOutDepth = nullptr;
-    p.cCnt = nullptr;
-    p.deferPro = defer;
     return r;
 }
 static int launchStepImpl(Router::Impl* d, int mode)
 {
     Params& p = d->p;
     // k_node(1) lists the live nodes only for the list-driven graphs
-    p.buildVlist = (mode == GM_SPARSE || mode == GM_LIST || mode == GM_FUSED || mode == GM_COMPACT) ? 1 : 0;
+    p.buildVlist = (mode == GM_SPARSE || mode == GM_LIST) ? 1 : 0;
     const bool multi = d->part.active();
     if (p.skipSteady) {                            // SKIP_STEADY_STATE: this step's inflow test
         hipLaunchKernelGGL(k_steady, dim3(d->gridN), dim3(kBlock), 0, d->stream, p);
@@ -5465,27 +4505,6 @@ static int launchStepImpl(Router::Impl* d, int mode)
         }
         if (!p.qualUnfreeze)
             launchTimed(d, k_unfreeze, dim3(d->gridN), (hipEvent_t) nullptr, (hipEvent_t) nullptr, p);
-    } else if (mode == GM_FUSED) {
-        for (int k = 0; k < 2; k++)
-            if (int r = launchIteration(d, k)) return r;
-        for (int k = 2; k < p.maxTrials; k++)
-            launchTimed(d, fusedKernel(d->fastLinks, d->general), dim3(d->fusedGrid), ev ? ev[4 * k] : nullptr,
-                        d->timing ? d->curHot[k] : nullptr, p, k);
-        if (!p.qualUnfreeze)
-            launchTimed(d, k_unfreeze, dim3(d->gridN), (hipEvent_t) nullptr, (hipEvent_t) nullptr, p);
-    } else if (mode == GM_COMPACT) {
-        for (int k = 0; k < 2; k++)
-            if (int r = launchIteration(d, k)) return r;
-        // (timing: the gather is counted with iteration 2's walk)
-        launchTimed(d, k_cgather1, dim3(d->gridCGather), ev ? ev[8] : nullptr, (hipEvent_t) nullptr, p, d->cv);
-        launchTimed(d, k_cgather2, dim3(d->gridCGather2), (hipEvent_t) nullptr, (hipEvent_t) nullptr, p, d->cv);
-        for (int k = 2; k < p.maxTrials; k++) {
-            launchTimed(d, d->fastLinks ? k_cwalk<true> : k_cwalk<false>, dim3(d->gridCWalk),
-                        (ev && k > 2) ? ev[4 * k] : nullptr, d->timing ? d->curHot[k] : nullptr, p, d->cv, k);
-            launchTimed(d, k_cnode, dim3(d->gridCNode), ev ? ev[4 * k + 1] : nullptr, ev ? ev[4 * k + 2] : nullptr,
-                        p, d->cv, k);
-        }
-        launchTimed(d, k_unfreeze, dim3(d->gridN), (hipEvent_t) nullptr, (hipEvent_t) nullptr, p);
     } else {
         for (int k = 0; k < p.maxTrials; k++)
             if (int r = launchIteration(d, k)) return r;
@@ -6033,16 +5052,6 @@ int Router::init(Project& prj, int device, const Partition* partIn)
             if (isDef[i]) { defNodes.push_back(i); nflags[i] = (int)((uint32_t)nflags[i] | NF_DEFER); }
     }
     d->nE = (int)csr.size();
-    // k_fused's conditions on the rows: degree (its LDS slot) and no conduit
-    // joining a node to itself (its producer is the lower-numbered end)
-    int maxRowDeg = 0;
-    for (int i = 0; i < nN; i++) {
-        maxRowDeg = std::max(maxRowDeg, rowptr[i + 1] - rowptr[i]);
-        for (int e = rowptr[i]; e < rowptr[i + 1]; e++) {
-            const int l = csr[e] & 0x7FFFFFFF;
-            if (l < (int)nodes2.size() / 2 && nodes2[2 * l] == nodes2[2 * l + 1]) maxRowDeg = 1 << 30;
-        }
-    }
     {
         int* fl;
         UPI(fl, nflags, nN);
@@ -6207,9 +5216,6 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (e == hipSuccess) e = hipMemset(p.wmark, 0, std::max<size_t>(nN, 1) * sizeof(int));
         if (e == hipSuccess) p.nstamp = devAlloc<unsigned>(d, (size_t)nN, &e);
         if (e == hipSuccess) e = hipMemset(p.nstamp, 0xFF, std::max<size_t>(nN, 1) * sizeof(unsigned));
-        if (e == hipSuccess) p.lstamp = devAlloc<unsigned>(d, (size_t)nL, &e);
-        if (e == hipSuccess) e = hipMemset(p.lstamp, 0xFF, std::max<size_t>(nL, 1) * sizeof(unsigned));
-        if (e == hipSuccess) p.gNode = devAlloc<int>(d, 5 * (size_t)nN, &e);
         if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
         p.dirty = devAlloc<unsigned char>(d, nN, &e);
         if (e == hipSuccess) e = hipMemset(p.dirty, 0, std::max<size_t>(nN, 1));
@@ -6659,8 +5665,6 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         const char* dp = getenv("SWMM5_DEFER_OUTFALL");
         const char* es = getenv("SWMM5_STEPEND_SKIP");
         p.endSkip = es ? atoi(es) : 0;
-        const char* ps = getenv("SWMM5_POLL_SLEEP");
-        p.pollSleep = ps ? std::max(0, atoi(ps)) : 2;
         p.deferPro = (outfallsDeferrable && dp && atoi(dp) != 0 && !part.active() && !d->comm && p.nNC == 0 &&
                       p.maxTrials > 2) ? 1 : 0;
     }
@@ -6736,140 +5740,6 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         }
         HIPCHECK(hipStreamEndCapture(d->stream, &g));
         HIPCHECK(hipGraphInstantiate(&d->graphList, g, nullptr, nullptr, 0));
-        (void)hipGraphDestroy(g);
-    }
-    // the k_fused variant: the list graph's conditions, plus freezing on (its
-    // node set is the list graph's), no cold conduits (their side-stream
-    // loop), every row at most kFusedMaxDeg entries (one LDS slot per node),
-    // the outfall conduits as deferPro needs them (each its outfall's only
-    // link: block 0 computes the depths once they are published, and no other
-    // conduit reads them) -- and a resident grid (its waits need every
-    // workgroup running: checked against the occupancy)
-    {
-        // built only when asked for (SWMM5_SPARSE=4, or SWMM5_FUSED=1 / 2):
-        // measured slower than the list graph (DESIGN §4 "Round 4")
-        const char* fm = getenv("SWMM5_FUSED");
-        const bool asked = d->sparseMode == 4 || (fm && atoi(fm) != 0);
-        bool ok = d->sparseOk && asked && p.freeze && p.nCold == 0 && outfallsDeferrable &&
-                  maxRowDeg <= kFusedMaxDeg;
-        int occ = 0, cus = 0;
-        if (ok && (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-                   hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                       &occ, (const void*)fusedKernel(d->fastLinks, d->general), kBlock, 0) != hipSuccess))
-            ok = false;
-        (void)hipGetLastError();
-        // two workgroups per CU (SWMM5_FUSED_GRID: per CU; measured on the
-        // surcharged 1M grid: 1 -> 55.2, 2 -> 54.4, 4 -> 59.4 us per iteration)
-        double f = 2.0;
-        if (const char* g = getenv("SWMM5_FUSED_GRID")) f = atof(g);
-        const int want = std::max(2, (int)(f * std::max(cus, 1)));
-        d->fusedGrid = (ok && occ >= 1 && cus > 0) ? std::min(want, occ * cus) : 0;
-        d->fusedAuto = fm && atoi(fm) == 2;
-        if (d->fusedGrid > 0) {
-            std::vector<unsigned> w(nN, 0u);
-            for (int i = 0; i < nN; i++)
-                if ((nflags[i] & NF_TYPE) == OUTFALL) w[i] = kConvOutfall;
-            d->convW = devAlloc<unsigned>(d, (size_t)nN, &e);
-            if (e == hipSuccess)
-                e = hipMemcpy(d->convW, w.data(), std::max<size_t>(nN, 1) * sizeof(unsigned), hipMemcpyHostToDevice);
-            if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
-        }
-    }
-    if (d->fusedGrid > 0) {
-        HIPCHECK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
-        if (launchStep(d, GM_FUSED)) {
-            (void)hipStreamEndCapture(d->stream, &g);
-            fail(d->xerrMsg);
-            return err_;
-        }
-        HIPCHECK(hipStreamEndCapture(d->stream, &g));
-        HIPCHECK(hipGraphInstantiate(&d->graphFused, g, nullptr, nullptr, 0));
-        (void)hipGraphDestroy(g);
-    }
-    // the compact graph: the list graph's conditions, plus freezing on (L1 is
-    // the nodes not frozen after iteration 1), no cold conduits, no storage
-    // units (the compact node update is nodeItem<.., kGeneral = false>), rows
-    // of at most kCompactMaxDeg entries (the slots) and no conduit from a node
-    // to itself (maxRowDeg is huge then)
-    {
-        // built on request only (SWMM5_SPARSE=5, or SWMM5_COMPACT=1 for the
-        // auto choice): measured slower than the list graph on the surcharged
-        // 1M grid (0.538 against 0.448 ms/step; DESIGN §4 "Round 5")
-        const char* cm = getenv("SWMM5_COMPACT");
-        d->compactAuto = cm && atoi(cm) != 0;
-        const bool asked = d->sparseMode == 5 || d->compactAuto;
-        d->compactOk = asked && d->sparseOk && p.freeze && p.nCold == 0 && !d->general && maxRowDeg >= 1 &&
-                       maxRowDeg <= kCompactMaxDeg;
-    }
-    if (d->compactOk) {
-        CView& v = d->cv;
-        const size_t capN = std::max<size_t>(nN, 1), capL = (size_t)nL + 1;
-        bool losses = false, qlim = false, seep = false;
-        for (int j = 0; j < nOwn; j++) {
-            const uint32_t f = (uint32_t)lflags[j];
-            losses = losses || (f & LF_LOSSES);
-            qlim = qlim || (f & LF_QLIMIT);
-            seep = seep || (f & LF_SEEP);
-        }
-        v.seep = seep ? 1 : 0;
-        hipError_t ea = hipSuccess;
-        auto aD = [&](double*& ptr, size_t n) { if (ea == hipSuccess) ptr = devAlloc<double>(d, n, &ea); };
-        auto aI = [&](int*& ptr, size_t n) { if (ea == hipSuccess) ptr = devAlloc<int>(d, n, &ea); };
-        auto aU = [&](uint32_t*& ptr, size_t n) { if (ea == hipSuccess) ptr = devAlloc<uint32_t>(d, n, &ea); };
-        auto aB = [&](unsigned char*& ptr, size_t n) { if (ea == hipSuccess) ptr = devAlloc<unsigned char>(d, n, &ea); };
-        aI(v.cnt, 4);
-        aU(v.lStamp, std::max<size_t>(nL, 1));
-        aI(v.lCid, std::max<size_t>(nL, 1));
-        aU(d->cmStamp, capN);
-        aI(d->cmCid, capN);
-        aI(v.node, capN);
-        aI(v.deg, capN);
-        aI(v.csr, (size_t)kCompactMaxDeg * capN);
-        aI(v.link, capL);
-        if (ea == hipSuccess) v.ends = devAlloc<int2>(d, capL, &ea);
-        aU(v.nflags, capN);
-        aB(v.dirty, capN);
-        aB(v.frz, capN);
-        aI(v.conv, capN);
-        for (double** a : {&v.nNewDepth, &v.yRaw, &v.yCrown, &v.yMaxNP, &v.nOldDepth, &v.newLat, &v.inflow, &v.outflow,
-                           &v.nSurf, &v.nDqdh, &v.fullDepth, &v.pondedArea, &v.oldNetInflow, &v.surDepth,
-                           &v.oldSurfArea, &v.fullVolume, &v.nOldVolume, &v.nNewVolume, &v.overflow})
-            aD(*a, capN);
-        aU(v.lflags, capL);
-        aI(v.lstate, capL);
-        for (double** a : {&v.lNewFlow, &v.lOldFlow, &v.q1, &v.setting, &v.inv1, &v.inv2, &v.a2, &v.modLength,
-                           &v.length, &v.roughFactor, &v.beta, &v.sa1, &v.sa2, &v.dqdh, &v.a1, &v.froude,
-                           &v.lNewDepth, &v.lNewVolume, &v.evapLoss, &v.seepLoss})
-            aD(*a, capL);
-        if (losses) for (double** a : {&v.cIn, &v.cOut, &v.cAvg}) aD(*a, capL);
-        if (qlim) aD(v.qLimit, capL);
-        if (seep) for (double** a : {&v.seepRate, &v.lOldDepth}) aD(*a, capL);
-        if (!d->fastLinks)
-            for (double** a : {&v.yFull, &v.wMax, &v.ywMax, &v.aFull, &v.rFull, &v.sFull, &v.sMax, &v.yBot, &v.aBot,
-                               &v.sBot, &v.rBot})
-                aD(*a, capL);
-        if (ea == hipSuccess) ea = hipMemset(v.cnt, 0, 4 * sizeof(int));
-        if (ea == hipSuccess) ea = hipMemset(v.lStamp, 0, std::max<size_t>(nL, 1) * sizeof(unsigned));
-        if (ea == hipSuccess) ea = hipMemset(d->cmStamp, 0, capN * sizeof(unsigned));
-        if (ea != hipSuccess) { fail(std::string("compact graph: ") + hipGetErrorString(ea)); return err_; }
-        // the walk: two workgroups per CU (one thread per compact conduit);
-        // the node pass and the gathers: two per CU (one thread per node, the
-        // first gather four per unconverged node too)
-        const int cus = std::max(prop.multiProcessorCount, 1);
-        d->gridCWalk = 2 * cus;
-        d->gridCNode = 2 * cus;
-        d->gridCGather = 4 * cus;
-        d->gridCGather2 = 2 * cus;
-        if (const char* gw = getenv("SWMM5_CWALK_GRID")) d->gridCWalk = std::max(1, (int)(atof(gw) * cus));
-        if (const char* gn2 = getenv("SWMM5_CNODE_GRID")) d->gridCNode = std::max(2, (int)(atof(gn2) * cus));
-        HIPCHECK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
-        if (launchStep(d, GM_COMPACT)) {
-            (void)hipStreamEndCapture(d->stream, &g);
-            fail(d->xerrMsg);
-            return err_;
-        }
-        HIPCHECK(hipStreamEndCapture(d->stream, &g));
-        HIPCHECK(hipGraphInstantiate(&d->graphCompact, g, nullptr, nullptr, 0));
         (void)hipGraphDestroy(g);
     }
     WAITCHECK(waitDone(d_, nullptr));
@@ -6985,8 +5855,7 @@ static void flushTiming(Router::Impl* d)
                 continue;
             }
             (void)hipEventElapsedTime(&ms1, t.ev[4 * k], t.evHot[k]);
-            if (!(t.mode == GM_FUSED && k >= 2))   // (k_fused: one launch, timed as the link class)
-                (void)hipEventElapsedTime(&ms2, t.ev[4 * k + 1], t.ev[4 * k + 2]);
+            (void)hipEventElapsedTime(&ms2, t.ev[4 * k + 1], t.ev[4 * k + 2]);
             {
                 const int M = p.maxTrials;
                 double* it = d->iterStats.data() + (size_t)Router::Impl::kIterCols * k;
@@ -7068,14 +5937,9 @@ static int chooseGraph(Router::Impl* d)
     if (d->part.active()) return d->listOk ? GM_LIST : GM_UNROLLED;
     if (d->sparseOk && d->sparseMode == 1) return GM_SPARSE;
     if (d->listOk && d->sparseMode == 3) return GM_LIST;
-    if (d->fusedGrid > 0 && d->sparseMode == 4) return GM_FUSED;
-    if (d->compactOk && d->sparseMode == 5) return GM_COMPACT;
     if (d->tailGrid > 0 && (d->tailMode == 1 || fresh || d->itersAvg <= kTailIters)) return GM_TAIL;
     if (d->sparseOk && !fresh && d->liveAvg <= d->sparseMax) return GM_SPARSE;
-    if (d->listOk && !fresh && d->liveAvg <= d->listMax) {
-        if (d->compactOk && d->compactAuto) return GM_COMPACT;
-        return (d->fusedGrid > 0 && d->fusedAuto) ? GM_FUSED : GM_LIST;
-    }
+    if (d->listOk && !fresh && d->liveAvg <= d->listMax) return GM_LIST;
     return GM_UNROLLED;
 }
 
@@ -7090,7 +5954,6 @@ static bool tailFailed(Router::Impl* d)
 {
     if (d->hostDt[2 * Router::Impl::kRing] == 0.0) return false;
     d->tailGrid = 0;
-    d->fusedGrid = 0;
     return true;
 }
 
@@ -7178,8 +6041,6 @@ int Router::step(const double* latFlow, const double* qualLoad, const double tot
         d->modeSteps[mode]++;
         HIPCHECK(hipGraphLaunch(mode == GM_SPARSE    ? d->graphSparse
                                 : mode == GM_LIST    ? d->graphList
-                                : mode == GM_FUSED   ? d->graphFused
-                                : mode == GM_COMPACT ? d->graphCompact
                                 : mode == GM_TAIL    ? d->graphTail
                                                      : d->graph,
                                 d->stream));
@@ -7591,8 +6452,7 @@ void Router::setTiming(bool on)
         d_->probeSum.clear();
     }
     if (on && getenv("SWMM5_PROBE") && !d_->p.probe) {
-        const int B = std::max(std::max(std::max(std::max(d_->gridL, d_->gridN), d_->gridLinkSparse), d_->gridNList),
-                               d_->fusedGrid);
+        const int B = std::max(std::max(std::max(d_->gridL, d_->gridN), d_->gridLinkSparse), d_->gridNList);
         const size_t n = (size_t)std::max(d_->p.maxTrials, 1) * kProbeSlots * B;
         if (hipMalloc((void**)&d_->p.probe, n * sizeof(unsigned long long)) == hipSuccess &&
             hipMemset(d_->p.probe, 0, n * sizeof(unsigned long long)) == hipSuccess)
@@ -7969,14 +6829,9 @@ void Router::graphStats(long long out[9])
     out[0] = d_->itersTimed1;
     for (int m = 0; m < 4; m++) out[1 + m] = d_->modeSteps[m];
     out[5] = d_->p.deferPro;
-    out[6] = d_->modeSteps[GM_FUSED];
-    out[7] = d_->modeSteps[GM_COMPACT];
-    // nodes the compact walks added to the compact sets (growth; a diagnostic:
-    // synchronous read)
-    int c[4] = {0, 0, 0, 0};
-    if (d_->cv.cnt && hipStreamSynchronize(d_->stream) == hipSuccess)
-        (void)hipMemcpy(c, d_->cv.cnt, sizeof(c), hipMemcpyDeviceToHost);
-    out[8] = c[2];
+    out[6] = 0;                                    // retired counters (fused / compact graphs)
+    out[7] = 0;
+    out[8] = 0;
 }
 
 int Router::kernelTimes(double* out, int n)

@@ -247,12 +247,9 @@ def test_frozen_junctions_bitwise(tmp_path, monkeypatch):
     junctions' final depths in k_unfreeze), and for the list graph (the same
     list-driven phases as k_walk / k_node_list launches per iteration), each
     with the outfall depths of iterations 2 .. MaxTrials-2 found in the next
-    walk launch (deferred outfall prologue) and without, for the fused
-    graph (one k_fused launch per iteration k >= 2: conduits published by
-    their producers, node updates waiting on them, no grid barrier), and for
-    the compact graph (iterations k >= 2 over compact copies of the live
-    sub-network, written through to the global arrays; nodes woken outside
-    it join it)."""
+    walk launch (deferred outfall prologue) and without.  (The fused and
+    compact graphs of rounds 4-5 were measured slower than the list graph
+    and removed: DESIGN section 4.)"""
     q, D = 0.3, 1.0
     inp = str(tmp_path / "g.inp")
     netgen.write_grid(inp, 60, 60, end_time="02:00:00", route_step=5.0, variable_step=0.75,
@@ -261,8 +258,7 @@ def test_frozen_junctions_bitwise(tmp_path, monkeypatch):
     for off, tail, sparse, defer in (("1", "0", "0", "0"), ("1", "0", "0", "1"), ("0", "0", "0", "0"),
                                      ("0", "0", "0", "1"), ("0", "1", "0", "1"), ("1", "1", "0", "1"),
                                      ("0", "0", "1", "1"), ("1", "0", "1", "1"), ("0", "0", "3", "1"),
-                                     ("1", "0", "3", "1"), ("0", "0", "3", "0"), ("0", "0", "4", "1"),
-                                     ("1", "0", "4", "0"), ("0", "0", "5", "0"), ("0", "0", "5", "1")):
+                                     ("1", "0", "3", "1"), ("0", "0", "3", "0")):
         monkeypatch.setenv("SWMM5_NO_FREEZE", off)
         monkeypatch.setenv("SWMM5_DEFER_OUTFALL", defer)
         monkeypatch.setenv("SWMM5_TAIL", tail)
@@ -279,11 +275,6 @@ def test_frozen_junctions_bitwise(tmp_path, monkeypatch):
             assert c["steps_sparse"] == c["steps"], c
         if sparse == "3":                         # every step ran the list graph
             assert c["steps_list"] == c["steps"], c
-        if sparse == "4" and off == "0":          # every step ran the fused graph
-            assert c["steps_fused"] == c["steps"], c
-        if sparse == "5":                         # every step ran the compact graph
-            assert c["steps_compact"] == c["steps"] and c["deferred_outfalls"] == int(defer), c
-            print("compact graph counters:", c)
         runs.append((snaps, c))
         s.end()
         s.close()
@@ -458,14 +449,13 @@ def test_sparse_tail_bitwise_1m(tmp_path, monkeypatch):
     and link field and every counter is bitwise equal, and the sparse run
     really ran its iterations >= 2 in k_sparse; the same for the list graph,
     and for the unrolled and list graphs without the deferred outfall
-    prologue, for the fused graph (one k_fused launch per iteration), and
-    for the compact graph."""
+    prologue."""
     import bench
     cfg = bench.PRESETS["1m_light"]
     inp = bench.make_inp(cfg["grid"], cfg["route_step"], cfg["variable_step"], cfg["pollutants"],
                          cfg["diameter"], cfg["q"])
     runs = []
-    for sparse, defer in (("0", "1"), ("1", "1"), ("3", "1"), ("0", "0"), ("3", "0"), ("4", "0"), ("5", "0")):
+    for sparse, defer in (("0", "1"), ("1", "1"), ("3", "1"), ("0", "0"), ("3", "0")):
         monkeypatch.setenv("SWMM5_TAIL", "0")
         monkeypatch.setenv("SWMM5_SPARSE", sparse)
         monkeypatch.setenv("SWMM5_DEFER_OUTFALL", defer)
@@ -483,8 +473,6 @@ def test_sparse_tail_bitwise_1m(tmp_path, monkeypatch):
         assert runs[0][1]["nonconverged"] == r[1]["nonconverged"]
     c0, c1, c3 = runs[0][1], runs[1][1], runs[2][1]
     assert c1["steps_sparse"] == c1["steps"] and c0["steps_sparse"] == 0 and c3["steps_list"] == c3["steps"]
-    assert runs[5][1]["steps_fused"] == runs[5][1]["steps"], runs[5][1]
-    assert runs[6][1]["steps_compact"] == runs[6][1]["steps"], runs[6][1]
     assert c0["iterations"] > 2 * c0["steps"] + 100, c0          # iterations >= 2 ran
 
 

@@ -462,6 +462,32 @@ def test_ranks_list_graph_bitwise(world, block, pollutants, transport, tmp_path)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["host", "ipc"])
+def test_eight_ranks_bitwise_benchmark_regime(transport, tmp_path):
+    """Eight ranks (the driver's node size) on this box's one GPU, in the
+    benchmark's regime: a surcharged, non-converging 100 x 100 grid (SURVEY
+    section 6's q = 0.1 row) in eight row strips, every step on the list graph,
+    shared nodes freezing.  The surcharged region spans several strips, so
+    iterations k >= 2 have live lists on several ranks; every owned node and
+    link field is bitwise the one-GPU run's, with equal iteration and
+    non-convergence counts."""
+    inp = _grid(tmp_path, 100, 100, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.1, end_time="00:40:00")
+    env = {"SWMM5_SPARSE": "3"}
+    one = _run_workers(inp, 100000, tmp_path, 1, "host", "one", extra_env=env)[0]
+    st, its, nonconv = one["counters"]
+    assert nonconv > 10 and its / st > 2.5, one["counters"]
+    parts = _run_workers(inp, 100000, tmp_path, 8, transport, "eight", extra_env=env, timeout=900)
+    for part in parts:
+        assert part["graphs"][1] == part["counters"][0], (part["graphs"], part["counters"])
+        assert _transport_of(part) == transport
+    owner = parts[0]["node_owner"]
+    sur = one["node.newDepth"][:-1] > 1.0
+    ranks_surcharged = sorted(set(owner[:-1][sur].tolist()))
+    assert len(ranks_surcharged) >= 3, ranks_surcharged       # live sparse work on several ranks
+    _assert_bitwise(parts, one)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("sparse", ["0", "3"])
 def test_regulators_two_ranks_bitwise(sparse, tmp_path):
     """An orifice, a weir across the strip boundary and an outlet (k_nc) with

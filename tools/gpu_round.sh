@@ -35,6 +35,12 @@ for s in $STEPS; do
     tsparse) run tsparse 900 python -u -m pytest tests/test_gpu_vs_oracle.py -x -v -p no:cacheprovider --timeout 400 --timeout-method thread -k "${TK:-frozen or sparse or regime_window_707}" ;;
     tipc) run tipc 900 python -u -m pytest tests/test_multigpu.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu -k "${TKM:-ipc}" ;;
     ipc2) for x in ${XS:-ipc host}; do run ipc2_$x 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${NP:-2} --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) bench.py --gpus ${NP:-2} --config ${CFG:-1m_surcharge} --steps ${BSTEPS:-20} --warmup 5 --spinup ${SPIN:-200} --exchange $x --no-cpu --no-stream --kernel-reps 0; done ;;
+    rcclprobe) # the captured RCCL call pattern on one rank (tools/rccl_capture_probe.cpp), phase by phase,
+           # bootstrap on the loopback interface and, for comparison, on RCCL's own interface choice
+           for n in ${PREPS:-2 8 16}; do
+             NCCL_SOCKET_IFNAME=lo NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,BOOTSTRAP run rcclprobe_lo_$n 90 ./tools/rccl_capture_probe $n
+             NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,BOOTSTRAP run rcclprobe_auto_$n 90 ./tools/rccl_capture_probe $n
+           done ;;
     tmulti) run tmulti 900 python -u -m pytest tests/test_multigpu.py -x -v -p no:cacheprovider --timeout 600 --timeout-method thread -m gpu -k "${TKM:-write_one_gpu or rccl}" ;;
     rccl1) for c in ${RCFGS:-1m_surcharge 4m}; do run rccl1_$c 600 python bench.py --config $c --rccl-1rank --no-cpu --kernel-reps 0 --steps 100 && run plain1_$c 600 python bench.py --config $c --no-cpu --kernel-reps 0 --steps 100; done ;;
     tk) run tk 900 python -u -m pytest tests -x -v -p no:cacheprovider -m gpu --timeout 400 --timeout-method thread -k "${TK:-exfil}" ;;

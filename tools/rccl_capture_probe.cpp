@@ -7,9 +7,16 @@
 //   hipcc -O2 -o tools/rccl_capture_probe tools/rccl_capture_probe.cpp -lrccl
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+
+static double secs()
+{
+    static const auto t0 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
 
 #define CK(x)                                                                   \
     do {                                                                        \
@@ -33,10 +40,14 @@ int main(int argc, char** argv)
     setvbuf(stdout, nullptr, _IONBF, 0);
     const int kRep = argc > 1 ? atoi(argv[1]) : 16;
     const size_t n = 4 * 2828;                    // a 4M strip boundary: 2 x 1414 links x 4 doubles
+    const char* ifn = getenv("NCCL_SOCKET_IFNAME");
+    printf("[%.3f s] start: %d repetitions, NCCL_SOCKET_IFNAME=%s\n", secs(), kRep, ifn ? ifn : "(unset)");
     ncclUniqueId id;
     NK(ncclGetUniqueId(&id));
+    printf("[%.3f s] unique id (bootstrap root listening)\n", secs());
     ncclComm_t comm;
     NK(ncclCommInitRank(&comm, 1, id, 0));
+    printf("[%.3f s] communicator initialised\n", secs());
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     double *snd, *rcv;
@@ -54,7 +65,7 @@ int main(int argc, char** argv)
     NK(ncclAllReduce(flag, flag, 1, ncclInt32, ncclMax, comm, s));
     CK(hipStreamEndCapture(s, &g));
     CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-    printf("single pattern captured\n");
+    printf("[%.3f s] single pattern captured\n", secs());
     std::vector<double> h(n), back(n);
     int bad = 0;
     for (int rep = 0; rep < 50; rep++) {
@@ -72,7 +83,7 @@ int main(int argc, char** argv)
             if (back[i] != h[i]) { bad++; break; }
         if (fo != fv) bad++;
     }
-    printf("50 replays checked: %d mismatches\n", bad);
+    printf("[%.3f s] 50 replays checked: %d mismatches\n", secs(), bad);
     // timing: the pattern, and its two parts alone, each captured kRep times
     // in one graph (the cost inside a graph, as the step graph has it, not
     // that of a graph launch)
@@ -105,7 +116,7 @@ int main(int argc, char** argv)
         }
         CK(hipStreamEndCapture(s, &gr[v]));
         CK(hipGraphInstantiate(&gx[v], gr[v], nullptr, nullptr, 0));
-        printf("variant %d captured (%d repetitions)\n", v, kRep);
+        printf("[%.3f s] variant %d captured (%d repetitions)\n", secs(), v, kRep);
     }
     float tAll = 0.f, tX = 0.f, tF = 0.f;
     if (timeGraph(gx[2], &tF)) return 2;
