@@ -99,6 +99,44 @@ def make_inp(nx, route_step, variable_step, pollutants, diameter, q, rows=None):
     return path
 
 
+def spinup_for(cfg, world):
+    """the preset's spin-up for this rank count (weak scaling: the longer grid's
+    own spin-up, nearest tabulated rank count below)"""
+    spin = cfg["spinup"]
+    if world > 1 and cfg.get("spinup_by_n"):
+        keys = sorted(k for k in cfg["spinup_by_n"] if k <= world)
+        if keys:
+            spin = cfg["spinup_by_n"][keys[-1]]
+    return spin
+
+
+def workload_name(config, cfg, rows):
+    return "%s: manhattan_grid_%dx%d_DYNWAVE_%s_D%gft_q%gcfs_P%d" % (
+        config, rows, cfg["grid"],
+        "fixed%gs" % cfg["route_step"] if cfg["variable_step"] == 0 else
+        "variable%g_max%gs" % (cfg["variable_step"], cfg["route_step"]),
+        cfg["diameter"], cfg["q"], cfg["pollutants"])
+
+
+def partition_weights(workload, rows, nx, n_nodes):
+    """Per-node weights from profiles/partition_weights.json (tools/
+    calibrate_partition.py: the workload's per-row sparse node updates per
+    step measured on one GPU, and the marginal cost of a sparse update
+    relative to a full-pass node): node i of row r weighs 1 + lambda u_r / nx,
+    the outfall 1.  None when no record matches this grid."""
+    path = os.path.join(ROOT, "profiles", "partition_weights.json")
+    if not os.path.exists(path):
+        return None, None
+    rec = json.load(open(path)).get(workload)
+    if not rec or rec.get("rows") != rows or rec.get("nx") != nx or rec.get("nodes") != n_nodes:
+        return None, None
+    import numpy as np
+    w = np.ones(n_nodes)
+    ru = np.asarray(rec["row_updates"], dtype=np.float64)
+    w[:rows * nx] = 1.0 + rec["lambda"] * np.repeat(ru / nx, nx)
+    return w, rec
+
+
 def _record(name, workload, backend):
     """profiles/<name> entry for this workload, only when it was measured on
     the same build inputs (swmm5.kernel_source_sha: every engine source,
@@ -241,6 +279,9 @@ def main():
                          "flag all-reduce every Picard iteration): the in-graph cost of the collectives")
     ap.add_argument("--no-stream", dest="stream", action="store_false",
                     help="skip the STREAM-triad measurement of the achievable HBM bandwidth")
+    ap.add_argument("--balance", choices=["auto", "off"], default="auto",
+                    help="several ranks: weigh the partition by the workload's measured sparse work "
+                         "(profiles/partition_weights.json, tools/calibrate_partition.py) when a record exists")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per link-momentum launch from rocprofv3 PMC (profiles/)")
     args = ap.parse_args()
@@ -257,11 +298,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.spinup is None and world > 1 and cfg.get("spinup_by_n"):
+    if args.spinup is None:
         # the weak-scaling grid's own spin-up (nearest tabulated rank count below)
-        keys = sorted(k for k in cfg["spinup_by_n"] if k <= world)
-        if keys:
-            cfg["spinup"] = cfg["spinup_by_n"][keys[-1]]
+        cfg["spinup"] = spinup_for(cfg, world)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -292,6 +331,12 @@ def main():
         s.set_partition(rank, world, bytes(idt.numpy().tobytes()))
     elif args.rccl_1rank:
         s.set_partition(0, 1, s.nccl_unique_id())
+    balance = None
+    if world > 1 and args.balance == "auto":
+        n_nodes = rows * cfg["grid"] + 1
+        w, balance = partition_weights(workload_name(args.config, cfg, rows), rows, cfg["grid"], n_nodes)
+        if w is not None:
+            s.set_partition_weights(w)
     if world > 1 and args.exchange in ("host", "ipc"):
         # host transport (gloo through torch.distributed): the rehearsal of
         # the multi-rank path with several ranks on one GPU; the IPC transport
@@ -380,11 +425,7 @@ def main():
     # three 512 MB fp64 arrays, HIP events, outside any profiler
     stream = s.stream_triad(64 << 20, 20) if args.stream else None
 
-    workload = "%s: manhattan_grid_%dx%d_DYNWAVE_%s_D%gft_q%gcfs_P%d" % (
-        args.config, rows, cfg["grid"],
-        "fixed%gs" % cfg["route_step"] if cfg["variable_step"] == 0 else
-        "variable%g_max%gs" % (cfg["variable_step"], cfg["route_step"]),
-        cfg["diameter"], cfg["q"], cfg["pollutants"])
+    workload = workload_name(args.config, cfg, rows)
 
     def avg_us(name):
         n, ms = kt[name]
@@ -582,7 +623,11 @@ def main():
                                        "ncclRecv and flag all-reduce every Picard iteration)"
                                        if args.rccl_1rank else "single"),
                        "backend": backend,
-                       "transport": transport},
+                       "transport": transport,
+                       "partition": None if world == 1 else (
+                           "contiguous row strips of equal node count" if balance is None else
+                           "contiguous node blocks of equal weight: 1 + %.3f x measured sparse node updates per "
+                           "step (%s)" % (balance["lambda"], balance["source"]))},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

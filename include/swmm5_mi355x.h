@@ -146,6 +146,18 @@ int    DLLEXPORT swmmx_setTransport(int kind);
  * a fallback note), written into buf. */
 int    DLLEXPORT swmmx_getTransport(char *buf, int size);
 
+/* Per-node work weights for the partition (global node order, n = the node
+ * count; call after swmmx_setPartition, on every rank, before swmm_open's
+ * partition is used): the contiguous node blocks then carry equal total
+ * weight instead of equal node counts.  n = 0 restores equal counts. */
+int    DLLEXPORT swmmx_setPartitionWeights(const double *w, int n);
+
+/* Per node (global order, owned nodes of this rank; 0 elsewhere): its updates
+ * in Picard iterations k >= 2 of the steps timed since swmmx_setTiming(1) --
+ * the measured sparse work a weighted partition balances.  Returns the node
+ * count or -1. */
+int    DLLEXPORT swmmx_getNodeWork(double *out, int n);
+
 /* Owning rank of every node (objType swmm_NODE) or link (swmm_LINK) under the
  * current partition; returns the object count. */
 int    DLLEXPORT swmmx_getOwner(int objType, int *out, int n);

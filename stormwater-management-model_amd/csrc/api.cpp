@@ -1272,6 +1272,21 @@ int DLLEXPORT swmmx_setExchange(int (*fn)(double*, long, int, void*), void* user
     return 0;
 }
 
+int DLLEXPORT swmmx_setPartitionWeights(const double* w, int n)
+{
+    if (n < 0 || (n > 0 && !w)) return 500;
+    gPart.weight.assign(w, w + n);
+    return 0;
+}
+
+int DLLEXPORT swmmx_getNodeWork(double* out, int n)
+{
+    if (!G || !G->router || !G->router->ok() || !out) return -1;
+    for (int i = 0; i < n; i++) out[i] = 0.0;
+    if (G->router->nodeWork(out, n)) return -1;
+    return G->prj->net.nNodes();
+}
+
 int DLLEXPORT swmmx_setTransport(int kind)
 {
     if (kind < XCHG_RCCL || kind > XCHG_IPC) return 500;
@@ -1293,6 +1308,7 @@ int DLLEXPORT swmmx_getOwner(int objType, int* out, int n)
     Partition p;
     p.rank = gPart.rank;
     p.nranks = gPart.nranks;
+    p.weight = gPart.weight;
     std::string m;
     if (buildPartition(G->prj->net, p, &m)) return -1;
     const std::vector<int>& v = (objType == swmm_NODE) ? p.nodeOwner : p.linkOwner;
@@ -1307,6 +1323,7 @@ long DLLEXPORT swmmx_getPartition(const char* name, int* out, long n)
     Partition p;
     p.rank = gPart.rank;
     p.nranks = gPart.nranks;
+    p.weight = gPart.weight;
     std::string m;
     if (buildPartition(G->prj->net, p, &m)) return -1;
     std::vector<int> rowptr, csr, hg;

@@ -332,6 +332,7 @@ struct Params {
     StatsDev st;
     int multi;                    // partitioned (multi-GPU) run
     int countWork;                // timing mode: count updated conduits per iteration
+    unsigned* nodeWork;           // timing mode: per node, its updates in iterations k >= 2 (partition weights)
     // multi-GPU exchange (partition.h): link arrays hold this rank's owned
     // links [0, nL) and its ghost links [nL, nLs) (other ranks' links touching
     // a held node).  Each iteration k_xpack packs the owned links other ranks
@@ -1814,7 +1815,10 @@ __device__ __forceinline__ void nodeItem(const Params& p, int k, int i, double d
                 }
             }
         }
-        if (!done || isFast) live++;
+        if (!done || isFast) {
+            live++;
+            if (!kFirst && k >= 2 && p.countWork) p.nodeWork[i] += 1u;   // (one thread per node and launch)
+        }
         if (isFast) fast++;
         if (!done) {
         // the CSR row bounds load with the node's own state (not after the
@@ -5219,6 +5223,8 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
         p.dirty = devAlloc<unsigned char>(d, nN, &e);
         if (e == hipSuccess) e = hipMemset(p.dirty, 0, std::max<size_t>(nN, 1));
+        if (e == hipSuccess) p.nodeWork = devAlloc<unsigned>(d, nN, &e);
+        if (e == hipSuccess) e = hipMemset(p.nodeWork, 0, std::max<size_t>(nN, 1) * sizeof(unsigned));
         if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
         p.frz = devAlloc<unsigned char>(d, nN, &e);
         if (e == hipSuccess) e = hipMemset(p.frz, 0, std::max<size_t>(nN, 1));
@@ -6467,6 +6473,8 @@ void Router::setTiming(bool on)
     }
     d_->timing = on;
     if (!on) d_->curX = nullptr;
+    if (on && d_->p.nodeWork)                      // the per-node work of the steps timed from now on
+        (void)hipMemsetAsync(d_->p.nodeWork, 0, std::max<size_t>(d_->p.nN, 1) * sizeof(unsigned), d_->stream);
     d_->p.countWork = on ? 1 : 0;                  // eager launches only; the graph keeps 0
     for (int k = 0; k < Impl::kClasses; k++) { d_->kms[k] = 0; d_->kcnt[k] = 0; d_->kbytesSum[k] = 0; }
     d_->workSum = 0;
@@ -6782,6 +6790,22 @@ int Router::packResults(double f, double uL, double uV, double uQ, const float**
 }
 
 const Partition& Router::partition() const { return d_->part; }
+
+int Router::nodeWork(double* out, int n)
+{
+    auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
+    Impl* d = d_;
+    flushTiming(d);
+    std::vector<unsigned> w((size_t)std::max(d->p.nN, 1));
+    WAITCHECK(waitDone(d_, nullptr));
+    HIPCHECK(hipMemcpy(w.data(), d->p.nodeWork, w.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+    const Partition& part = d->part;
+    for (int i = 0; i < d->p.nN; i++) {
+        const int g = part.active() ? part.lnode[i] : i;
+        if (g < n && (!part.active() || part.owned[i])) out[g] = (double)w[i];
+    }
+    return 0;
+}
 std::string Router::transport() const { return d_->transportName; }
 
 int Router::allreduceHost(double* buf, int n, int op)

@@ -3,6 +3,7 @@
 #include "partition.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <numeric>
 #include <string>
@@ -40,8 +41,24 @@ int buildPartition(const Network& net, Partition& part, std::string* msg)
     part.nodeOwner.assign(nN, 0);
     long long block = 0;
     if (const char* b = getenv("SWMM5_PART_BLOCK")) block = atoll(b);
-    for (int i = 0; i < nN; i++)
-        part.nodeOwner[i] = block > 0 ? (int)((i / block) % R) : (int)((long long)i * R / nN);
+    const bool weighted = block <= 0 && (int)part.weight.size() == nN && nN > 0;
+    if (weighted) {
+        // contiguous blocks of equal weight: node i goes to the rank whose
+        // share holds the midpoint of its weight interval
+        double total = 0.0;
+        for (int i = 0; i < nN; i++) total += std::max(part.weight[i], 0.0);
+        double run = 0.0;
+        for (int i = 0; i < nN; i++) {
+            const double w = std::max(part.weight[i], 0.0);
+            const double mid = run + 0.5 * w;
+            run += w;
+            int r = total > 0.0 ? (int)(mid * R / total) : (int)((long long)i * R / nN);
+            part.nodeOwner[i] = std::min(std::max(r, 0), R - 1);
+        }
+    } else {
+        for (int i = 0; i < nN; i++)
+            part.nodeOwner[i] = block > 0 ? (int)((i / block) % R) : (int)((long long)i * R / nN);
+    }
     // pumps / regulators: their end nodes ("deferred": updated by k_nc from
     // running link-order totals) and every link touching one stay on one rank,
     // the owner of the group's smallest node

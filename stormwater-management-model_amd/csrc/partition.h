@@ -44,6 +44,11 @@ struct Partition {
     std::vector<unsigned char> ncclId;     // 128-byte ncclUniqueId (RCCL transport / bootstrap)
     ExchangeFn xchg = nullptr;             // host callback (HOST transport; IPC bootstrap)
     void* xuser = nullptr;
+    // optional per-node work weights (global node order; empty: every node
+    // weighs 1): the contiguous node blocks then carry equal weight instead
+    // of equal node counts (swmmx_setPartitionWeights; e.g. 1 + the node's
+    // measured sparse-iteration updates times their relative cost)
+    std::vector<double> weight;
 
     // ---- derived by buildPartition (identical on every rank) -------------
     std::vector<int> nodeOwner, linkOwner;  // global object -> rank

@@ -106,6 +106,9 @@ public:
     // conduits updated, nodes gathered, nodes updated, relaxation-only node
     // updates, k_link ms, k_node ms; returns the number of values available
     int iterationStats(double* out, int n);
+    // per global node (owned ones; out[] untouched elsewhere): its updates in
+    // Picard iterations k >= 2 of the steps timed since setTiming(true)
+    int nodeWork(double* out, int n);
     std::string deviceName() const { return devName_; }
     // the multi-GPU transport in use ("single", "rccl", "host", "ipc", or a
     // fallback note)

@@ -109,6 +109,8 @@ def load_library(path: str | None = None):
         "swmmx_setPartition": (c_int, [c_int, c_int, ctypes.c_void_p, c_int]),
         "swmmx_setExchange": (c_int, [ctypes.c_void_p, ctypes.c_void_p]),
         "swmmx_setTransport": (c_int, [c_int]),
+        "swmmx_setPartitionWeights": (c_int, [P(c_dbl), c_int]),
+        "swmmx_getNodeWork": (c_int, [P(c_dbl), c_int]),
         "swmmx_getTransport": (c_int, [ctypes.c_char_p, c_int]),
         "swmmx_getOwner": (c_int, [c_int, P(c_int), c_int]),
         "swmmx_getPartition": (ctypes.c_long, [c_char_p, P(c_int), ctypes.c_long]),
@@ -379,6 +381,24 @@ class SWMM:
         "host" (the set_exchange callback) or "ipc" (device stores into the
         peers' memory; bootstrapped over the callback when one is set)."""
         return self.L.swmmx_setTransport(self.TRANSPORTS[kind])
+
+    def set_partition_weights(self, w):
+        """Per-node work weights of the partition (swmmx_setPartitionWeights);
+        None or empty: equal node counts."""
+        import numpy as np
+        if w is None or len(w) == 0:
+            return self.L.swmmx_setPartitionWeights(None, 0)
+        a = np.ascontiguousarray(w, dtype=np.float64)
+        self._pw = a
+        return self.L.swmmx_setPartitionWeights(a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), a.size)
+
+    def node_work(self):
+        """Per-node updates in iterations k >= 2 of the timed steps (owned nodes)."""
+        import numpy as np
+        n = self.getCount(NODE)
+        a = np.zeros(max(n, 1))
+        self.L.swmmx_getNodeWork(a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n)
+        return a[:n]
 
     def transport(self) -> str:
         buf = ctypes.create_string_buffer(256)

@@ -42,6 +42,9 @@ def main():
 
         s.set_partition(rank, world)
         s.set_exchange(xchg)
+        if os.environ.get("WORKER_WEIGHTS") == "ramp":   # a weighted partition: later nodes weigh up to 4x
+            nN = int(os.environ["WORKER_NODES"])
+            s.set_partition_weights(np.linspace(1.0, 4.0, nN))
         if transport == "ipc":          # device stores into the peers' memory; gloo bootstraps it
             s.set_transport("ipc")
     else:

@@ -118,6 +118,50 @@ def _layout(inp, tmp_path, rank, world):
         s.set_partition(0, 1)
 
 
+def test_weighted_partition_layout(tmp_path):
+    """swmmx_setPartitionWeights: contiguous node blocks of equal total
+    weight (node i to the rank whose share holds the midpoint of its weight
+    interval); every held node still sees all its conduits in global order
+    and every ghost is sent by its owner in the receiver's order."""
+    inp = _grid(tmp_path, 24, 20)
+    d = _topology(inp, tmp_path)
+    n1, n2 = d["link.node1"].astype(int), d["link.node2"].astype(int)
+    nN = len(d["node.type"])
+    w = np.linspace(1.0, 4.0, nN)
+    for world in (2, 3):
+        mid = np.cumsum(w) - 0.5 * w
+        ref = np.minimum((mid * world / w.sum()).astype(int), world - 1)
+        lays = []
+        for r in range(world):
+            s = swmm5.SWMM()
+            s.set_partition(r, world)
+            s.set_partition_weights(w)
+            try:
+                assert s.open(inp, str(tmp_path / "w.rpt"), str(tmp_path / "w.out")) == 0
+                owner = s.owners(swmm5.NODE)
+                lays.append({k: s.partition_array(k) for k in ("lnode", "llink", "lghost", "nbr", "sendOff",
+                                                               "sendLink", "recvOff", "rowptr", "csr")})
+            finally:
+                s.close()
+                s.set_partition(0, 1)
+            junction = d["node.type"].astype(int) != 1
+            np.testing.assert_array_equal(owner[junction], ref[junction])
+        counts = np.bincount(owner[:-1], minlength=world)
+        assert counts[0] > counts[-1]                      # the heavier tail is split finer
+        rows = _incident(n1, n2, nN)
+        for r, L in enumerate(lays):
+            loc = np.concatenate([L["llink"], L["lghost"]])
+            rp, csr = L["rowptr"], L["csr"]
+            for i, g in enumerate(L["lnode"]):
+                got = [(int(loc[e & 0x7FFFFFFF]), int((e >> 31) & 1)) for e in csr[rp[i]:rp[i + 1]]]
+                assert got == rows[g], (r, g)
+            for k, s_ in enumerate(L["nbr"]):
+                S = lays[s_]
+                ks = list(S["nbr"]).index(r)
+                np.testing.assert_array_equal(L["lghost"][L["recvOff"][k]:L["recvOff"][k + 1]],
+                                              S["llink"][S["sendLink"][S["sendOff"][ks]:S["sendOff"][ks + 1]]])
+
+
 def _incident(n1, n2, nN):
     rows = [[] for _ in range(nN)]
     for j in range(len(n1)):
@@ -438,7 +482,7 @@ def _grid_with_regulators(tmp_path, n=20):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,block,pollutants,transport", [
     (2, 0, 0, "host"), (3, 0, 0, "host"), (2, 90, 0, "host"), (3, 60, 0, "host"), (2, 0, 2, "host"),
-    (2, 0, 0, "ipc"), (3, 60, 0, "ipc"), (2, 0, 2, "ipc")])
+    (2, 0, 0, "ipc"), (3, 60, 0, "ipc"), (2, 0, 2, "ipc"), (3, -1, 0, "ipc")])
 def test_ranks_list_graph_bitwise(world, block, pollutants, transport, tmp_path):
     """The list graph (iterations k >= 2 as unconverged-list walks and
     live-list node passes, each followed by the neighbour exchange and the
@@ -450,7 +494,9 @@ def test_ranks_list_graph_bitwise(world, block, pollutants, transport, tmp_path)
     with two pollutants (the frozen junctions' final depths then come from the
     quality kernel, after the ghost links' concentrations moved)."""
     inp = _grid(tmp_path, 30, 30, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.5, pollutants=pollutants)
-    env = {"SWMM5_SPARSE": "3", "SWMM5_PART_BLOCK": str(block)}
+    env = {"SWMM5_SPARSE": "3", "SWMM5_PART_BLOCK": str(max(block, 0))}
+    if block < 0:                         # a weighted partition (node weights 1 .. 4, swmmx_setPartitionWeights)
+        env.update(WORKER_WEIGHTS="ramp", WORKER_NODES=str(30 * 30 + 1))
     one = _run_workers(inp, 250, tmp_path, 1, "host", "one", extra_env=env)[0]
     st, its, nonconv = one["counters"]
     assert nonconv > 10 and its / st > 2.5, one["counters"]

@@ -41,6 +41,14 @@ for s in $STEPS; do
              NCCL_SOCKET_IFNAME=lo NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,BOOTSTRAP run rcclprobe_lo_$n 90 ./tools/rccl_capture_probe $n
              NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,BOOTSTRAP run rcclprobe_auto_$n 90 ./tools/rccl_capture_probe $n
            done ;;
+    calib) # partition weights from one GPU (tools/calibrate_partition.py) -> profiles/partition_weights.json
+           for spec in ${CALS:-4m:2 1m_surcharge:2 1m_surcharge:4 1m_surcharge:8}; do
+             run calib_${spec/:/_} 600 python tools/calibrate_partition.py --config ${spec%%:*} --gpus ${spec##*:}
+           done ;;
+    balance) # the 2-rank 4M rehearsal on this GPU: equal strips against weighted blocks (per_rank_sparse_work)
+           for bal in off auto; do
+             run balance_$bal 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${NP:-2} --master-addr 127.0.0.1 --master-port $((29700 + RANDOM % 200)) bench.py --gpus ${NP:-2} --config ${CFG:-4m} --steps 10 --warmup 2 --timing-steps 4 --exchange ${XCH:-ipc} --balance $bal --no-cpu --no-stream --kernel-reps 0
+           done ;;
     tmulti) run tmulti 900 python -u -m pytest tests/test_multigpu.py -x -v -p no:cacheprovider --timeout 600 --timeout-method thread -m gpu -k "${TKM:-write_one_gpu or rccl}" ;;
     rccl1) for c in ${RCFGS:-1m_surcharge 4m}; do run rccl1_$c 600 python bench.py --config $c --rccl-1rank --no-cpu --kernel-reps 0 --steps 100 && run plain1_$c 600 python bench.py --config $c --no-cpu --kernel-reps 0 --steps 100; done ;;
     tk) run tk 900 python -u -m pytest tests -x -v -p no:cacheprovider -m gpu --timeout 400 --timeout-method thread -k "${TK:-exfil}" ;;
