@@ -156,7 +156,7 @@ CASES = {
     # never steady, routing.c:224, 388-391), storage units and pollutants
     "example_steady_pump": (netgen.write_example, dict(end_time="08:00:00", route_step=10.0,
                                                        regulators=True, storage=True, pollutants=True,
-                                                       options={"SKIP_STEADY_STATE": "YES"}), 2),
+                                                       options={"SKIP_STEADY_STATE": "YES"}), 1),
     "example_dummy": (netgen.write_example, dict(end_time="02:00:00", route_step=5.0, dummy=True,
                                                  pollutants=True), 1),
     "example_dummy_var": (netgen.write_example, dict(end_time="02:00:00", route_step=10.0, variable_step=0.75,

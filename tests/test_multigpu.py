@@ -619,7 +619,9 @@ def test_steady_state_skipping_ranks_bitwise(case, transport, tmp_path):
     shutil.copy(_golden.inp(case), inp)
     one = _run_workers(inp, 100000, tmp_path, 1, "host", "one", save=True)[0]
     parts = _run_workers(inp, 100000, tmp_path, 2, transport, "two", save=True)
-    assert all((p["link_owner"] == r).any() for r, p in enumerate(parts))
+    # both ranks own nodes (with pumps and regulators the end-node groups may
+    # leave every link on one rank: the steady decision is still reduced)
+    assert all((p["node_owner"] == r).any() for r, p in enumerate(parts))
     _assert_bitwise(parts, one)
     assert open(str(tmp_path / "two_r0.out"), "rb").read() == open(str(tmp_path / "one_r0.out"), "rb").read()
 

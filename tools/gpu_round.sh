@@ -44,7 +44,8 @@ for s in $STEPS; do
     calib) # partition weights from one GPU (tools/calibrate_partition.py) -> profiles/partition_weights.json
            for spec in ${CALS:-4m:2 1m_surcharge:2 1m_surcharge:4 1m_surcharge:8}; do
              run calib_${spec/:/_} 600 python tools/calibrate_partition.py --config ${spec%%:*} --gpus ${spec##*:}
-           done ;;
+           done
+           cp profiles/partition_weights.json gpurun_out/ ;;
     balance) # the 2-rank 4M rehearsal on this GPU: equal strips against weighted blocks (per_rank_sparse_work)
            for bal in off auto; do
              run balance_$bal 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${NP:-2} --master-addr 127.0.0.1 --master-port $((29700 + RANDOM % 200)) bench.py --gpus ${NP:-2} --config ${CFG:-4m} --steps 10 --warmup 2 --timing-steps 4 --exchange ${XCH:-ipc} --balance $bal --no-cpu --no-stream --kernel-reps 0
