@@ -362,6 +362,9 @@ def main():
     nL = s.getCount(swmm5.LINK)
     nN = s.getCount(swmm5.NODE)
     nL_rank = int((s.owners(swmm5.LINK) == rank).sum()) if world > 1 else nL
+    # this rank's layout: owned nodes, held nodes (owned + replicas), ghost links
+    layout = ([int((s.owners(swmm5.NODE) == rank).sum()), int(s.partition_array("lnode").size),
+               int(s.partition_array("lghost").size)] if world > 1 else [nN, nN, 0])
 
     if cfg["spinup"]:
         err, _ = s.run_steps(cfg["spinup"])
@@ -546,11 +549,14 @@ def main():
         # each rank's sparse work (iterations k >= 2): the load balance of the
         # strips (the surcharged region sits next to the outlet, on the last one)
         mine_w = [round(sum(x["conduits_updated"] for x in per_iter if x["k"] >= 2)),
-                  round(sum(x["nodes_updated"] for x in per_iter if x["k"] >= 2))]
+                  round(sum(x["nodes_updated"] for x in per_iter if x["k"] >= 2)),
+                  *layout]
         allw = [None] * world
         dist.all_gather_object(allw, mine_w)
         roof["per_rank_sparse_work"] = {"conduits_updated_k>=2": [w[0] for w in allw],
-                                        "nodes_updated_k>=2": [w[1] for w in allw]}
+                                        "nodes_updated_k>=2": [w[1] for w in allw],
+                                        "owned_nodes": [w[2] for w in allw], "held_nodes": [w[3] for w in allw],
+                                        "ghost_links": [w[4] for w in allw]}
     if world > 1 and kt.get("ghost_exchange", (0, 0))[0]:
         # the per-iteration exchanges on the routing stream (timing-mode
         # steps): their cost per Picard iteration on this rank
@@ -625,6 +631,8 @@ def main():
                        "backend": backend,
                        "transport": transport,
                        "partition": None if world == 1 else (
+                           ("blocks of %s nodes dealt to the ranks in turn (SWMM5_PART_BLOCK)"
+                            % os.environ["SWMM5_PART_BLOCK"]) if int(os.environ.get("SWMM5_PART_BLOCK", "0")) > 0 else
                            "contiguous row strips of equal node count" if balance is None else
                            "contiguous node blocks of equal weight: 1 + %.3f x measured sparse node updates per "
                            "step (%s)" % (balance["lambda"], balance["source"]))},

@@ -35,12 +35,27 @@ for s in $STEPS; do
     tsparse) run tsparse 900 python -u -m pytest tests/test_gpu_vs_oracle.py -x -v -p no:cacheprovider --timeout 400 --timeout-method thread -k "${TK:-frozen or sparse or regime_window_707}" ;;
     tipc) run tipc 900 python -u -m pytest tests/test_multigpu.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu -k "${TKM:-ipc}" ;;
     ipc2) for x in ${XS:-ipc host}; do run ipc2_$x 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${NP:-2} --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) bench.py --gpus ${NP:-2} --config ${CFG:-1m_surcharge} --steps ${BSTEPS:-20} --warmup 5 --spinup ${SPIN:-200} --exchange $x --no-cpu --no-stream --kernel-reps 0; done ;;
+    sig) # per-iteration exchange cost: a tiny launch-bound grid on one rank, then on two ranks of this GPU
+         SWMM5_SPARSE=3 run sig_1 300 python bench.py --grid ${SGRID:-24} --spinup 0 --steps 400 --warmup 20 --no-cpu --no-stream --kernel-reps 0
+         for x in ${XS:-ipc host}; do
+           run sig_2_$x 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $((29400 + RANDOM % 100)) bench.py --gpus 2 --grid ${SGRID:-24} --spinup 0 --steps 400 --warmup 20 --exchange $x --no-cpu --no-stream --kernel-reps 0
+         done ;;
+    trace2) # kernel traces of both ranks of a small 2-rank IPC run (tools/mrank_launch.py: one rocprofv3 per rank)
+           rm -rf gpurun_out/trace2 && run trace2 300 python tools/mrank_launch.py --np 2 --prof gpurun_out/trace2 -- bench.py --gpus 2 --grid ${SGRID:-24} --spinup 0 --steps 100 --warmup 10 --exchange ${XCH:-ipc} --no-cpu --no-stream --kernel-reps 0 --timing-steps 2 ;;
+    sigprobe) # the IPC signalling alone (tools/ipc_signal_probe.hip): two ranks on two streams of one
+           # process, then two processes on this one device
+           run sigprobe_thread 60 ./tools/ipc_signal_probe \
+           && rm -rf gpurun_out/sigp && mkdir -p gpurun_out/sigp \
+           && run sigprobe_proc 120 bash -c './tools/ipc_signal_probe proc 0 gpurun_out/sigp > gpurun_out/sigprobe_p0.txt 2>&1 & ./tools/ipc_signal_probe proc 1 gpurun_out/sigp > gpurun_out/sigprobe_p1.txt 2>&1; s1=$?; wait $!; s0=$?; cat gpurun_out/sigprobe_p0.txt gpurun_out/sigprobe_p1.txt; exit $((s0 | s1))' ;;
     rcclprobe) # the captured RCCL call pattern on one rank (tools/rccl_capture_probe.cpp), phase by phase,
            # bootstrap on the loopback interface and, for comparison, on RCCL's own interface choice
+           # (graphs destroyed before the communicator); TEARDOWN=comm: the round-5 order
            for n in ${PREPS:-2 8 16}; do
-             NCCL_SOCKET_IFNAME=lo NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,BOOTSTRAP run rcclprobe_lo_$n 90 ./tools/rccl_capture_probe $n
-             NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,BOOTSTRAP run rcclprobe_auto_$n 90 ./tools/rccl_capture_probe $n
+             NCCL_SOCKET_IFNAME=lo NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,BOOTSTRAP run rcclprobe_lo_$n 90 ./tools/rccl_capture_probe $n ${TEARDOWN:-graphs}
+             NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT,BOOTSTRAP run rcclprobe_auto_$n 90 ./tools/rccl_capture_probe $n ${TEARDOWN:-graphs}
            done ;;
+    rcclteardown) # the round-5 teardown order alone, bounded (expected to hang in ncclCommDestroy)
+           NCCL_SOCKET_IFNAME=lo NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT run rcclprobe_commfirst 60 ./tools/rccl_capture_probe 2 comm ;;
     calib) # partition weights from one GPU (tools/calibrate_partition.py) -> profiles/partition_weights.json
            for spec in ${CALS:-4m:2 1m_surcharge:2 1m_surcharge:4 1m_surcharge:8}; do
              run calib_${spec/:/_} 600 python tools/calibrate_partition.py --config ${spec%%:*} --gpus ${spec##*:}
@@ -49,6 +64,10 @@ for s in $STEPS; do
     balance) # the 2-rank 4M rehearsal on this GPU: equal strips against weighted blocks (per_rank_sparse_work)
            for bal in off auto; do
              run balance_$bal 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${NP:-2} --master-addr 127.0.0.1 --master-port $((29700 + RANDOM % 200)) bench.py --gpus ${NP:-2} --config ${CFG:-4m} --steps 10 --warmup 2 --timing-steps 4 --exchange ${XCH:-ipc} --balance $bal --no-cpu --no-stream --kernel-reps 0
+           done ;;
+    blocks) # the 2-rank 4M rehearsal with node blocks dealt in turn (shared nodes freeze since round 6)
+           for b in ${PBLOCKS:-22624 90496}; do
+             SWMM5_PART_BLOCK=$b run balance_block_$b 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $((29700 + RANDOM % 200)) bench.py --gpus 2 --config ${CFG:-4m} --steps 10 --warmup 2 --timing-steps 4 --exchange ${XCH:-ipc} --balance off --no-cpu --no-stream --kernel-reps 0
            done ;;
     tmulti) run tmulti 900 python -u -m pytest tests/test_multigpu.py -x -v -p no:cacheprovider --timeout 600 --timeout-method thread -m gpu -k "${TKM:-write_one_gpu or rccl}" ;;
     rccl1) for c in ${RCFGS:-1m_surcharge 4m}; do run rccl1_$c 600 python bench.py --config $c --rccl-1rank --no-cpu --kernel-reps 0 --steps 100 && run plain1_$c 600 python bench.py --config $c --no-cpu --kernel-reps 0 --steps 100; done ;;
@@ -73,7 +92,7 @@ for s in $STEPS; do
            for m in ${SKIPS:-0 1 2 4 8 16 32 64}; do
              SWMM5_STEPEND_SKIP=$m run pmcskip_f_$m 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcskip_f_$m -o run -- python3 bench.py --no-cpu --steps 30 --warmup 5 --timing-steps 2 --kernel-reps 0 \
              && SWMM5_STEPEND_SKIP=$m run pmcskip_w_$m 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcskip_w_$m -o run -- python3 bench.py --no-cpu --steps 30 --warmup 5 --timing-steps 2 --kernel-reps 0; done ;;
-    calib)  run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/calib_fetch -o run -- ./tools/pmc_calib \
+    pmccal) run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/calib_fetch -o run -- ./tools/pmc_calib \
               && run calib_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/calib_write -o run -- ./tools/pmc_calib ;;
     sq)     run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD --output-format csv -d gpurun_out/pmc_sq -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu ;;
   esac

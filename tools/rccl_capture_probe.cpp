@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 #include <chrono>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <vector>
 
@@ -39,6 +40,10 @@ int main(int argc, char** argv)
 {
     setvbuf(stdout, nullptr, _IONBF, 0);
     const int kRep = argc > 1 ? atoi(argv[1]) : 16;
+    // teardown order: "graphs" (default) destroys every graph that captured
+    // RCCL work before the communicator; "comm" destroys the communicator
+    // while the timing graphs still exist (the round-5 order of this probe)
+    const bool commFirst = argc > 2 && strcmp(argv[2], "comm") == 0;
     const size_t n = 4 * 2828;                    // a 4M strip boundary: 2 x 1414 links x 4 doubles
     const char* ifn = getenv("NCCL_SOCKET_IFNAME");
     printf("[%.3f s] start: %d repetitions, NCCL_SOCKET_IFNAME=%s\n", secs(), kRep, ifn ? ifn : "(unset)");
@@ -126,8 +131,21 @@ int main(int argc, char** argv)
     if (timeGraph(gx[0], &tAll)) return 2;
     printf("captured send/recv (%zu doubles) + all-reduce, 50 checked replays: %d mismatches\n", n, bad);
     printf("inside a graph, per occurrence: both %.2f us, send/recv alone %.2f us, all-reduce alone %.2f us\n", tAll, tX, tF);
+    printf("[%.3f s] teardown (%s first)\n", secs(), commFirst ? "communicator" : "graphs");
+    if (commFirst) {
+        ncclCommDestroy(comm);
+        printf("[%.3f s] communicator destroyed\n", secs());
+    }
+    for (int v = 0; v < 3; v++) {
+        (void)hipGraphExecDestroy(gx[v]);
+        (void)hipGraphDestroy(gr[v]);
+    }
     (void)hipGraphExecDestroy(ge);
     (void)hipGraphDestroy(g);
-    ncclCommDestroy(comm);
+    printf("[%.3f s] graphs destroyed\n", secs());
+    if (!commFirst) {
+        ncclCommDestroy(comm);
+        printf("[%.3f s] communicator destroyed\n", secs());
+    }
     return bad ? 1 : 0;
 }
