@@ -118,12 +118,13 @@ def workload_name(config, cfg, rows):
         cfg["diameter"], cfg["q"], cfg["pollutants"])
 
 
-def partition_weights(workload, rows, nx, n_nodes):
+def partition_weights(workload, rows, nx, n_nodes, lam=None):
     """Per-node weights from profiles/partition_weights.json (tools/
     calibrate_partition.py: the workload's per-row sparse node updates per
     step measured on one GPU, and the marginal cost of a sparse update
-    relative to a full-pass node): node i of row r weighs 1 + lambda u_r / nx,
-    the outfall 1.  None when no record matches this grid."""
+    relative to a full-pass node): node i of row r weighs 1 + lambda u_r / nx
+    (lam overrides the record's lambda), the outfall 1.  None when no record
+    matches this grid."""
     path = os.path.join(ROOT, "profiles", "partition_weights.json")
     if not os.path.exists(path):
         return None, None
@@ -133,7 +134,7 @@ def partition_weights(workload, rows, nx, n_nodes):
     import numpy as np
     w = np.ones(n_nodes)
     ru = np.asarray(rec["row_updates"], dtype=np.float64)
-    w[:rows * nx] = 1.0 + rec["lambda"] * np.repeat(ru / nx, nx)
+    w[:rows * nx] = 1.0 + (rec["lambda"] if lam is None else lam) * np.repeat(ru / nx, nx)
     return w, rec
 
 
@@ -279,9 +280,11 @@ def main():
                          "flag all-reduce every Picard iteration): the in-graph cost of the collectives")
     ap.add_argument("--no-stream", dest="stream", action="store_false",
                     help="skip the STREAM-triad measurement of the achievable HBM bandwidth")
-    ap.add_argument("--balance", choices=["auto", "off"], default="auto",
-                    help="several ranks: weigh the partition by the workload's measured sparse work "
-                         "(profiles/partition_weights.json, tools/calibrate_partition.py) when a record exists")
+    ap.add_argument("--balance", choices=["auto", "weighted", "off"], default="auto",
+                    help="several ranks, when the workload has a record of its measured sparse work "
+                         "(profiles/partition_weights.json, tools/calibrate_partition.py): auto = two regions "
+                         "(the surcharged band and the rest, each shared equally), weighted = contiguous blocks "
+                         "of equal weight; off = row strips of equal node count")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per link-momentum launch from rocprofv3 PMC (profiles/)")
     args = ap.parse_args()
@@ -332,11 +335,19 @@ def main():
     elif args.rccl_1rank:
         s.set_partition(0, 1, s.nccl_unique_id())
     balance = None
-    if world > 1 and args.balance == "auto":
+    if world > 1 and args.balance != "off":
+        # auto: two regions -- the surcharged band (nodes that run every
+        # sparse iteration) and the rest, each cut into equal blocks, so
+        # every rank gets an equal share of both (only the per-node work's
+        # shape matters, lambda = 1); weighted: one contiguous block of equal
+        # weight 1 + lambda u per rank
         n_nodes = rows * cfg["grid"] + 1
-        w, balance = partition_weights(workload_name(args.config, cfg, rows), rows, cfg["grid"], n_nodes)
+        w, balance = partition_weights(workload_name(args.config, cfg, rows), rows, cfg["grid"], n_nodes,
+                                       lam=1.0 if args.balance == "auto" else None)
         if w is not None:
             s.set_partition_weights(w)
+            if args.balance == "auto":
+                s.set_partition_mode("two_region")
     if world > 1 and args.exchange in ("host", "ipc"):
         # host transport (gloo through torch.distributed): the rehearsal of
         # the multi-rank path with several ranks on one GPU; the IPC transport
@@ -634,6 +645,9 @@ def main():
                            ("blocks of %s nodes dealt to the ranks in turn (SWMM5_PART_BLOCK)"
                             % os.environ["SWMM5_PART_BLOCK"]) if int(os.environ.get("SWMM5_PART_BLOCK", "0")) > 0 else
                            "contiguous row strips of equal node count" if balance is None else
+                           ("two regions, the surcharged band (per-node sparse updates at least half the "
+                            "largest) and the rest, each cut into one equal block per rank (%s)" % balance["source"])
+                           if args.balance == "auto" else
                            "contiguous node blocks of equal weight: 1 + %.3f x measured sparse node updates per "
                            "step (%s)" % (balance["lambda"], balance["source"]))},
             "roofline": roof,

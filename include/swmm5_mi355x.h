@@ -152,6 +152,16 @@ int    DLLEXPORT swmmx_getTransport(char *buf, int size);
  * weight instead of equal node counts.  n = 0 restores equal counts. */
 int    DLLEXPORT swmmx_setPartitionWeights(const double *w, int n);
 
+/* Partition mode (with weights; call like swmmx_setPartitionWeights): 0 one
+ * contiguous block of equal weight per rank (the default); 1 two regions --
+ * the "hot" nodes (weight excess over the lightest node at least half the
+ * largest excess: e.g. the surcharged band whose nodes run every sparse
+ * Picard iteration) and the other nodes are each cut into nranks contiguous
+ * blocks of equal weight, rank r taking block r of both, so every rank gets
+ * an equal share of the sparse work and of the full passes.  Returns 0 or 500
+ * for an unknown mode. */
+int    DLLEXPORT swmmx_setPartitionMode(int mode);
+
 /* Per node (global order, owned nodes of this rank; 0 elsewhere): its updates
  * in Picard iterations k >= 2 of the steps timed since swmmx_setTiming(1) --
  * the measured sparse work a weighted partition balances.  Returns the node

@@ -1279,6 +1279,13 @@ int DLLEXPORT swmmx_setPartitionWeights(const double* w, int n)
     return 0;
 }
 
+int DLLEXPORT swmmx_setPartitionMode(int mode)
+{
+    if (mode != PART_CONTIGUOUS && mode != PART_TWO_REGION) return 500;
+    gPart.mode = mode;
+    return 0;
+}
+
 int DLLEXPORT swmmx_getNodeWork(double* out, int n)
 {
     if (!G || !G->router || !G->router->ok() || !out) return -1;
@@ -1309,6 +1316,7 @@ int DLLEXPORT swmmx_getOwner(int objType, int* out, int n)
     p.rank = gPart.rank;
     p.nranks = gPart.nranks;
     p.weight = gPart.weight;
+    p.mode = gPart.mode;
     std::string m;
     if (buildPartition(G->prj->net, p, &m)) return -1;
     const std::vector<int>& v = (objType == swmm_NODE) ? p.nodeOwner : p.linkOwner;
@@ -1324,6 +1332,7 @@ long DLLEXPORT swmmx_getPartition(const char* name, int* out, long n)
     p.rank = gPart.rank;
     p.nranks = gPart.nranks;
     p.weight = gPart.weight;
+    p.mode = gPart.mode;
     std::string m;
     if (buildPartition(G->prj->net, p, &m)) return -1;
     std::vector<int> rowptr, csr, hg;

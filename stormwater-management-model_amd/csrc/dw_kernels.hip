@@ -2755,15 +2755,15 @@ __device__ __forceinline__ double llDouble(unsigned lo, unsigned hi)
 {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+// The owner's side: this rank's sent links' values, as granules, into each
+// receiving rank's ghost area (threads tid, tid + nthr, ... of the sends)
 template <bool kQual>
-__global__ __launch_bounds__(kBlock) void k_ipc_pack(Params p, int k)
+__device__ void ipcPack(const Params& p, int tid, int nthr)
 {
-    if (!kQual && !iterRuns(p, k)) return;
-    if (xAborted(p) || xStalled(p)) return;
     const unsigned seq = (kQual ? p.xctl->qualSeq : p.xctl->ghostSeq) + 1;
     const int par = seq & 1, F = kQual ? p.P : p.xF;
     const double* lq = kQual ? p.lQual[p.ctl->qualPar] : nullptr;
-    for (int e = blockIdx.x * kBlock + threadIdx.x; e < p.nSend; e += gridDim.x * kBlock) {
+    for (int e = tid; e < p.nSend; e += nthr) {
         const int l = p.sendLink[e];
         const XPeer X = p.xpeer[p.sendNbr[e]];
         const int gi = p.sendGi[e];
@@ -2780,18 +2780,19 @@ __global__ __launch_bounds__(kBlock) void k_ipc_pack(Params p, int k)
         }
     }
 }
+// The receiver's side: wait for every ghost value of this exchange in this
+// rank's own area and write the ghost slots (iteration k >= 2: wake the held
+// ends of a ghost whose value changed).  false when a wait gave up.
 template <bool kQual>
-__global__ __launch_bounds__(kBlock) void k_ipc_unpack(Params p, int k)
+__device__ bool ipcUnpack(const Params& p, int k, int tid, int nthr)
 {
-    if (!kQual && !iterRuns(p, k)) return;
-    if (xAborted(p)) return;
     const unsigned seq = (kQual ? p.xctl->qualSeq : p.xctl->ghostSeq) + 1;
     const int par = seq & 1, F = kQual ? p.P : p.xF;
     const size_t nG = (size_t)p.nGhost;
     const unsigned long long t0 = wall_clock64();
     const unsigned long long* b = (kQual ? p.qualRx : p.ghostRx) + (size_t)par * 2 * F * nG;
     double* lq = kQual ? p.lQual[p.ctl->qualPar] : nullptr;
-    for (int g = blockIdx.x * kBlock + threadIdx.x; g < p.nGhost; g += gridDim.x * kBlock) {
+    for (int g = tid; g < p.nGhost; g += nthr) {
         const int l = p.nL + g;
         bool ch = false;
         for (int f = 0; f < F; f++) {
@@ -2799,7 +2800,7 @@ __global__ __launch_bounds__(kBlock) void k_ipc_unpack(Params p, int k)
             if (!llWait(p, b + (size_t)(2 * f) * nG + g, seq, &lo, t0) ||
                 !llWait(p, b + (size_t)(2 * f + 1) * nG + g, seq, &hi, t0)) {
                 xFail(p, kQual ? XK_QUAL : XK_GHOST, p.ghostFrom[g], seq);
-                return;
+                return false;
             }
             const double v = llDouble(lo, hi);
             if (!kQual && p.xwake && k >= 2) {
@@ -2817,6 +2818,37 @@ __global__ __launch_bounds__(kBlock) void k_ipc_unpack(Params p, int k)
         }
         if (ch) ghostWake(p, l, k);
     }
+    return true;
+}
+template <bool kQual>
+__global__ __launch_bounds__(kBlock) void k_ipc_pack(Params p, int k)
+{
+    if (!kQual && !iterRuns(p, k)) return;
+    if (xAborted(p) || xStalled(p)) return;
+    ipcPack<kQual>(p, blockIdx.x * kBlock + threadIdx.x, gridDim.x * kBlock);
+}
+template <bool kQual>
+__global__ __launch_bounds__(kBlock) void k_ipc_unpack(Params p, int k)
+{
+    if (!kQual && !iterRuns(p, k)) return;
+    if (xAborted(p)) return;
+    (void)ipcUnpack<kQual>(p, k, blockIdx.x * kBlock + threadIdx.x, gridDim.x * kBlock);
+}
+// Pack and unpack in one launch (one kernel boundary less per exchange:
+// tools/ipc_signal_probe measures 3.0-3.3 against 4.1-4.4 us per iteration;
+// opt-in, SWMM5_XCHG_FUSED=1).
+// Every workgroup posts its share of the sends before it waits for anything,
+// and the grid (kXchgGrid workgroups) is small enough to be resident at once,
+// so every rank's posts are made whatever its waiting workgroups hold.
+constexpr int kXchgGrid = 128;
+template <bool kQual>
+__global__ __launch_bounds__(kBlock) void k_ipc_xchg(Params p, int k)
+{
+    if (!kQual && !iterRuns(p, k)) return;
+    if (xAborted(p)) return;
+    const int tid = blockIdx.x * kBlock + threadIdx.x, nthr = gridDim.x * kBlock;
+    if (!xStalled(p)) ipcPack<kQual>(p, tid, nthr);
+    (void)ipcUnpack<kQual>(p, k, tid, nthr);
 }
 // One wave: iteration k's flag from every rank, ORed into unconv[k] (the
 // all-reduce(max) of the RCCL transport); kHello: the start-up handshake
@@ -3922,6 +3954,12 @@ struct Router::Impl {
     int* xerrHost = nullptr;
     int* hostAbortH = nullptr;
     double xTimeoutSec = 60.0;       // SWMM5_XCHG_TIMEOUT: bound of every wait behind an exchange
+    // SWMM5_XCHG_FUSED=1: k_ipc_xchg (pack and unpack in one launch) instead of
+    // k_ipc_pack + k_ipc_unpack.  Off by default: alone (tools/ipc_signal_probe)
+    // it saves a kernel boundary per exchange, but with two ranks time-sharing
+    // one GPU its waiting workgroup held the other rank's kernels back (147
+    // against 17 us per exchange)
+    bool xchgFused = false;
     std::string transportName = "single";
     float *resN = nullptr, *resL = nullptr;          // packed period results (device)
     float *resNHost = nullptr, *resLHost = nullptr;  // pinned copies
@@ -4328,8 +4366,12 @@ static int ghostExchangeImpl(Router::Impl* d, int k)
 {
     const Params& p = d->p;
     if (d->part.transport == XCHG_IPC) {
-        if (p.nSend) hipLaunchKernelGGL(k_ipc_pack<false>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
-        if (p.nGhost) hipLaunchKernelGGL(k_ipc_unpack<false>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
+        if (p.nSend && p.nGhost && d->xchgFused)
+            hipLaunchKernelGGL(k_ipc_xchg<false>, dim3(kXchgGrid), dim3(kBlock), 0, d->stream, p, k);
+        else {
+            if (p.nSend) hipLaunchKernelGGL(k_ipc_pack<false>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
+            if (p.nGhost) hipLaunchKernelGGL(k_ipc_unpack<false>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
+        }
         return 0;
     }
     if (p.nSend) hipLaunchKernelGGL(k_xpack, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
@@ -4341,8 +4383,12 @@ static int qualExchange(Router::Impl* d)
 {
     const Params& p = d->p;
     if (d->part.transport == XCHG_IPC) {
-        if (p.nSend) hipLaunchKernelGGL(k_ipc_pack<true>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, 0);
-        if (p.nGhost) hipLaunchKernelGGL(k_ipc_unpack<true>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, 0);
+        if (p.nSend && p.nGhost && d->xchgFused)
+            hipLaunchKernelGGL(k_ipc_xchg<true>, dim3(kXchgGrid), dim3(kBlock), 0, d->stream, p, 0);
+        else {
+            if (p.nSend) hipLaunchKernelGGL(k_ipc_pack<true>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, 0);
+            if (p.nGhost) hipLaunchKernelGGL(k_ipc_unpack<true>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, 0);
+        }
         return 0;
     }
     if (p.nSend) hipLaunchKernelGGL(k_xpack_qual, dim3(d->gridX), dim3(kBlock), 0, d->stream, p);
@@ -5436,6 +5482,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         }
         if (const char* ts = getenv("SWMM5_XCHG_TIMEOUT"))
             if (atof(ts) > 0.0) d->xTimeoutSec = atof(ts);
+        if (const char* xf = getenv("SWMM5_XCHG_FUSED")) d->xchgFused = atoi(xf) != 0;
         p.xTimeout = (long long)(d->xTimeoutSec * d->wallKHz * 1000.0);
         if (const char* st = getenv("SWMM5_XCHG_STALL")) {     // test hook "rank:step"
             int r = -1;

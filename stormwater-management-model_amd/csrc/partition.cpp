@@ -42,19 +42,36 @@ int buildPartition(const Network& net, Partition& part, std::string* msg)
     long long block = 0;
     if (const char* b = getenv("SWMM5_PART_BLOCK")) block = atoll(b);
     const bool weighted = block <= 0 && (int)part.weight.size() == nN && nN > 0;
-    if (weighted) {
-        // contiguous blocks of equal weight: node i goes to the rank whose
-        // share holds the midpoint of its weight interval
+    // node i of `idx` (ascending node order) goes to the rank whose equal
+    // share of the list's total weight holds the midpoint of its interval
+    auto equalWeightBlocks = [&](const std::vector<int>& idx) {
         double total = 0.0;
-        for (int i = 0; i < nN; i++) total += std::max(part.weight[i], 0.0);
+        for (int i : idx) total += std::max(part.weight[i], 0.0);
         double run = 0.0;
-        for (int i = 0; i < nN; i++) {
-            const double w = std::max(part.weight[i], 0.0);
+        const long long m = (long long)idx.size();
+        for (long long q = 0; q < m; q++) {
+            const double w = std::max(part.weight[idx[q]], 0.0);
             const double mid = run + 0.5 * w;
             run += w;
-            int r = total > 0.0 ? (int)(mid * R / total) : (int)((long long)i * R / nN);
-            part.nodeOwner[i] = std::min(std::max(r, 0), R - 1);
+            int r = total > 0.0 ? (int)(mid * R / total) : (int)(q * R / m);
+            part.nodeOwner[idx[q]] = std::min(std::max(r, 0), R - 1);
         }
+    };
+    if (weighted && part.mode == PART_TWO_REGION) {
+        double lo = part.weight[0], hi = part.weight[0];
+        for (int i = 0; i < nN; i++) {
+            lo = std::min(lo, part.weight[i]);
+            hi = std::max(hi, part.weight[i]);
+        }
+        const double cut = lo + 0.5 * (hi - lo);
+        std::vector<int> hot, cold;
+        for (int i = 0; i < nN; i++) (hi > lo && part.weight[i] >= cut ? hot : cold).push_back(i);
+        equalWeightBlocks(hot);
+        equalWeightBlocks(cold);
+    } else if (weighted) {
+        std::vector<int> all(nN);
+        std::iota(all.begin(), all.end(), 0);
+        equalWeightBlocks(all);
     } else {
         for (int i = 0; i < nN; i++)
             part.nodeOwner[i] = block > 0 ? (int)((i / block) % R) : (int)((long long)i * R / nN);

@@ -37,6 +37,7 @@ typedef int (*ExchangeFn)(double* buf, long n, int op, void* user);
 // memory, mapped with hipIpcOpenMemHandle; no collective library inside a
 // step; bootstrapped over the host callback when one is set, else over RCCL).
 enum { XCHG_RCCL = 0, XCHG_HOST = 1, XCHG_IPC = 2 };
+enum { PART_CONTIGUOUS = 0, PART_TWO_REGION = 1 };
 
 struct Partition {
     int rank = 0, nranks = 1;
@@ -49,6 +50,14 @@ struct Partition {
     // of equal node counts (swmmx_setPartitionWeights; e.g. 1 + the node's
     // measured sparse-iteration updates times their relative cost)
     std::vector<double> weight;
+    // PART_CONTIGUOUS: one contiguous block of equal weight per rank;
+    // PART_TWO_REGION (needs weights): the "hot" nodes -- weight excess over
+    // the lightest node at least half the largest excess (the surcharged band
+    // whose nodes run every sparse iteration) -- and the other nodes are each
+    // cut into nranks contiguous blocks of equal weight, rank r taking block r
+    // of both: every rank gets an equal share of the sparse work and of the
+    // full passes, at the price of a few more cut rows
+    int mode = 0;
 
     // ---- derived by buildPartition (identical on every rank) -------------
     std::vector<int> nodeOwner, linkOwner;  // global object -> rank

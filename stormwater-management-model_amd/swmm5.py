@@ -111,6 +111,7 @@ def load_library(path: str | None = None):
         "swmmx_setTransport": (c_int, [c_int]),
         "swmmx_setPartitionWeights": (c_int, [P(c_dbl), c_int]),
         "swmmx_getNodeWork": (c_int, [P(c_dbl), c_int]),
+        "swmmx_setPartitionMode": (c_int, [c_int]),
         "swmmx_getTransport": (c_int, [ctypes.c_char_p, c_int]),
         "swmmx_getOwner": (c_int, [c_int, P(c_int), c_int]),
         "swmmx_getPartition": (ctypes.c_long, [c_char_p, P(c_int), ctypes.c_long]),
@@ -391,6 +392,11 @@ class SWMM:
         a = np.ascontiguousarray(w, dtype=np.float64)
         self._pw = a
         return self.L.swmmx_setPartitionWeights(a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), a.size)
+
+    def set_partition_mode(self, mode):
+        """Partition mode (swmmx_setPartitionMode): "contiguous" (0) or "two_region" (1)."""
+        m = {"contiguous": 0, "two_region": 1}.get(mode, mode)
+        return self.L.swmmx_setPartitionMode(int(m))
 
     def node_work(self):
         """Per-node updates in iterations k >= 2 of the timed steps (owned nodes)."""

@@ -162,6 +162,57 @@ def test_weighted_partition_layout(tmp_path):
                                               S["llink"][S["sendLink"][S["sendOff"][ks]:S["sendOff"][ks + 1]]])
 
 
+def test_two_region_partition_layout(tmp_path):
+    """swmmx_setPartitionMode(1): the hot nodes (weight excess at least half
+    the largest: here the last 40 grid rows' worth, a surcharged band) and the
+    others are each cut into contiguous blocks of equal weight, rank r taking
+    block r of both -- every rank owns an equal share of the band and of the
+    rest; the layout keeps every held node's conduits in global order."""
+    inp = _grid(tmp_path, 24, 20)
+    d = _topology(inp, tmp_path)
+    n1, n2 = d["link.node1"].astype(int), d["link.node2"].astype(int)
+    nN = len(d["node.type"])
+    junction = d["node.type"].astype(int) != 1
+    w = np.ones(nN)
+    band = np.arange(nN) >= nN - 1 - 4 * 20          # the last four rows (and the outfall)
+    w[band] = 7.0
+    w[band & (np.arange(nN) % 3 == 0)] = 6.0         # uneven inside the band: still >= the cut (4.0)
+    rows = _incident(n1, n2, nN)
+    for world in (2, 3):
+        lays, owner = [], None
+        for r in range(world):
+            s = swmm5.SWMM()
+            s.set_partition(r, world)
+            s.set_partition_weights(w)
+            assert s.set_partition_mode("two_region") == 0
+            try:
+                assert s.open(inp, str(tmp_path / "w.rpt"), str(tmp_path / "w.out")) == 0
+                owner = s.owners(swmm5.NODE)
+                lays.append({k: s.partition_array(k) for k in ("lnode", "llink", "lghost", "rowptr", "csr")})
+            finally:
+                s.close()
+                s.set_partition_mode("contiguous")
+                s.set_partition_weights(None)
+                s.set_partition(0, 1)
+        # reference: each region in equal-weight contiguous blocks (midpoint rule)
+        ref = np.zeros(nN, dtype=int)
+        for sel in (band, ~band):
+            idx = np.nonzero(sel)[0]
+            ww = w[idx]
+            mid = np.cumsum(ww) - 0.5 * ww
+            ref[idx] = np.minimum((mid * world / ww.sum()).astype(int), world - 1)
+        np.testing.assert_array_equal(owner[junction], ref[junction])
+        hot = np.bincount(owner[band & junction], minlength=world)
+        cold = np.bincount(owner[~band & junction], minlength=world)
+        assert hot.max() - hot.min() <= 2 and cold.max() - cold.min() <= 2, (hot, cold)
+        for r, L in enumerate(lays):
+            loc = np.concatenate([L["llink"], L["lghost"]])
+            rp, csr = L["rowptr"], L["csr"]
+            for i, g in enumerate(L["lnode"]):
+                got = [(int(loc[e & 0x7FFFFFFF]), int((e >> 31) & 1)) for e in csr[rp[i]:rp[i + 1]]]
+                assert got == rows[g], (r, g)
+
+
 def _incident(n1, n2, nN):
     rows = [[] for _ in range(nN)]
     for j in range(len(n1)):
@@ -482,7 +533,7 @@ def _grid_with_regulators(tmp_path, n=20):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,block,pollutants,transport", [
     (2, 0, 0, "host"), (3, 0, 0, "host"), (2, 90, 0, "host"), (3, 60, 0, "host"), (2, 0, 2, "host"),
-    (2, 0, 0, "ipc"), (3, 60, 0, "ipc"), (2, 0, 2, "ipc"), (3, -1, 0, "ipc")])
+    (2, 0, 0, "ipc"), (3, 60, 0, "ipc"), (2, 0, 2, "ipc"), (3, -1, 0, "ipc"), (3, -2, 0, "ipc")])
 def test_ranks_list_graph_bitwise(world, block, pollutants, transport, tmp_path):
     """The list graph (iterations k >= 2 as unconverged-list walks and
     live-list node passes, each followed by the neighbour exchange and the
@@ -490,13 +541,17 @@ def test_ranks_list_graph_bitwise(world, block, pollutants, transport, tmp_path)
     bitwise equal to one GPU's (which runs it too) -- the surcharged,
     non-converging 30 x 30 grid, host transport; with row strips and with
     node blocks dealt to the ranks in turn (SWMM5_PART_BLOCK: 3 and 2 grid
-    rows per block, every rank holding part of the surcharged corner); and
+    rows per block, every rank holding part of the surcharged corner); with
+    node weights (contiguous blocks of equal weight, and two regions each cut
+    into equal-weight blocks: every rank holds two separate stretches); and
     with two pollutants (the frozen junctions' final depths then come from the
     quality kernel, after the ghost links' concentrations moved)."""
     inp = _grid(tmp_path, 30, 30, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.5, pollutants=pollutants)
     env = {"SWMM5_SPARSE": "3", "SWMM5_PART_BLOCK": str(max(block, 0))}
     if block < 0:                         # a weighted partition (node weights 1 .. 4, swmmx_setPartitionWeights)
         env.update(WORKER_WEIGHTS="ramp", WORKER_NODES=str(30 * 30 + 1))
+    if block == -2:                       # two regions: the heavier half and the rest, each cut in three
+        env.update(WORKER_PARTMODE="two_region")
     one = _run_workers(inp, 250, tmp_path, 1, "host", "one", extra_env=env)[0]
     st, its, nonconv = one["counters"]
     assert nonconv > 10 and its / st > 2.5, one["counters"]

@@ -21,6 +21,7 @@ for s in $STEPS; do
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pytest) run pytest_gpu 900 python -u -m pytest tests -v -m gpu --maxfail=5 -p no:cacheprovider --timeout 600 --timeout-method thread ;;
     bench)  run bench 600 python bench.py ;;
+    benchdrv) for i in 1 2; do run benchdrv_$i 600 python bench.py --steps 20 --warmup 5; done ;;
     benchq)  run benchq 600 python bench.py --steps 200 --no-cpu ;;
     tailab) for t in 0 1; do SWMM5_TAIL=$t run bench_tail$t 600 python bench.py --steps 200 --no-cpu; SWMM5_TAIL=$t run bench100k_tail$t 600 python bench.py --config 100k --steps 400 --no-cpu; done ;;
     bench100k) run bench100k 600 python bench.py --config 100k --steps 400 --no-cpu ;;
@@ -42,6 +43,14 @@ for s in $STEPS; do
          done ;;
     trace2) # kernel traces of both ranks of a small 2-rank IPC run (tools/mrank_launch.py: one rocprofv3 per rank)
            rm -rf gpurun_out/trace2 && run trace2 300 python tools/mrank_launch.py --np 2 --prof gpurun_out/trace2 -- bench.py --gpus 2 --grid ${SGRID:-24} --spinup 0 --steps 100 --warmup 10 --exchange ${XCH:-ipc} --no-cpu --no-stream --kernel-reps 0 --timing-steps 2 ;;
+    sigq) # the 2-rank IPC run on this one GPU with fewer hardware queues per process
+           for q in ${HWQ:-1 2}; do
+             GPU_MAX_HW_QUEUES=$q run sigq_$q 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $((29400 + RANDOM % 100)) bench.py --gpus 2 --grid ${SGRID:-24} --spinup 0 --steps 400 --warmup 20 --exchange ${XCH:-ipc} --no-cpu --no-stream --kernel-reps 0
+           done ;;
+    sigx) # fused (k_ipc_xchg) against split (k_ipc_pack + k_ipc_unpack) exchanges, 2 ranks on this GPU
+           for f in 1 0; do
+             SWMM5_XCHG_FUSED=$f GPU_MAX_HW_QUEUES=${HWQ:-2} run sigx_$f 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $((29400 + RANDOM % 100)) bench.py --gpus 2 --grid ${SGRID:-24} --spinup 0 --steps 400 --warmup 20 --exchange ipc --no-cpu --no-stream --kernel-reps 0
+           done ;;
     sigprobe) # the IPC signalling alone (tools/ipc_signal_probe.hip): two ranks on two streams of one
            # process, then two processes on this one device
            run sigprobe_thread 60 ./tools/ipc_signal_probe \
@@ -62,7 +71,7 @@ for s in $STEPS; do
            done
            cp profiles/partition_weights.json gpurun_out/ ;;
     balance) # the 2-rank 4M rehearsal on this GPU: equal strips against weighted blocks (per_rank_sparse_work)
-           for bal in off auto; do
+           for bal in ${BALS:-off auto}; do
              run balance_$bal 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${NP:-2} --master-addr 127.0.0.1 --master-port $((29700 + RANDOM % 200)) bench.py --gpus ${NP:-2} --config ${CFG:-4m} --steps 10 --warmup 2 --timing-steps 4 --exchange ${XCH:-ipc} --balance $bal --no-cpu --no-stream --kernel-reps 0
            done ;;
     blocks) # the 2-rank 4M rehearsal with node blocks dealt in turn (shared nodes freeze since round 6)
