@@ -121,9 +121,10 @@ def workload_name(config, cfg, rows):
 def partition_weights(workload, rows, nx, n_nodes, lam=None):
     """Per-node weights from profiles/partition_weights.json (tools/
     calibrate_partition.py: the workload's per-row sparse node updates per
-    step measured on one GPU, and the marginal cost of a sparse update
-    relative to a full-pass node): node i of row r weighs 1 + lambda u_r / nx
-    (lam overrides the record's lambda), the outfall 1.  None when no record
+    step measured on one GPU -- node updates plus the updates of the
+    conduits whose node1 lies in the row -- and the marginal cost of a sparse
+    update relative to a full-pass node): node i of row r weighs
+    1 + lambda u_r / nx (lam overrides the record's lambda), the outfall 1.  None when no record
     matches this grid."""
     path = os.path.join(ROOT, "profiles", "partition_weights.json")
     if not os.path.exists(path):
@@ -134,6 +135,8 @@ def partition_weights(workload, rows, nx, n_nodes, lam=None):
     import numpy as np
     w = np.ones(n_nodes)
     ru = np.asarray(rec["row_updates"], dtype=np.float64)
+    if "row_conduit_updates" in rec:          # + the conduits' updates, charged to their node1 (their owner)
+        ru = ru + np.asarray(rec["row_conduit_updates"], dtype=np.float64)
     w[:rows * nx] = 1.0 + (rec["lambda"] if lam is None else lam) * np.repeat(ru / nx, nx)
     return w, rec
 

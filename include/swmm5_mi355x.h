@@ -156,10 +156,11 @@ int    DLLEXPORT swmmx_setPartitionWeights(const double *w, int n);
  * contiguous block of equal weight per rank (the default); 1 two regions --
  * the "hot" nodes (weight excess over the lightest node at least half the
  * largest excess: e.g. the surcharged band whose nodes run every sparse
- * Picard iteration) and the other nodes are each cut into nranks contiguous
- * blocks of equal weight, rank r taking block r of both, so every rank gets
- * an equal share of the sparse work and of the full passes.  Returns 0 or 500
- * for an unknown mode. */
+ * Picard iteration) are cut into 2 nranks contiguous blocks of equal weight
+ * dealt to ranks 0, 1, .., nranks-1, nranks-1, .., 0, the other nodes into
+ * nranks blocks (rank r takes block r), so every rank gets an equal share of
+ * the sparse work and of the full passes.  Returns 0 or 500 for an unknown
+ * mode. */
 int    DLLEXPORT swmmx_setPartitionMode(int mode);
 
 /* Per node (global order, owned nodes of this rank; 0 elsewhere): its updates
@@ -167,6 +168,10 @@ int    DLLEXPORT swmmx_setPartitionMode(int mode);
  * the measured sparse work a weighted partition balances.  Returns the node
  * count or -1. */
 int    DLLEXPORT swmmx_getNodeWork(double *out, int n);
+
+/* Same layout: per node, the updates in iterations k >= 2 (list walks) of the
+ * conduits whose node1 it is -- a conduit's owner follows its node1. */
+int    DLLEXPORT swmmx_getConduitWork(double *out, int n);
 
 /* Owning rank of every node (objType swmm_NODE) or link (swmm_LINK) under the
  * current partition; returns the object count. */

@@ -1294,6 +1294,14 @@ int DLLEXPORT swmmx_getNodeWork(double* out, int n)
     return G->prj->net.nNodes();
 }
 
+int DLLEXPORT swmmx_getConduitWork(double* out, int n)
+{
+    if (!G || !G->router || !G->router->ok() || !out) return -1;
+    for (int i = 0; i < n; i++) out[i] = 0.0;
+    if (G->router->nodeWork(out, n, true)) return -1;
+    return G->prj->net.nNodes();
+}
+
 int DLLEXPORT swmmx_setTransport(int kind)
 {
     if (kind < XCHG_RCCL || kind > XCHG_IPC) return 500;

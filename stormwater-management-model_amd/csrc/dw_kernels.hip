@@ -333,6 +333,7 @@ struct Params {
     int multi;                    // partitioned (multi-GPU) run
     int countWork;                // timing mode: count updated conduits per iteration
     unsigned* nodeWork;           // timing mode: per node, its updates in iterations k >= 2 (partition weights)
+    unsigned* nodeLinkWork;       // timing mode: per node, updates in iterations k >= 2 of the conduits it is node1 of
     // multi-GPU exchange (partition.h): link arrays hold this rank's owned
     // links [0, nL) and its ghost links [nL, nLs) (other ranks' links touching
     // a held node).  Each iteration k_xpack packs the owned links other ranks
@@ -1251,6 +1252,7 @@ __device__ __forceinline__ int linkListWalk(const Params& p, int k, int cnt, dou
             p.dirty[nn.x] = 1;                        // their sums are stale
             p.dirty[nn.y] = 1;
             if (kWake) sparseWake(p, f1 != 0, nn.x, f2 != 0, nn.y, wake);
+            if (p.countWork) atomicAdd(&p.nodeLinkWork[nn.x], 1u);   // measurement only
             work++;
         }
     }
@@ -1408,6 +1410,7 @@ __device__ __forceinline__ int coldConduitsS(const Params& p, int k, double dt, 
         conduitFlow<kFirst, true>(p, j, f, nn, k, dt, ct, y1, y2);
         if (k >= 2) { p.dirty[nn.x] = 1; p.dirty[nn.y] = 1; }
         if (kWake) sparseWake(p, f1 != 0, nn.x, f2 != 0, nn.y, wake);
+        if (k >= 2 && p.countWork) atomicAdd(&p.nodeLinkWork[nn.x], 1u);   // measurement only
         work++;
     }
     return work;
@@ -2755,6 +2758,7 @@ __device__ __forceinline__ double llDouble(unsigned lo, unsigned hi)
 {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+constexpr int kMaxXF = 6;         // values per ghost link: flow, 2 surface areas, dq/dh (+ evaporation, seepage)
 // The owner's side: this rank's sent links' values, as granules, into each
 // receiving rank's ghost area (threads tid, tid + nthr, ... of the sends)
 template <bool kQual>
@@ -2795,10 +2799,12 @@ __device__ bool ipcUnpack(const Params& p, int k, int tid, int nthr)
     for (int g = tid; g < p.nGhost; g += nthr) {
         const int l = p.nL + g;
         bool ch = false;
-        for (int f = 0; f < F; f++) {
-            unsigned lo = 0, hi = 0;
-            if (!llWait(p, b + (size_t)(2 * f) * nG + g, seq, &lo, t0) ||
-                !llWait(p, b + (size_t)(2 * f + 1) * nG + g, seq, &hi, t0)) {
+        // value f of the ghost from its two granules (a, c: as loaded; a
+        // granule that has not arrived yet is polled); false at a give-up
+        auto take = [&](int f, unsigned long long a, unsigned long long c) -> bool {
+            unsigned lo = (unsigned)a, hi = (unsigned)c;
+            if (((unsigned)(a >> 32) != seq && !llWait(p, b + (size_t)(2 * f) * nG + g, seq, &lo, t0)) ||
+                ((unsigned)(c >> 32) != seq && !llWait(p, b + (size_t)(2 * f + 1) * nG + g, seq, &hi, t0))) {
                 xFail(p, kQual ? XK_QUAL : XK_GHOST, p.ghostFrom[g], seq);
                 return false;
             }
@@ -2815,7 +2821,19 @@ __device__ bool ipcUnpack(const Params& p, int k, int tid, int nthr)
             else if (f == 3) p.dqdh[l] = v;
             else if (f == 4) p.evapLoss[l] = v;
             else p.seepLoss[l] = v;
-        }
+            return true;
+        };
+        // the first kMaxXF values' granules in flight at once (independent
+        // uncached loads), so a ghost costs one memory round trip, not 2F
+        unsigned long long w[2 * kMaxXF];
+#pragma unroll
+        for (int q = 0; q < 2 * kMaxXF; q++) w[q] = q < 2 * F ? llLoad(b + (size_t)q * nG + g) : 0ull;
+#pragma unroll
+        for (int f = 0; f < kMaxXF; f++)
+            if (f < F && !take(f, w[2 * f], w[2 * f + 1])) return false;
+        for (int f = kMaxXF; f < F; f++)                 // more pollutants than that
+            if (!take(f, llLoad(b + (size_t)(2 * f) * nG + g), llLoad(b + (size_t)(2 * f + 1) * nG + g)))
+                return false;
         if (ch) ghostWake(p, l, k);
     }
     return true;
@@ -4353,6 +4371,16 @@ static int flagExchangeImpl(Router::Impl* d, int k)
 // pack, transfer, unpack on the RCCL / host transports; on XCHG_IPC the owners
 // store them straight into this rank's ghost area and k_ipc_unpack waits for
 // them.  qualExchange: the ghost links' concentrations, once per step.
+// Grid of a kernel that waits for the peers (k_ipc_unpack): at most
+// kXchgGrid workgroups, so that its waiting waves never fill the GPU -- with
+// several ranks on one device a full-grid waiter kept the peer's own kernels
+// off the CUs it was waiting for (a 2-rank run with 4-row node blocks timed
+// out) -- and no more than the ghosts need
+static int waitGrid(const Router::Impl* d)
+{
+    const int need = (d->p.nGhost + kBlock - 1) / kBlock;
+    return std::max(1, std::min(std::min(d->gridX, kXchgGrid), need));
+}
 static int ghostExchangeImpl(Router::Impl* d, int k);
 static int ghostExchange(Router::Impl* d, int k)
 {
@@ -4370,7 +4398,7 @@ static int ghostExchangeImpl(Router::Impl* d, int k)
             hipLaunchKernelGGL(k_ipc_xchg<false>, dim3(kXchgGrid), dim3(kBlock), 0, d->stream, p, k);
         else {
             if (p.nSend) hipLaunchKernelGGL(k_ipc_pack<false>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
-            if (p.nGhost) hipLaunchKernelGGL(k_ipc_unpack<false>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, k);
+            if (p.nGhost) hipLaunchKernelGGL(k_ipc_unpack<false>, dim3(waitGrid(d)), dim3(kBlock), 0, d->stream, p, k);
         }
         return 0;
     }
@@ -4387,7 +4415,7 @@ static int qualExchange(Router::Impl* d)
             hipLaunchKernelGGL(k_ipc_xchg<true>, dim3(kXchgGrid), dim3(kBlock), 0, d->stream, p, 0);
         else {
             if (p.nSend) hipLaunchKernelGGL(k_ipc_pack<true>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, 0);
-            if (p.nGhost) hipLaunchKernelGGL(k_ipc_unpack<true>, dim3(d->gridX), dim3(kBlock), 0, d->stream, p, 0);
+            if (p.nGhost) hipLaunchKernelGGL(k_ipc_unpack<true>, dim3(waitGrid(d)), dim3(kBlock), 0, d->stream, p, 0);
         }
         return 0;
     }
@@ -5271,6 +5299,8 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         if (e == hipSuccess) e = hipMemset(p.dirty, 0, std::max<size_t>(nN, 1));
         if (e == hipSuccess) p.nodeWork = devAlloc<unsigned>(d, nN, &e);
         if (e == hipSuccess) e = hipMemset(p.nodeWork, 0, std::max<size_t>(nN, 1) * sizeof(unsigned));
+        if (e == hipSuccess) p.nodeLinkWork = devAlloc<unsigned>(d, nN, &e);
+        if (e == hipSuccess) e = hipMemset(p.nodeLinkWork, 0, std::max<size_t>(nN, 1) * sizeof(unsigned));
         if (e != hipSuccess) { fail(hipGetErrorString(e)); return err_; }
         p.frz = devAlloc<unsigned char>(d, nN, &e);
         if (e == hipSuccess) e = hipMemset(p.frz, 0, std::max<size_t>(nN, 1));
@@ -6520,8 +6550,10 @@ void Router::setTiming(bool on)
     }
     d_->timing = on;
     if (!on) d_->curX = nullptr;
-    if (on && d_->p.nodeWork)                      // the per-node work of the steps timed from now on
+    if (on && d_->p.nodeWork) {                    // the per-node work of the steps timed from now on
         (void)hipMemsetAsync(d_->p.nodeWork, 0, std::max<size_t>(d_->p.nN, 1) * sizeof(unsigned), d_->stream);
+        (void)hipMemsetAsync(d_->p.nodeLinkWork, 0, std::max<size_t>(d_->p.nN, 1) * sizeof(unsigned), d_->stream);
+    }
     d_->p.countWork = on ? 1 : 0;                  // eager launches only; the graph keeps 0
     for (int k = 0; k < Impl::kClasses; k++) { d_->kms[k] = 0; d_->kcnt[k] = 0; d_->kbytesSum[k] = 0; }
     d_->workSum = 0;
@@ -6838,14 +6870,15 @@ int Router::packResults(double f, double uL, double uV, double uQ, const float**
 
 const Partition& Router::partition() const { return d_->part; }
 
-int Router::nodeWork(double* out, int n)
+int Router::nodeWork(double* out, int n, bool conduits)
 {
     auto fail = [&](const std::string& m) { err_ = 500; errMsg_ = "ERROR 500: GPU router: " + m; };
     Impl* d = d_;
     flushTiming(d);
     std::vector<unsigned> w((size_t)std::max(d->p.nN, 1));
     WAITCHECK(waitDone(d_, nullptr));
-    HIPCHECK(hipMemcpy(w.data(), d->p.nodeWork, w.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(w.data(), conduits ? d->p.nodeLinkWork : d->p.nodeWork, w.size() * sizeof(unsigned),
+                       hipMemcpyDeviceToHost));
     const Partition& part = d->part;
     for (int i = 0; i < d->p.nN; i++) {
         const int g = part.active() ? part.lnode[i] : i;

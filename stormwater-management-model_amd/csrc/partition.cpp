@@ -42,9 +42,10 @@ int buildPartition(const Network& net, Partition& part, std::string* msg)
     long long block = 0;
     if (const char* b = getenv("SWMM5_PART_BLOCK")) block = atoll(b);
     const bool weighted = block <= 0 && (int)part.weight.size() == nN && nN > 0;
-    // node i of `idx` (ascending node order) goes to the rank whose equal
-    // share of the list's total weight holds the midpoint of its interval
-    auto equalWeightBlocks = [&](const std::vector<int>& idx) {
+    // the nodes of `idx` (ascending node order) cut into nb contiguous blocks
+    // of equal weight (node i to the block whose share holds the midpoint of
+    // its weight interval); block b goes to rank rankOf(b)
+    auto equalWeightBlocks = [&](const std::vector<int>& idx, int nb, auto rankOf) {
         double total = 0.0;
         for (int i : idx) total += std::max(part.weight[i], 0.0);
         double run = 0.0;
@@ -53,10 +54,11 @@ int buildPartition(const Network& net, Partition& part, std::string* msg)
             const double w = std::max(part.weight[idx[q]], 0.0);
             const double mid = run + 0.5 * w;
             run += w;
-            int r = total > 0.0 ? (int)(mid * R / total) : (int)(q * R / m);
-            part.nodeOwner[idx[q]] = std::min(std::max(r, 0), R - 1);
+            int b = total > 0.0 ? (int)(mid * nb / total) : (int)(q * nb / m);
+            part.nodeOwner[idx[q]] = rankOf(std::min(std::max(b, 0), nb - 1));
         }
     };
+    auto same = [](int b) { return b; };
     if (weighted && part.mode == PART_TWO_REGION) {
         double lo = part.weight[0], hi = part.weight[0];
         for (int i = 0; i < nN; i++) {
@@ -66,12 +68,15 @@ int buildPartition(const Network& net, Partition& part, std::string* msg)
         const double cut = lo + 0.5 * (hi - lo);
         std::vector<int> hot, cold;
         for (int i = 0; i < nN; i++) (hi > lo && part.weight[i] >= cut ? hot : cold).push_back(i);
-        equalWeightBlocks(hot);
-        equalWeightBlocks(cold);
+        // the hot region in 2R blocks dealt 0, 1, .., R-1, R-1, .., 1, 0: a
+        // trend of the work across the region (the surcharge front at its
+        // upstream edge) cancels between each rank's two blocks
+        equalWeightBlocks(hot, 2 * R, [R](int b) { return b < R ? b : 2 * R - 1 - b; });
+        equalWeightBlocks(cold, R, same);
     } else if (weighted) {
         std::vector<int> all(nN);
         std::iota(all.begin(), all.end(), 0);
-        equalWeightBlocks(all);
+        equalWeightBlocks(all, R, same);
     } else {
         for (int i = 0; i < nN; i++)
             part.nodeOwner[i] = block > 0 ? (int)((i / block) % R) : (int)((long long)i * R / nN);

@@ -53,10 +53,12 @@ struct Partition {
     // PART_CONTIGUOUS: one contiguous block of equal weight per rank;
     // PART_TWO_REGION (needs weights): the "hot" nodes -- weight excess over
     // the lightest node at least half the largest excess (the surcharged band
-    // whose nodes run every sparse iteration) -- and the other nodes are each
-    // cut into nranks contiguous blocks of equal weight, rank r taking block r
-    // of both: every rank gets an equal share of the sparse work and of the
-    // full passes, at the price of a few more cut rows
+    // whose nodes run every sparse iteration) -- are cut into 2 nranks
+    // contiguous blocks of equal weight dealt 0, 1, .., R-1, R-1, .., 0 (a
+    // trend across the band cancels between a rank's two blocks), the other
+    // nodes into nranks blocks, rank r taking block r: every rank gets an
+    // equal share of the sparse work and of the full passes, at the price of
+    // a few more cut rows
     int mode = 0;
 
     // ---- derived by buildPartition (identical on every rank) -------------

@@ -107,8 +107,10 @@ public:
     // updates, k_link ms, k_node ms; returns the number of values available
     int iterationStats(double* out, int n);
     // per global node (owned ones; out[] untouched elsewhere): its updates in
-    // Picard iterations k >= 2 of the steps timed since setTiming(true)
-    int nodeWork(double* out, int n);
+    // Picard iterations k >= 2 of the steps timed since setTiming(true), or
+    // (conduits) the updates of the conduits it is node1 of (their owner
+    // follows node1) in those iterations
+    int nodeWork(double* out, int n, bool conduits = false);
     std::string deviceName() const { return devName_; }
     // the multi-GPU transport in use ("single", "rccl", "host", "ipc", or a
     // fallback note)

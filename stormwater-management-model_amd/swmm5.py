@@ -111,6 +111,7 @@ def load_library(path: str | None = None):
         "swmmx_setTransport": (c_int, [c_int]),
         "swmmx_setPartitionWeights": (c_int, [P(c_dbl), c_int]),
         "swmmx_getNodeWork": (c_int, [P(c_dbl), c_int]),
+        "swmmx_getConduitWork": (c_int, [P(c_dbl), c_int]),
         "swmmx_setPartitionMode": (c_int, [c_int]),
         "swmmx_getTransport": (c_int, [ctypes.c_char_p, c_int]),
         "swmmx_getOwner": (c_int, [c_int, P(c_int), c_int]),
@@ -398,15 +399,19 @@ class SWMM:
         m = {"contiguous": 0, "two_region": 1}.get(mode, mode)
         return self.L.swmmx_setPartitionMode(int(m))
 
-    def node_work(self):
-        """Per-node updates in iterations k >= 2 of the timed steps (owned nodes)."""
+    def node_work(self, conduits: bool = False):
+        """Per-node updates in iterations k >= 2 of the timed steps (owned
+        nodes); conduits: the updates of the conduits each node is node1 of."""
         import numpy as np
         n = self.getCount(NODE)
         a = np.zeros(max(n, 1))
-        self.L.swmmx_getNodeWork(a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n)
+        fn = self.L.swmmx_getConduitWork if conduits else self.L.swmmx_getNodeWork
+        fn(a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n)
         return a[:n]
 
     def transport(self) -> str:
+        if not hasattr(self.L, "swmmx_getTransport"):     # an older build (SWMM5_LIB A/B runs)
+            return "single"
         buf = ctypes.create_string_buffer(256)
         self.L.swmmx_getTransport(buf, 256)
         return buf.value.decode()

@@ -164,10 +164,11 @@ def test_weighted_partition_layout(tmp_path):
 
 def test_two_region_partition_layout(tmp_path):
     """swmmx_setPartitionMode(1): the hot nodes (weight excess at least half
-    the largest: here the last 40 grid rows' worth, a surcharged band) and the
-    others are each cut into contiguous blocks of equal weight, rank r taking
-    block r of both -- every rank owns an equal share of the band and of the
-    rest; the layout keeps every held node's conduits in global order."""
+    the largest: here the last four grid rows, a surcharged band) are cut into
+    2 x ranks contiguous blocks of equal weight dealt 0, 1, .., 1, 0, the
+    others into one block per rank -- every rank owns an equal share of the
+    band and of the rest; the layout keeps every held node's conduits in
+    global order."""
     inp = _grid(tmp_path, 24, 20)
     d = _topology(inp, tmp_path)
     n1, n2 = d["link.node1"].astype(int), d["link.node2"].astype(int)
@@ -194,13 +195,15 @@ def test_two_region_partition_layout(tmp_path):
                 s.set_partition_mode("contiguous")
                 s.set_partition_weights(None)
                 s.set_partition(0, 1)
-        # reference: each region in equal-weight contiguous blocks (midpoint rule)
+        # reference: the band in 2 x world equal-weight blocks dealt
+        # 0, 1, .., world-1, world-1, .., 0; the rest in world blocks
         ref = np.zeros(nN, dtype=int)
-        for sel in (band, ~band):
+        for sel, nb in ((band, 2 * world), (~band, world)):
             idx = np.nonzero(sel)[0]
             ww = w[idx]
             mid = np.cumsum(ww) - 0.5 * ww
-            ref[idx] = np.minimum((mid * world / ww.sum()).astype(int), world - 1)
+            b = np.minimum((mid * nb / ww.sum()).astype(int), nb - 1)
+            ref[idx] = np.where(b < world, b, 2 * world - 1 - b) if nb == 2 * world else b
         np.testing.assert_array_equal(owner[junction], ref[junction])
         hot = np.bincount(owner[band & junction], minlength=world)
         cold = np.bincount(owner[~band & junction], minlength=world)

@@ -41,6 +41,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "stormwater-management-model_amd"))
 
+os.environ.setdefault("SWMM5_SPARSE", "3")   # the list graph, as every rank of a partitioned run
 import bench  # noqa: E402
 import swmm5  # noqa: E402
 
@@ -74,7 +75,7 @@ def main():
         """Time --steps steps: per-iteration stats, kernel times, node work."""
         s.set_timing(True)
         assert s.run_steps(args.steps)[0] == 0, s.getError()
-        out = (s.kernel_times(), s.iteration_stats(), s.node_work(), s.counters())
+        out = (s.kernel_times(), s.iteration_stats(), s.node_work(), s.counters(), s.node_work(conduits=True))
         s.set_timing(False)
         return out
 
@@ -88,13 +89,14 @@ def main():
 
     early = int(args.early_frac * spinup)
     assert s.run_steps(early)[0] == 0, s.getError()
-    _, itsA, _, _ = window()
+    _, itsA, _, _, _ = window()
     assert s.run_steps(max(spinup - early - args.steps, 0) + args.warmup)[0] == 0, s.getError()
-    kt, its, nw, c = window()
+    kt, its, nw, c, cw = window()
     s.end()
     s.close()
     nN = nw.size
     row_updates = nw[:rows * nx].reshape(rows, nx).sum(axis=1) / args.steps
+    row_conduit_updates = cw[:rows * nx].reshape(rows, nx).sum(axis=1) / args.steps
     uA, tA, _ = sparse(itsA)
     uB, tB, nB = sparse(its)
     reliable = uB - uA > 0.1 * max(uB, 1.0) and tB > tA
@@ -114,6 +116,7 @@ def main():
            "lambda": (b / c_node_us) if c_node_us > 0 else 0.0,
            "sparse_updates_per_step": float(row_updates.sum()),
            "row_updates": [round(float(x), 3) for x in row_updates],
+           "row_conduit_updates": [round(float(x), 3) for x in row_conduit_updates],
            "backend": backend,
            "source": "tools/calibrate_partition.py --config %s --gpus %d --steps %d" % (args.config, args.gpus,
                                                                                        args.steps)}
@@ -121,7 +124,7 @@ def main():
     db[key] = rec
     with open(OUT, "w") as f:
         json.dump(db, f, indent=1)
-    print(json.dumps({k: v for k, v in rec.items() if k != "row_updates"}))
+    print(json.dumps({k: v for k, v in rec.items() if not k.startswith("row_")}))
 
 
 if __name__ == "__main__":

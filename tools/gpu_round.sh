@@ -26,7 +26,7 @@ for s in $STEPS; do
     tailab) for t in 0 1; do SWMM5_TAIL=$t run bench_tail$t 600 python bench.py --steps 200 --no-cpu; SWMM5_TAIL=$t run bench100k_tail$t 600 python bench.py --config 100k --steps 400 --no-cpu; done ;;
     bench100k) run bench100k 600 python bench.py --config 100k --steps 400 --no-cpu ;;
     benchall) for c in 100k 1m_fixed 1m_quality; do run bench_$c 600 python bench.py --config $c --no-cpu; done ;;
-    prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu ;;
+    prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu ${BARGS:-} ;;
     benchqual) run benchqual 600 python bench.py --config 1m_quality --steps 200 --no-cpu ;;
     bench4m) run bench4m 900 python bench.py --config 4m --steps 100 ;;
     mrehearse4m) run mrehearse4m 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --config 4m --steps 10 --warmup 2 --spinup 20 --exchange host --no-cpu ;;
@@ -51,9 +51,13 @@ for s in $STEPS; do
            for f in 1 0; do
              SWMM5_XCHG_FUSED=$f GPU_MAX_HW_QUEUES=${HWQ:-2} run sigx_$f 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $((29400 + RANDOM % 100)) bench.py --gpus 2 --grid ${SGRID:-24} --spinup 0 --steps 400 --warmup 20 --exchange ipc --no-cpu --no-stream --kernel-reps 0
            done ;;
+    ablib) # the same bench against older builds of the engine (ab/*.so via SWMM5_LIB), interleaved
+           for rep in 1 2; do for l in ${ABLIBS:-r05 head}; do
+             SWMM5_LIB=$PWD/ab/libswmm5_$l.so run ablib_${l}_$rep 300 python bench.py --no-cpu --kernel-reps 0 ${BARGS:---steps 20 --warmup 5}
+           done; done ;;
     sigprobe) # the IPC signalling alone (tools/ipc_signal_probe.hip): two ranks on two streams of one
            # process, then two processes on this one device
-           run sigprobe_thread 60 ./tools/ipc_signal_probe \
+           for g in ${SGRAN:-22624}; do run sigprobe_thread_$g 60 ./tools/ipc_signal_probe thread $g || break; done \
            && rm -rf gpurun_out/sigp && mkdir -p gpurun_out/sigp \
            && run sigprobe_proc 120 bash -c './tools/ipc_signal_probe proc 0 gpurun_out/sigp > gpurun_out/sigprobe_p0.txt 2>&1 & ./tools/ipc_signal_probe proc 1 gpurun_out/sigp > gpurun_out/sigprobe_p1.txt 2>&1; s1=$?; wait $!; s0=$?; cat gpurun_out/sigprobe_p0.txt gpurun_out/sigprobe_p1.txt; exit $((s0 | s1))' ;;
     rcclprobe) # the captured RCCL call pattern on one rank (tools/rccl_capture_probe.cpp), phase by phase,

@@ -12,9 +12,9 @@
 //   fused: work, xchg, work, flag     (pack and unpack in one launch)
 // The cost of the signalling is (variant - base) / N per iteration.
 //
-//   thread mode (default): one process, the two ranks on two HIP streams of
+//   thread mode (default, `ipc_signal_probe thread G`): one process, the two ranks on two HIP streams of
 //     one device (concurrent hardware queues of one process);
-//   proc mode: `ipc_signal_probe proc R DIR` for R = 0, 1 started together,
+//   proc mode: `ipc_signal_probe proc R DIR [G]` for R = 0, 1 started together,
 //     two processes on the same device, regions exchanged through
 //     hipIpcGetMemHandle / hipIpcOpenMemHandle (files in DIR), as the engine
 //     does with one process per rank.
@@ -162,7 +162,9 @@ int main(int argc, char** argv)
     const int rank = proc && argc > 2 ? atoi(argv[2]) : 0;
     const char* dir = proc && argc > 3 ? argv[3] : "/tmp";
     const int N = 50, reps = 20;
-    const int G = 4 * 2 * 2828;                   // a 4M strip boundary: 2828 links x 4 values x 2 granules
+    // ghost granules per rank per exchange; default a 4M strip boundary:
+    // 2828 links x 4 values x 2 granules (thread mode: argv[2]; proc: argv[4])
+    const int G = proc ? (argc > 4 ? atoi(argv[4]) : 4 * 2 * 2828) : (argc > 2 ? atoi(argv[2]) : 4 * 2 * 2828);
     const int grid = 64;
     const int nr = proc ? 1 : 2;                  // ranks driven by this process
     Side s[2];
