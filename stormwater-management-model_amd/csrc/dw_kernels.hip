@@ -3972,12 +3972,15 @@ struct Router::Impl {
     int* xerrHost = nullptr;
     int* hostAbortH = nullptr;
     double xTimeoutSec = 60.0;       // SWMM5_XCHG_TIMEOUT: bound of every wait behind an exchange
-    // SWMM5_XCHG_FUSED=1: k_ipc_xchg (pack and unpack in one launch) instead of
-    // k_ipc_pack + k_ipc_unpack.  Off by default: alone (tools/ipc_signal_probe)
-    // it saves a kernel boundary per exchange, but with two ranks time-sharing
-    // one GPU its waiting workgroup held the other rank's kernels back (147
-    // against 17 us per exchange)
+    // k_ipc_xchg (pack and unpack in one launch) instead of k_ipc_pack +
+    // k_ipc_unpack: one kernel boundary less per exchange (tools/
+    // ipc_signal_probe), but with ranks time-sharing one GPU its waiting
+    // workgroups held the other rank's kernels back (147 against 17 us per
+    // exchange).  So it is chosen when every rank drives
+    // a GPU of its own (setupIpc compares the ranks' PCI addresses);
+    // SWMM5_XCHG_FUSED=0/1 forces either
     bool xchgFused = false;
+    int xchgFusedEnv = -1;
     std::string transportName = "single";
     float *resN = nullptr, *resL = nullptr;          // packed period results (device)
     float *resNHost = nullptr, *resLHost = nullptr;  // pinned copies
@@ -4652,9 +4655,10 @@ static int setupIpc(Router::Impl* d)
     hipIpcMemHandle_t h{};
     ok = ok && hipIpcGetMemHandle(&h, d->ipcBase) == hipSuccess;
     (void)hipGetLastError();
-    // record per rank: 64 handle bytes, ok, nGhost, then per sender rank the
-    // start of its ghosts here + 1 (0: none) and their count
-    const int RL = 66 + 2 * R;
+    // record per rank: 64 handle bytes, ok, nGhost, its GPU's PCI address,
+    // then per sender rank the start of its ghosts here + 1 (0: none) and
+    // their count
+    const int RH = 67, RL = RH + 2 * R;
     std::vector<double> rec((size_t)R * RL, 0.0);
     double* mine = rec.data() + (size_t)me * RL;
     const unsigned char* hb = (const unsigned char*)&h;
@@ -4662,12 +4666,29 @@ static int setupIpc(Router::Impl* d)
     for (size_t i = 0; i < sizeof h; i++) mine[i] = hb[i];
     mine[64] = ok ? 1.0 : 0.0;
     mine[65] = (double)nG;
+    {
+        int dom = 0, bus = 0, dev = 0, ord = 0;
+        (void)hipGetDevice(&ord);
+        (void)hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, ord);
+        (void)hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, ord);
+        (void)hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, ord);
+        (void)hipGetLastError();
+        mine[66] = 1.0 + (double)dom * 65536.0 + (double)bus * 256.0 + (double)dev;
+    }
     for (size_t k = 0; k < part.nbr.size(); k++) {
-        mine[66 + 2 * part.nbr[k]] = part.recvOff[k] + 1.0;
-        mine[67 + 2 * part.nbr[k]] = part.recvOff[k + 1] - part.recvOff[k];
+        mine[RH + 2 * part.nbr[k]] = part.recvOff[k] + 1.0;
+        mine[RH + 1 + 2 * part.nbr[k]] = part.recvOff[k + 1] - part.recvOff[k];
     }
     if (int r = bootReduce(d, rec.data(), (long)rec.size(), 0)) return r;
     for (int r = 0; r < R; r++) ok = ok && rec[(size_t)r * RL + 64] == 1.0;
+    {
+        // every rank on a GPU of its own: the one-launch exchange
+        std::vector<double> key(R);
+        for (int r = 0; r < R; r++) key[r] = rec[(size_t)r * RL + 66];
+        std::sort(key.begin(), key.end());
+        const bool distinct = std::adjacent_find(key.begin(), key.end()) == key.end();
+        d->xchgFused = d->xchgFusedEnv >= 0 ? d->xchgFusedEnv == 1 : distinct;
+    }
     // map the peers' regions
     d->ipcPeer.assign(R, nullptr);
     std::vector<unsigned long long*> base(R, nullptr);
@@ -4693,8 +4714,8 @@ static int setupIpc(Router::Impl* d)
         const int r = part.nbr[k];
         const double* rr = rec.data() + (size_t)r * RL;
         const int ns = part.sendOff[k + 1] - part.sendOff[k];
-        if (ns > 0 && (rr[66 + 2 * me] < 1.0 || (int)rr[67 + 2 * me] != ns)) { ok = false; break; }
-        const int start = ns > 0 ? (int)rr[66 + 2 * me] - 1 : 0;
+        if (ns > 0 && (rr[RH + 2 * me] < 1.0 || (int)rr[RH + 1 + 2 * me] != ns)) { ok = false; break; }
+        const int start = ns > 0 ? (int)rr[RH + 2 * me] - 1 : 0;
         const size_t ngr = (size_t)rr[65];
         xp[k].nGhost = (int)ngr;
         xp[k].ghost = base[r] + fixedW;
@@ -5512,7 +5533,7 @@ int Router::init(Project& prj, int device, const Partition* partIn)
         }
         if (const char* ts = getenv("SWMM5_XCHG_TIMEOUT"))
             if (atof(ts) > 0.0) d->xTimeoutSec = atof(ts);
-        if (const char* xf = getenv("SWMM5_XCHG_FUSED")) d->xchgFused = atoi(xf) != 0;
+        if (const char* xf = getenv("SWMM5_XCHG_FUSED")) d->xchgFusedEnv = atoi(xf) != 0 ? 1 : 0;
         p.xTimeout = (long long)(d->xTimeoutSec * d->wallKHz * 1000.0);
         if (const char* st = getenv("SWMM5_XCHG_STALL")) {     // test hook "rank:step"
             int r = -1;

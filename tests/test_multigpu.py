@@ -536,7 +536,8 @@ def _grid_with_regulators(tmp_path, n=20):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,block,pollutants,transport", [
     (2, 0, 0, "host"), (3, 0, 0, "host"), (2, 90, 0, "host"), (3, 60, 0, "host"), (2, 0, 2, "host"),
-    (2, 0, 0, "ipc"), (3, 60, 0, "ipc"), (2, 0, 2, "ipc"), (3, -1, 0, "ipc"), (3, -2, 0, "ipc")])
+    (2, 0, 0, "ipc"), (3, 60, 0, "ipc"), (2, 0, 2, "ipc"), (3, -1, 0, "ipc"), (3, -2, 0, "ipc"),
+    (2, 0, 2, "ipc_fused"), (3, -2, 0, "ipc_fused")])
 def test_ranks_list_graph_bitwise(world, block, pollutants, transport, tmp_path):
     """The list graph (iterations k >= 2 as unconverged-list walks and
     live-list node passes, each followed by the neighbour exchange and the
@@ -548,7 +549,8 @@ def test_ranks_list_graph_bitwise(world, block, pollutants, transport, tmp_path)
     node weights (contiguous blocks of equal weight, and two regions each cut
     into equal-weight blocks: every rank holds two separate stretches); and
     with two pollutants (the frozen junctions' final depths then come from the
-    quality kernel, after the ghost links' concentrations moved)."""
+    quality kernel, after the ghost links' concentrations moved); the IPC
+    cases also with the one-launch exchange (k_ipc_xchg)."""
     inp = _grid(tmp_path, 30, 30, route_step=5.0, variable_step=0.75, diameter=1.0, q=0.5, pollutants=pollutants)
     env = {"SWMM5_SPARSE": "3", "SWMM5_PART_BLOCK": str(max(block, 0))}
     if block < 0:                         # a weighted partition (node weights 1 .. 4, swmmx_setPartitionWeights)
@@ -558,6 +560,9 @@ def test_ranks_list_graph_bitwise(world, block, pollutants, transport, tmp_path)
     one = _run_workers(inp, 250, tmp_path, 1, "host", "one", extra_env=env)[0]
     st, its, nonconv = one["counters"]
     assert nonconv > 10 and its / st > 2.5, one["counters"]
+    if transport == "ipc_fused":          # the one-launch exchange (chosen when every rank has its own GPU)
+        env["SWMM5_XCHG_FUSED"] = "1"
+        transport = "ipc"
     parts = _run_workers(inp, 250, tmp_path, world, transport, "part", extra_env=env)
     for part in parts:
         assert part["graphs"][1] == part["counters"][0], (part["graphs"], part["counters"])
