@@ -137,7 +137,9 @@ def partition_weights(workload, rows, nx, n_nodes, lam=None):
     ru = np.asarray(rec["row_updates"], dtype=np.float64)
     if "row_conduit_updates" in rec:          # + the conduits' updates, charged to their node1 (their owner)
         ru = ru + np.asarray(rec["row_conduit_updates"], dtype=np.float64)
-    w[:rows * nx] = 1.0 + (rec["lambda"] if lam is None else lam) * np.repeat(ru / nx, nx)
+    if lam is None:                           # an unreliable calibration (no lambda): weigh updates 1:1
+        lam = rec["lambda"] if rec.get("lambda", 0.0) > 0.0 else 1.0
+    w[:rows * nx] = 1.0 + lam * np.repeat(ru / nx, nx)
     return w, rec
 
 
@@ -269,7 +271,8 @@ def main():
     ap.add_argument("--spinup", type=int, default=None)
     ap.add_argument("--q", type=float, default=None, help="override the preset's DWF per junction (cfs)")
     ap.add_argument("--diameter", type=float, default=None, help="override the preset's pipe diameter (ft)")
-    ap.add_argument("--cpu-steps", type=int, default=12)
+    ap.add_argument("--cpu-steps", type=int, default=60, help="routing steps of the CPU port's leg (~6 s on 16 "
+                                                                   "cores, ~15 s on one)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--timing-steps", type=int, default=10)
     ap.add_argument("--kernel-reps", type=int, default=20)
@@ -339,14 +342,14 @@ def main():
         s.set_partition(0, 1, s.nccl_unique_id())
     balance = None
     if world > 1 and args.balance != "off":
-        # auto: two regions -- the surcharged band (nodes that run every
-        # sparse iteration) and the rest, each cut into equal blocks, so
-        # every rank gets an equal share of both (only the per-node work's
-        # shape matters, lambda = 1); weighted: one contiguous block of equal
-        # weight 1 + lambda u per rank
+        # node i weighs 1 + lambda u_i (u: its measured sparse updates per
+        # step, node and conduits; lambda: a sparse update's cost relative to
+        # a full-pass node, both from the calibration record).  auto: two
+        # regions -- the surcharged band, dealt in 2R blocks 0..R-1, R-1..0,
+        # and the rest in R blocks, all of equal weight; weighted: one
+        # contiguous block of equal weight per rank
         n_nodes = rows * cfg["grid"] + 1
-        w, balance = partition_weights(workload_name(args.config, cfg, rows), rows, cfg["grid"], n_nodes,
-                                       lam=1.0 if args.balance == "auto" else None)
+        w, balance = partition_weights(workload_name(args.config, cfg, rows), rows, cfg["grid"], n_nodes)
         if w is not None:
             s.set_partition_weights(w)
             if args.balance == "auto":
@@ -648,8 +651,9 @@ def main():
                            ("blocks of %s nodes dealt to the ranks in turn (SWMM5_PART_BLOCK)"
                             % os.environ["SWMM5_PART_BLOCK"]) if int(os.environ.get("SWMM5_PART_BLOCK", "0")) > 0 else
                            "contiguous row strips of equal node count" if balance is None else
-                           ("two regions, the surcharged band (per-node sparse updates at least half the "
-                            "largest) and the rest, each cut into one equal block per rank (%s)" % balance["source"])
+                           ("two regions of equal weight 1 + %.3f x measured sparse updates per node and step: "
+                            "the surcharged band (weight excess at least a quarter of the largest) in 2R blocks "
+                            "dealt 0..R-1, R-1..0, and the rest in R blocks (%s)" % (balance["lambda"], balance["source"]))
                            if args.balance == "auto" else
                            "contiguous node blocks of equal weight: 1 + %.3f x measured sparse node updates per "
                            "step (%s)" % (balance["lambda"], balance["source"]))},

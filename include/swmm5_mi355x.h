@@ -154,8 +154,8 @@ int    DLLEXPORT swmmx_setPartitionWeights(const double *w, int n);
 
 /* Partition mode (with weights; call like swmmx_setPartitionWeights): 0 one
  * contiguous block of equal weight per rank (the default); 1 two regions --
- * the "hot" nodes (weight excess over the lightest node at least half the
- * largest excess: e.g. the surcharged band whose nodes run every sparse
+ * the "hot" nodes (weight excess over the lightest node at least a quarter of
+ * the largest excess: e.g. the surcharged band whose nodes run every sparse
  * Picard iteration) are cut into 2 nranks contiguous blocks of equal weight
  * dealt to ranks 0, 1, .., nranks-1, nranks-1, .., 0, the other nodes into
  * nranks blocks (rank r takes block r), so every rank gets an equal share of

@@ -65,7 +65,7 @@ int buildPartition(const Network& net, Partition& part, std::string* msg)
             lo = std::min(lo, part.weight[i]);
             hi = std::max(hi, part.weight[i]);
         }
-        const double cut = lo + 0.5 * (hi - lo);
+        const double cut = lo + 0.25 * (hi - lo);
         std::vector<int> hot, cold;
         for (int i = 0; i < nN; i++) (hi > lo && part.weight[i] >= cut ? hot : cold).push_back(i);
         // the hot region in 2R blocks dealt 0, 1, .., R-1, R-1, .., 1, 0: a

@@ -52,7 +52,7 @@ struct Partition {
     std::vector<double> weight;
     // PART_CONTIGUOUS: one contiguous block of equal weight per rank;
     // PART_TWO_REGION (needs weights): the "hot" nodes -- weight excess over
-    // the lightest node at least half the largest excess (the surcharged band
+    // the lightest node at least a quarter of the largest excess (the surcharged band
     // whose nodes run every sparse iteration) -- are cut into 2 nranks
     // contiguous blocks of equal weight dealt 0, 1, .., R-1, R-1, .., 0 (a
     // trend across the band cancels between a rank's two blocks), the other

@@ -163,7 +163,7 @@ def test_weighted_partition_layout(tmp_path):
 
 
 def test_two_region_partition_layout(tmp_path):
-    """swmmx_setPartitionMode(1): the hot nodes (weight excess at least half
+    """swmmx_setPartitionMode(1): the hot nodes (weight excess at least a quarter of
     the largest: here the last four grid rows, a surcharged band) are cut into
     2 x ranks contiguous blocks of equal weight dealt 0, 1, .., 1, 0, the
     others into one block per rank -- every rank owns an equal share of the

@@ -99,8 +99,12 @@ for s in $STEPS; do
     gsweep)for g in ${GFACTORS:-0.34 0.67 2}; do SWMM5_GRID_FACTOR=$g run gsweep_$g 300 python bench.py --no-cpu; done ;;
     nsweep) for g in ${NFACTORS:-1 2 3}; do SWMM5_NODE_GRID_FACTOR=$g run nsweep_$g 300 python bench.py --no-cpu; done ;;
     sweep)  for w in 1 3 4 5; do SWMM5_LINK_WAVES=$w run sweep_w$w 300 python bench.py --steps 200 --no-cpu; done ;;
-    pmc)    run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --no-cpu \
-              && run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --no-cpu ;;
+    pmc)    run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --no-cpu ${BARGS:-} \
+              && run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --no-cpu ${BARGS:-} ;;
+    mrank) # the driver's multi-GPU invocation rehearsed on this one GPU (default config, weak scaling)
+           for n in ${NPS:-2 4}; do
+             GPU_MAX_HW_QUEUES=2 run mrank_$n 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29800 + RANDOM % 100)) bench.py --gpus $n ${BARGS:---steps 20 --warmup 5} --no-cpu
+           done ;;
     pmcskip) # k_step_end byte attribution: FETCH/WRITE passes per SWMM5_STEPEND_SKIP mask
            for m in ${SKIPS:-0 1 2 4 8 16 32 64}; do
              SWMM5_STEPEND_SKIP=$m run pmcskip_f_$m 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcskip_f_$m -o run -- python3 bench.py --no-cpu --steps 30 --warmup 5 --timing-steps 2 --kernel-reps 0 \
