@@ -634,8 +634,8 @@ def main():
                        "step_graphs": {g: c1["steps_" + g] - c0["steps_" + g]
                                        for g in ("unrolled", "tail", "sparse", "list")},
                        "sim_time_at_end_s": round(t_days * 86400.0, 1),
-                       "parallelism": ("link-partitioned x%d (row strips); per Picard iteration "
-                                       "%s of the strip neighbours' ghost-link values and an "
+                       "parallelism": ("link-partitioned x%d (node blocks: see partition); per Picard iteration "
+                                       "%s of the neighbours' ghost-link values and an "
                                        "all-reduce(max) of the convergence flag"
                                        % (world, {"ipc": "device stores into the peers' memory (IPC)",
                                                   "rccl": "RCCL ncclSend/ncclRecv"}.get(
