@@ -103,7 +103,7 @@ for s in $STEPS; do
               && run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --no-cpu ${BARGS:-} ;;
     mrank) # the driver's multi-GPU invocation rehearsed on this one GPU (default config, weak scaling)
            for n in ${NPS:-2 4}; do
-             GPU_MAX_HW_QUEUES=2 run mrank_$n 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29800 + RANDOM % 100)) bench.py --gpus $n ${BARGS:---steps 20 --warmup 5} --no-cpu
+             GPU_MAX_HW_QUEUES=${HWQ:-2} run mrank_$n 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29800 + RANDOM % 100)) bench.py --gpus $n ${BARGS:---steps 20 --warmup 5} --no-cpu
            done ;;
     pmcskip) # k_step_end byte attribution: FETCH/WRITE passes per SWMM5_STEPEND_SKIP mask
            for m in ${SKIPS:-0 1 2 4 8 16 32 64}; do
