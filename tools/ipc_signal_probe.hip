@@ -10,6 +10,8 @@
 //   flag : work, work, flag           (the convergence-flag exchange alone)
 //   split: work, post, wait, work, flag   (the engine's k_ipc_pack / k_ipc_unpack / k_ipc_flag)
 //   fused: work, xchg, work, flag     (pack and unpack in one launch)
+//   fold : work, xchg, work+flag      (the flag posted and awaited by the
+//                                      node pass's last workgroup)
 // The cost of the signalling is (variant - base) / N per iteration.
 //
 //   thread mode (default, `ipc_signal_probe thread G`): one process, the two ranks on two HIP streams of
@@ -89,9 +91,28 @@ __global__ void k_flag(Side s, int G)
     }
 }
 __global__ void k_bump(Side s) { if (threadIdx.x == 0) s.ctl[0] += 1; }
+// the node pass with the flag folded in: every workgroup does its work; the
+// last one to finish (a device-scope arrival count) posts the flag and waits
+// for the peer's -- one waiting workgroup, no launch of its own
+__global__ void k_work_flag(Side s, int G)
+{
+    __shared__ int last;
+    if (threadIdx.x == 0) s.work[blockIdx.x] += 1;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(&s.ctl[2], 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last || threadIdx.x != 0) return;
+    s.ctl[2] = 0;
+    const unsigned seq = s.ctl[0] + 1;
+    st(s.peer + G, seq, 1u);
+    if (waitSeq(s.mine + G, seq, s.ctl)) s.ctl[0] = seq;
+}
 
-enum { V_BASE, V_FLAG, V_SPLIT, V_FUSED, V_COUNT };
-static const char* kName[V_COUNT] = {"base", "flag", "split", "fused"};
+enum { V_BASE, V_FLAG, V_SPLIT, V_FUSED, V_FOLD, V_COUNT };
+static const char* kName[V_COUNT] = {"base", "flag", "split", "fused", "fold"};
 
 static hipGraphExec_t capture(hipStream_t st, const Side& s, int v, int N, int G, int grid)
 {
@@ -103,8 +124,12 @@ static hipGraphExec_t capture(hipStream_t st, const Side& s, int v, int N, int G
         if (v == V_SPLIT) {
             hipLaunchKernelGGL(k_post, dim3(grid), dim3(kBlock), 0, st, s, G);
             hipLaunchKernelGGL(k_wait, dim3(grid), dim3(kBlock), 0, st, s, G);
-        } else if (v == V_FUSED) {
+        } else if (v == V_FUSED || v == V_FOLD) {
             hipLaunchKernelGGL(k_xchg, dim3(grid), dim3(kBlock), 0, st, s, G);
+        }
+        if (v == V_FOLD) {
+            hipLaunchKernelGGL(k_work_flag, dim3(grid), dim3(kBlock), 0, st, s, G);
+            continue;
         }
         hipLaunchKernelGGL(k_work, dim3(grid), dim3(kBlock), 0, st, s);
         if (v == V_BASE) hipLaunchKernelGGL(k_bump, dim3(1), dim3(64), 0, st, s);
@@ -198,7 +223,7 @@ int main(int argc, char** argv)
     CK(hipDeviceSynchronize());
     printf("mode %s%s: %d iterations per graph, %d ghost granules per rank per exchange, grid %d x %d\n",
            proc ? "proc rank " : "thread", proc ? std::to_string(rank).c_str() : "", N, G, grid, kBlock);
-    double us[V_COUNT] = {0, 0, 0, 0};
+    double us[V_COUNT] = {0, 0, 0, 0, 0};
     int barrierNo = 0;
     for (int v = 0; v < V_COUNT; v++) {
         hipGraphExec_t x[2];
