@@ -1049,6 +1049,11 @@ __device__ __forceinline__ void stageTables(double* ct, const double* g, int nGe
 // after convergence.
 __device__ __forceinline__ void finalizeFrozen(const Params& p, int m, int tid, int nthr)
 {
+    // a node frozen at iteration k >= 1 carries frz = k + 1 >= 2, and
+    // frozenDepth advances it over iterations frz - 1 .. m - 1: after a step
+    // that converged at iteration m <= 1 no depth moves, and the flags are
+    // reset by the next step's iteration-0 node pass (nodePass<true>)
+    if (m <= 1) return;
     for (int i = tid; i < p.nN; i += nthr) {
         const int fz = p.frz[i];
         if (fz) {
@@ -1983,6 +1988,9 @@ __device__ __forceinline__ void nodePass(const Params& p, int k, int tid, int nt
         // so a thread's nodes cost one load latency, not one each
         const NodePre preNext = loadNodePre(p, i + nthr, k);
         bool alive = true;
+        // a step starts with no frozen node: the flags a step that converged
+        // at iteration 1 left (finalizeFrozen) are cleared here
+        if (kFirst && p.freeze) p.frz[i] = 0;
         nodeItem<kFirst, kGeneral>(p, k, i, dt, pre, listMe, row, anyUnconv, gathered, live, fast, alive);
         // list this iteration's unconverged nodes for the next k_link
         if (!kFirst) sinkAppend(su, listMe, i, row);
@@ -2575,6 +2583,7 @@ __global__ __launch_bounds__(kBlock) void k_unfreeze(Params p)
     if (!p.freeze) return;
     bool converged;
     const int m = stepIterations(p, &converged) - 1;
+    if (m <= 1) return;                               // nothing advances (finalizeFrozen)
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < p.nN; i += gridDim.x * kBlock) {
         const int fz = p.frz[i];
         if (fz) {
