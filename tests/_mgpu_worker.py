@@ -42,11 +42,14 @@ def main():
 
         s.set_partition(rank, world)
         s.set_exchange(xchg)
-        if os.environ.get("WORKER_WEIGHTS") == "ramp":   # a weighted partition: later nodes weigh up to 4x
+        ww = os.environ.get("WORKER_WEIGHTS", "")
+        if ww == "ramp":                 # a weighted partition: later nodes weigh up to 4x
             nN = int(os.environ["WORKER_NODES"])
             s.set_partition_weights(np.linspace(1.0, 4.0, nN))
-            if os.environ.get("WORKER_PARTMODE"):      # e.g. two_region: the heavier half dealt separately
-                s.set_partition_mode(os.environ["WORKER_PARTMODE"])
+        elif ww.startswith("file:"):     # weights saved by the test (e.g. bench.py's calibrated ones)
+            s.set_partition_weights(np.load(ww[5:]))
+        if ww and os.environ.get("WORKER_PARTMODE"):   # e.g. two_region: the band and the rest dealt separately
+            s.set_partition_mode(os.environ["WORKER_PARTMODE"])
         if transport == "ipc":          # device stores into the peers' memory; gloo bootstraps it
             s.set_transport("ipc")
     else:

@@ -712,7 +712,8 @@ def test_two_ranks_match_one_gpu_4m(tmp_path):
     ranks on this box's GPU) against one GPU, in the benchmark's regime.  One
     GPU spins the network up for 2000 s and saves a hot start file; both runs
     restart from it for 15 steps, which surcharge and do not all converge;
-    the two strips are bitwise equal to one GPU."""
+    the two strips (host and IPC transports) and bench.py's default
+    two-region partition (IPC) are bitwise equal to one GPU."""
     sys.path.insert(0, os.path.dirname(HERE))
     import bench
     cfg = bench.PRESETS["4m"]
@@ -735,4 +736,15 @@ def test_two_ranks_match_one_gpu_4m(tmp_path):
     for transport in ("host", "ipc"):
         parts = _run_workers(inp, steps, tmp_path, 2, transport, "two_" + transport)
         assert all(_transport_of(p) == transport for p in parts)
+        _assert_bitwise(parts, one)
+    # bench.py's default partition with two ranks: two regions from the
+    # calibration record (profiles/partition_weights.json), over IPC
+    w, rec = bench.partition_weights(bench.workload_name("4m", cfg, n), n, n, n * n + 1)
+    if w is not None:
+        wpath = str(tmp_path / "w4m.npy")
+        np.save(wpath, w)
+        env = {"WORKER_WEIGHTS": "file:" + wpath, "WORKER_PARTMODE": "two_region"}
+        parts = _run_workers(inp, steps, tmp_path, 2, "ipc", "two_region", extra_env=env)
+        owner = parts[0]["node_owner"]
+        assert (owner[n * (n - 20):n * n] == 0).any() and (owner[n * (n - 20):n * n] == 1).any()
         _assert_bitwise(parts, one)
